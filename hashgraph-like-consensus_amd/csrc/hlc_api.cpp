@@ -1,0 +1,457 @@
+// hlc_api.cpp -- the C ABI of include/hlc.h: context, device workspace, host<->device staging,
+// and the orchestration of the kernels in hlc_prehash.hip / hlc_recover.hip.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hlc.h"
+#include "hlc_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                                 \
+  do {                                                                                               \
+    hipError_t e_ = (expr);                                                                          \
+    if (e_ != hipSuccess)                                                                            \
+      return set_err(e_ == hipErrorOutOfMemory ? HLC_ENOMEM : HLC_EDEVICE,                           \
+                     std::string(#expr) + ": " + hipGetErrorString(e_));                             \
+  } while (0)
+
+#define CHK(expr)            \
+  do {                       \
+    int rc_ = (expr);        \
+    if (rc_ != 0) return rc_; \
+  } while (0)
+
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = bytes + bytes / 4 + 256;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return set_err(HLC_ENOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    }
+    cap = want;
+    return 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+}  // namespace
+
+struct hlc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DBuf gtab, fbtab, rec_scratch;
+  uint64_t rec_lanes = 0;
+  // staged host inputs (host-buffer entry points)
+  DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
+  DBuf in_off2, in_len2, in_off3, in_len3, in_priv;
+  // outputs staged on device
+  DBuf out_res, out_status, out_reason, out_rec, out_misc;
+  // internal workspace
+  DBuf vote_prop, sha_sz, sha_off, kec_sz, kec_off, sha_buf, kec_buf, sha_dig, kec_dig, pre, pre_reason,
+      verify, status, reason, chain_code, chain_tab, dup_tab, red, scan_tmp, totals;
+};
+
+namespace {
+
+int activate(hlc_ctx* ctx) {
+  HIPCHK(hipSetDevice(ctx->device));
+  return 0;
+}
+
+template <class T>
+int upload(DBuf& b, const T* host, size_t count, hipStream_t s) {
+  CHK(b.ensure(count * sizeof(T) + 16));
+  if (count) HIPCHK(hipMemcpyAsync(b.p, host, count * sizeof(T), hipMemcpyHostToDevice, s));
+  return 0;
+}
+
+// Prefix sums of message sizes + device->host read of the totals (one sync).
+int scan_sizes(hlc_ctx* c, uint64_t n, const uint64_t* sz, uint64_t* off, uint64_t* total, hipStream_t s) {
+  size_t tb = 0;
+  hlc::launch_exclusive_scan(sz, off, n, nullptr, tb, s);
+  CHK(c->scan_tmp.ensure(tb + 16));
+  hlc::launch_exclusive_scan(sz, off, n, c->scan_tmp.p, tb, s);
+  HIPCHK(hipGetLastError());
+  CHK(c->totals.ensure(4 * sizeof(uint64_t)));
+  uint64_t* t = c->totals.as<uint64_t>();
+  HIPCHK(hipMemcpyAsync(t, off + (n - 1), sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemcpyAsync(t + 1, sz + (n - 1), sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+  uint64_t h[2];
+  HIPCHK(hipMemcpyAsync(h, t, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *total = h[0] + h[1];
+  return 0;
+}
+
+// Builds + hashes the vote messages: sha_dig (vote hash) and kec_dig (EIP-191 prehash).
+int run_prehash(hlc_ctx* c, const hlc_votes* dv, uint64_t n, int mode, const uint8_t* bytes,
+                const uint64_t* pay_off, const uint32_t* pay_len, hipStream_t s) {
+  CHK(c->sha_sz.ensure(n * 8));
+  CHK(c->sha_off.ensure(n * 8));
+  CHK(c->kec_sz.ensure(n * 8));
+  CHK(c->kec_off.ensure(n * 8));
+  hlc::launch_msg_sizes(dv, n, pay_off, pay_len, mode, c->sha_sz.as<uint64_t>(), c->kec_sz.as<uint64_t>(), s);
+  uint64_t sha_total = 0, kec_total = 0;
+  if (mode == hlc::MSG_VOTE) CHK(scan_sizes(c, n, c->sha_sz.as<uint64_t>(), c->sha_off.as<uint64_t>(), &sha_total, s));
+  CHK(scan_sizes(c, n, c->kec_sz.as<uint64_t>(), c->kec_off.as<uint64_t>(), &kec_total, s));
+  CHK(c->sha_buf.ensure(sha_total + 64));
+  CHK(c->kec_buf.ensure(kec_total + 136));
+  CHK(c->sha_dig.ensure(n * 32));
+  CHK(c->kec_dig.ensure(n * 32));
+  hlc::launch_build_msgs(dv, n, bytes, pay_off, pay_len, mode, c->sha_off.as<uint64_t>(), c->sha_sz.as<uint64_t>(),
+                         c->sha_buf.as<uint8_t>(), c->kec_off.as<uint64_t>(), c->kec_sz.as<uint64_t>(),
+                         c->kec_buf.as<uint8_t>(), s);
+  if (mode == hlc::MSG_VOTE)
+    hlc::launch_sha_blocks(n, c->sha_off.as<uint64_t>(), c->sha_sz.as<uint64_t>(), c->sha_buf.as<uint8_t>(),
+                           c->sha_dig.as<uint32_t>(), s);
+  hlc::launch_keccak_blocks(n, c->kec_off.as<uint64_t>(), c->kec_sz.as<uint64_t>(), c->kec_buf.as<uint8_t>(),
+                            c->kec_dig.as<uint32_t>(), s);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ensure_recover_scratch(hlc_ctx* c) {
+  if (c->rec_lanes) return 0;
+  uint64_t lanes = hlc::recover_grid_lanes();
+  CHK(c->rec_scratch.ensure(lanes * (uint64_t)(8 * 24 + 4 * 33) * sizeof(uint32_t)));
+  c->rec_lanes = lanes;
+  return 0;
+}
+
+int ensure_fbtab(hlc_ctx* c) {
+  if (c->fbtab.p) return 0;
+  CHK(c->fbtab.ensure(hlc::FBTAB_WORDS * sizeof(uint32_t)));
+  hlc::launch_build_fbtab(c->fbtab.as<uint32_t>(), c->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// Device-resident validate-many (every pointer is device memory).
+int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops, uint64_t np, uint64_t now,
+                    hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s) {
+  const uint64_t n = dv->n;
+  if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
+  CHK(c->vote_prop.ensure(n * 4 + 4));
+  hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, s);
+  uint8_t* status = dstatus;
+  uint8_t* reason = dreason;
+  if (!status) {
+    CHK(c->status.ensure(n + 1));
+    status = c->status.as<uint8_t>();
+  }
+  if (!reason) {
+    CHK(c->reason.ensure(n + 1));
+    reason = c->reason.as<uint8_t>();
+  }
+  if (n) {
+    CHK(run_prehash(c, dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
+    CHK(c->pre.ensure(n));
+    CHK(c->pre_reason.ensure(n));
+    CHK(c->verify.ensure(n));
+    hlc::launch_pre_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->sha_dig.as<uint32_t>(),
+                           c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
+    CHK(ensure_recover_scratch(c));
+    if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
+    hlc::launch_recover(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
+                        dv->field_off + HLC_F_SIGNATURE, dv->field_off + HLC_F_OWNER, HLC_NFIELDS,
+                        c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(), c->rec_lanes,
+                        c->verify.as<uint8_t>(), drec, s);
+    hlc::launch_vote_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, now, c->pre.as<uint8_t>(),
+                            c->pre_reason.as<uint8_t>(), c->verify.as<uint8_t>(), status, reason, s);
+  }
+  uint64_t cap = 64;
+  while (cap < 2 * n) cap <<= 1;
+  CHK(c->chain_tab.ensure(cap * 4));
+  CHK(c->dup_tab.ensure(cap * 4));
+  CHK(c->chain_code.ensure(n + 1));
+  CHK(c->red.ensure(np * 16 + 16));
+  hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
+                     c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), s);
+  hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
+                          c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
+                          c->red.as<uint32_t>(), np, s);
+  hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int check_votes_host(const hlc_votes* v) {
+  if (!v) return set_err(HLC_EINVAL, "votes is NULL");
+  if (v->n && (!v->vote_id || !v->proposal_id || !v->timestamp || !v->vote || !v->field_off || !v->field_len))
+    return set_err(HLC_EINVAL, "NULL vote array");
+  for (uint64_t i = 0; i < v->n * HLC_NFIELDS; ++i) {
+    if (v->field_len[i] && (!v->bytes || v->field_off[i] + v->field_len[i] > v->bytes_len ||
+                            v->field_off[i] + v->field_len[i] < v->field_off[i]))
+      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+  }
+  return 0;
+}
+
+// Stage host votes on the device; returns a device-pointer view in *dv.
+int stage_votes(hlc_ctx* c, const hlc_votes* v, hlc_votes* dv, hipStream_t s) {
+  const uint64_t n = v->n;
+  CHK(upload(c->in_vote_id, v->vote_id, n, s));
+  CHK(upload(c->in_pid, v->proposal_id, n, s));
+  CHK(upload(c->in_ts, v->timestamp, n, s));
+  CHK(upload(c->in_vote, v->vote, n, s));
+  CHK(upload(c->in_off, v->field_off, n * HLC_NFIELDS, s));
+  CHK(upload(c->in_len, v->field_len, n * HLC_NFIELDS, s));
+  CHK(upload(c->in_bytes, v->bytes, v->bytes ? v->bytes_len : 0, s));
+  dv->n = n;
+  dv->vote_id = c->in_vote_id.as<uint32_t>();
+  dv->proposal_id = c->in_pid.as<uint32_t>();
+  dv->timestamp = c->in_ts.as<uint64_t>();
+  dv->vote = c->in_vote.as<uint8_t>();
+  dv->field_off = c->in_off.as<uint64_t>();
+  dv->field_len = c->in_len.as<uint32_t>();
+  dv->bytes = c->in_bytes.as<uint8_t>();
+  dv->bytes_len = v->bytes_len;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* hlc_last_error(void) { return g_err.c_str(); }
+
+int hlc_abi_version(void) { return HLC_ABI_VERSION; }
+
+int hlc_ctx_create(int device, hlc_ctx** out) {
+  if (!out) return set_err(HLC_EINVAL, "out is NULL");
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0)
+    return set_err(HLC_ENODEV, "no HIP device with that ordinal");
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(HLC_ENODEV, std::string("libhlc is built for gfx950, device is ") + prop.gcnArchName);
+  hlc_ctx* c = new hlc_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return set_err(HLC_EDEVICE, "stream creation failed");
+  }
+  if (c->gtab.ensure(hlc::GTAB_WORDS * sizeof(uint32_t)) != 0) {
+    delete c;
+    return HLC_ENOMEM;
+  }
+  hlc::launch_build_gtab(c->gtab.as<uint32_t>(), c->stream);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) {
+    delete c;
+    return set_err(HLC_EDEVICE, "generator table construction failed");
+  }
+  *out = c;
+  return 0;
+}
+
+void hlc_ctx_destroy(hlc_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  hipStream_t s = ctx->stream;
+  delete ctx;
+  if (s) (void)hipStreamDestroy(s);
+}
+
+int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, uint64_t max_bytes) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  const uint64_t n = max_votes;
+  CHK(ensure_recover_scratch(ctx));
+  for (DBuf* b : {&ctx->sha_sz, &ctx->sha_off, &ctx->kec_sz, &ctx->kec_off}) CHK(b->ensure(n * 8));
+  for (DBuf* b : {&ctx->sha_dig, &ctx->kec_dig}) CHK(b->ensure(n * 32));
+  for (DBuf* b : {&ctx->pre, &ctx->pre_reason, &ctx->verify, &ctx->status, &ctx->reason, &ctx->chain_code})
+    CHK(b->ensure(n + 1));
+  CHK(ctx->vote_prop.ensure(n * 4 + 4));
+  CHK(ctx->sha_buf.ensure(n * 128 + max_bytes + 64));
+  CHK(ctx->kec_buf.ensure(n * 272 + max_bytes + 136));
+  uint64_t cap = 64;
+  while (cap < 2 * n) cap <<= 1;
+  CHK(ctx->chain_tab.ensure(cap * 4));
+  CHK(ctx->dup_tab.ensure(cap * 4));
+  CHK(ctx->red.ensure(max_proposals * 16 + 16));
+  return 0;
+}
+
+int hlc_validate_proposals_device(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,
+                                  uint64_t n_proposals, uint64_t now, hlc_result* out_results,
+                                  uint8_t* out_vote_status, uint8_t* out_vote_reason, uint8_t* out_recovered,
+                                  void* stream) {
+  if (!ctx || !votes || (n_proposals && (!proposals || !out_results)))
+    return set_err(HLC_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  return validate_device(ctx, votes, proposals, n_proposals, now, out_results, out_vote_status, out_vote_reason,
+                         out_recovered, s);
+}
+
+int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,
+                           uint64_t n_proposals, uint64_t now, hlc_result* out_results, uint8_t* out_vote_status,
+                           uint8_t* out_vote_reason, uint8_t* out_recovered) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  CHK(check_votes_host(votes));
+  if (n_proposals && (!proposals || !out_results)) return set_err(HLC_EINVAL, "NULL proposals/results");
+  for (uint64_t p = 0; p < n_proposals; ++p) {
+    if (proposals[p].vote_begin + proposals[p].vote_count > votes->n)
+      return set_err(HLC_EINVAL, "proposal vote range outside the vote batch");
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  const uint64_t n = votes->n;
+  hlc_votes dv;
+  CHK(stage_votes(ctx, votes, &dv, s));
+  CHK(upload(ctx->in_props, proposals, n_proposals, s));
+  CHK(ctx->out_res.ensure(n_proposals * sizeof(hlc_result) + 16));
+  CHK(ctx->out_status.ensure(n + 1));
+  CHK(ctx->out_reason.ensure(n + 1));
+  if (out_recovered) CHK(ctx->out_rec.ensure(n * 20 + 20));
+  CHK(validate_device(ctx, &dv, ctx->in_props.as<hlc_proposal>(), n_proposals, now, ctx->out_res.as<hlc_result>(),
+                      ctx->out_status.as<uint8_t>(), ctx->out_reason.as<uint8_t>(),
+                      out_recovered ? ctx->out_rec.as<uint8_t>() : nullptr, s));
+  if (n_proposals)
+    HIPCHK(hipMemcpyAsync(out_results, ctx->out_res.p, n_proposals * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
+  if (out_vote_status && n) HIPCHK(hipMemcpyAsync(out_vote_status, ctx->out_status.p, n, hipMemcpyDeviceToHost, s));
+  if (out_vote_reason && n) HIPCHK(hipMemcpyAsync(out_vote_reason, ctx->out_reason.p, n, hipMemcpyDeviceToHost, s));
+  if (out_recovered && n) HIPCHK(hipMemcpyAsync(out_recovered, ctx->out_rec.p, n * 20, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hlc_compute_vote_hashes(hlc_ctx* ctx, const hlc_votes* votes, uint8_t* out_hash32) {
+  if (!ctx || !out_hash32) return set_err(HLC_EINVAL, "NULL argument");
+  CHK(check_votes_host(votes));
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  const uint64_t n = votes->n;
+  if (!n) return 0;
+  hlc_votes dv;
+  CHK(stage_votes(ctx, votes, &dv, s));
+  CHK(run_prehash(ctx, &dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
+  HIPCHK(hipMemcpyAsync(out_hash32, ctx->sha_dig.p, n * 32, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_t bytes_len, const uint64_t* id_off,
+                         const uint32_t* id_len, const uint64_t* payload_off, const uint32_t* payload_len,
+                         const uint64_t* sig_off, const uint32_t* sig_len, uint8_t* out_status, uint8_t* out_addr) {
+  if (!ctx || (n && (!id_off || !id_len || !payload_off || !payload_len || !sig_off || !sig_len || !out_status)))
+    return set_err(HLC_EINVAL, "NULL argument");
+  for (uint64_t i = 0; i < n; ++i) {
+    if (id_off[i] + id_len[i] > bytes_len || payload_off[i] + payload_len[i] > bytes_len ||
+        sig_off[i] + sig_len[i] > bytes_len)
+      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
+  }
+  if (!n) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  CHK(upload(ctx->in_bytes, bytes, bytes_len, s));
+  CHK(upload(ctx->in_off, id_off, n, s));
+  CHK(upload(ctx->in_len, id_len, n, s));
+  CHK(upload(ctx->in_off2, payload_off, n, s));
+  CHK(upload(ctx->in_len2, payload_len, n, s));
+  CHK(upload(ctx->in_off3, sig_off, n, s));
+  CHK(upload(ctx->in_len3, sig_len, n, s));
+  const uint8_t* dbytes = ctx->in_bytes.as<uint8_t>();
+  CHK(run_prehash(ctx, nullptr, n, hlc::MSG_PAYLOAD, dbytes, ctx->in_off2.as<uint64_t>(), ctx->in_len2.as<uint32_t>(), s));
+  CHK(ctx->pre.ensure(n));
+  CHK(ctx->verify.ensure(n));
+  hlc::launch_verify_pre(n, ctx->in_len3.as<uint32_t>(), ctx->in_len.as<uint32_t>(), ctx->pre.as<uint8_t>(),
+                         ctx->verify.as<uint8_t>(), s);
+  CHK(ensure_recover_scratch(ctx));
+  uint8_t* drec = nullptr;
+  if (out_addr) {
+    CHK(ctx->out_rec.ensure(n * 20 + 20));
+    drec = ctx->out_rec.as<uint8_t>();
+    HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
+  }
+  hlc::launch_recover(n, ctx->pre.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), dbytes, ctx->in_off3.as<uint64_t>(),
+                      ctx->in_off.as<uint64_t>(), 1, ctx->gtab.as<uint32_t>(), ctx->rec_scratch.as<uint32_t>(),
+                      ctx->rec_lanes, ctx->verify.as<uint8_t>(), drec, s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out_status, ctx->verify.p, n, hipMemcpyDeviceToHost, s));
+  if (out_addr) HIPCHK(hipMemcpyAsync(out_addr, drec, n * 20, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hlc_eth_address_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, uint8_t* out_addr20) {
+  if (!ctx || (n && (!priv32 || !out_addr20))) return set_err(HLC_EINVAL, "NULL argument");
+  if (!n) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  CHK(ensure_fbtab(ctx));
+  CHK(upload(ctx->in_priv, priv32, n * 32, s));
+  CHK(ctx->out_rec.ensure(n * 20 + 20));
+  hlc::launch_address(n, ctx->in_priv.as<uint8_t>(), ctx->fbtab.as<uint32_t>(), ctx->out_rec.as<uint8_t>(), s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out_addr20, ctx->out_rec.p, n * 20, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hlc_eth_sign_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, const uint8_t* bytes, uint64_t bytes_len,
+                       const uint64_t* payload_off, const uint32_t* payload_len, uint8_t* out_sig65) {
+  if (!ctx || (n && (!priv32 || !payload_off || !payload_len || !out_sig65)))
+    return set_err(HLC_EINVAL, "NULL argument");
+  for (uint64_t i = 0; i < n; ++i)
+    if (payload_off[i] + payload_len[i] > bytes_len) return set_err(HLC_EINVAL, "payload outside the byte arena");
+  if (!n) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  CHK(ensure_fbtab(ctx));
+  CHK(upload(ctx->in_bytes, bytes, bytes_len, s));
+  CHK(upload(ctx->in_off2, payload_off, n, s));
+  CHK(upload(ctx->in_len2, payload_len, n, s));
+  CHK(upload(ctx->in_priv, priv32, n * 32, s));
+  CHK(run_prehash(ctx, nullptr, n, hlc::MSG_PAYLOAD, ctx->in_bytes.as<uint8_t>(), ctx->in_off2.as<uint64_t>(),
+                  ctx->in_len2.as<uint32_t>(), s));
+  CHK(ctx->out_misc.ensure(n * 65 + 65));
+  hlc::launch_sign(n, ctx->in_priv.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), ctx->fbtab.as<uint32_t>(),
+                   ctx->out_misc.as<uint8_t>(), s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out_sig65, ctx->out_misc.p, n * 65, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+}  // extern "C"

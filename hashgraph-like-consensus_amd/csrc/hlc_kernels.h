@@ -1,0 +1,76 @@
+// hlc_kernels.h -- host-side launchers of the HIP kernels (internal to libhlc.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/hlc.h"
+
+namespace hlc {
+
+constexpr uint32_t NO_PROP = 0xFFFFFFFFu;
+constexpr uint32_t EMPTY_SLOT = 0xFFFFFFFFu;
+// pre_status values beyond the public HLC_* codes
+constexpr uint8_t PRE_PENDING = 0xFE;  // needs signature recovery
+constexpr uint8_t PRE_SKIP = 0xFF;     // vote not covered by any proposal
+
+// message-building modes
+enum MsgMode { MSG_VOTE = 0, MSG_PAYLOAD = 1 };
+
+struct Workspace;  // defined in hlc_api.cpp
+
+// ---- prehash stage ----
+void launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv,
+                         hipStream_t s);
+void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
+                      int mode, uint64_t* sha_sz, uint64_t* kec_sz, hipStream_t s);
+void launch_build_msgs(const hlc_votes* v, uint64_t n, const uint8_t* bytes, const uint64_t* pay_off,
+                       const uint32_t* pay_len, int mode, const uint64_t* sha_off, const uint64_t* sha_sz,
+                       uint8_t* sha_buf, const uint64_t* kec_off, const uint64_t* kec_sz, uint8_t* kec_buf,
+                       hipStream_t s);
+void launch_sha_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, const uint8_t* buf,
+                       uint32_t* out_digest_words, hipStream_t s);
+void launch_keccak_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, const uint8_t* buf,
+                          uint32_t* out_digest_words, hipStream_t s);
+// exclusive prefix sum of u64 sizes (hipcub); temp == nullptr queries temp_bytes
+void launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
+                           hipStream_t s);
+// hlc_eth_verify_batch length checks (ethereum.rs:71-82): pre[i] = PRE_PENDING or verify_out set
+void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
+                       uint8_t* verify_out, hipStream_t s);
+void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                       const uint32_t* sha_digest, uint8_t* pre, uint8_t* pre_reason, hipStream_t s);
+
+// ---- recovery ----
+// items: i in [0, n) with pre[i] == PRE_PENDING; signature bytes / identity bytes read from
+// bytes + sig_off[i*stride_f] etc.  verify_out[i]: HLC_VERIFY_TRUE/FALSE or 1+SCHEME.
+void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
+                    const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride,
+                    const uint32_t* gtab, uint32_t* scratch, uint64_t scratch_lanes,
+                    uint8_t* verify_out, uint8_t* addr_out, hipStream_t s);
+uint64_t recover_grid_lanes();
+void launch_build_gtab(uint32_t* gtab, hipStream_t s);
+
+// ---- validation tail ----
+void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                        uint64_t now, const uint8_t* pre, const uint8_t* pre_reason, const uint8_t* verify,
+                        uint8_t* status, uint8_t* reason, hipStream_t s);
+void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, hipStream_t s);
+void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                        const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
+                        uint32_t mask, uint8_t* chain_code, uint32_t* red, uint64_t np, hipStream_t s);
+void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
+                     const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red,
+                     hlc_result* out, hipStream_t s);
+
+// ---- signing ----
+void launch_build_fbtab(uint32_t* fbtab, hipStream_t s);
+void launch_address(uint64_t n, const uint8_t* priv, const uint32_t* fbtab, uint8_t* addr, hipStream_t s);
+void launch_sign(uint64_t n, const uint8_t* priv, const uint32_t* z_digest, const uint32_t* fbtab,
+                 uint8_t* sig, hipStream_t s);
+
+constexpr size_t GTAB_WORDS = 2 * 64 * 16;      // odd multiples of G and lambda*G, affine
+constexpr size_t FBTAB_WORDS = 32 * 256 * 16;   // fixed-base comb: 32 windows x 256 affine points
+
+}  // namespace hlc

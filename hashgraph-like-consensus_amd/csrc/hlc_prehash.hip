@@ -1,0 +1,574 @@
+// hlc_prehash.hip -- byte-level stages of the validate-many path (one lane per vote):
+//   * proposal assignment, message sizing, message materialisation (SHA-256 input of
+//     compute_vote_hash, utils.rs:37-47; EIP-191 framing of the prost-encoded Vote with the
+//     signature cleared, utils.rs:150-152 + alloy eip191_hash_message),
+//   * SHA-256 / keccak-256 over the materialised, padded messages,
+//   * per-vote status assembly (validate_proposal loop body, utils.rs:112-117, 127-171),
+//   * chain-link (utils.rs:175-215) and duplicate-owner (session.rs:270-275) hash tables,
+//   * per-proposal reduction and the initialize_with_votes tail (session.rs:253-298).
+// All integer/byte work: HBM/L2-bound and tiny next to recovery.
+#include <hipcub/hipcub.hpp>
+
+#include "hlc_hash.hpp"
+#include "hlc_kernels.h"
+
+namespace hlc {
+
+namespace {
+
+constexpr int TPB = 256;
+
+__device__ __forceinline__ uint32_t flen(const hlc_votes& v, uint64_t i, int f) {
+  return v.field_len[i * HLC_NFIELDS + f];
+}
+__device__ __forceinline__ const uint8_t* fptr(const hlc_votes& v, uint64_t i, int f) {
+  return v.bytes + v.field_off[i * HLC_NFIELDS + f];
+}
+
+__device__ __forceinline__ uint32_t varint_len(uint64_t x) {
+  uint32_t n = 1;
+  while (x >= 0x80) {
+    x >>= 7;
+    ++n;
+  }
+  return n;
+}
+__device__ __forceinline__ uint32_t dec_digits(uint64_t x) {
+  uint32_t n = 1;
+  while (x >= 10) {
+    x /= 10;
+    ++n;
+  }
+  return n;
+}
+
+// prost encoded length of Vote with signature cleared (consensus.proto:19-29)
+__device__ uint64_t vote_enc_len(const hlc_votes& v, uint64_t i) {
+  uint64_t n = 0;
+  uint32_t id = v.vote_id[i], pid = v.proposal_id[i];
+  uint64_t ts = v.timestamp[i];
+  if (id) n += 2 + varint_len(id);
+  uint32_t lo = flen(v, i, HLC_F_OWNER);
+  if (lo) n += 2 + varint_len(lo) + lo;
+  if (pid) n += 2 + varint_len(pid);
+  if (ts) n += 2 + varint_len(ts);
+  if (v.vote[i]) n += 3;
+  for (int f = HLC_F_PARENT; f <= HLC_F_VOTE_HASH; ++f) {
+    uint32_t l = flen(v, i, f);
+    if (l) n += 2 + varint_len(l) + l;
+  }
+  return n;
+}
+
+__global__ void k_assign_props(const hlc_proposal* props, uint32_t* vote_prop) {
+  const uint32_t p = blockIdx.x;
+  const hlc_proposal d = props[p];
+  for (uint64_t j = threadIdx.x; j < d.vote_count; j += blockDim.x) vote_prop[d.vote_begin + j] = p;
+}
+
+__global__ void k_msg_sizes(hlc_votes v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
+                            int mode, uint64_t* sha_sz, uint64_t* kec_sz) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t klen;
+  if (mode == MSG_VOTE) {
+    uint64_t sl = 17ull + flen(v, i, HLC_F_OWNER) + flen(v, i, HLC_F_PARENT) + flen(v, i, HLC_F_RECEIVED);
+    sha_sz[i] = ((sl + 8) / 64 + 1) * 64;
+    uint64_t el = vote_enc_len(v, i);
+    klen = 26 + dec_digits(el) + el;
+  } else {
+    uint64_t pl = pay_len[i];
+    klen = 26 + dec_digits(pl) + pl;
+    if (sha_sz) sha_sz[i] = 0;
+  }
+  kec_sz[i] = (klen / 136 + 1) * 136;
+}
+
+struct Cursor {
+  uint8_t* o;
+  uint64_t pos;
+  __device__ void put(uint8_t b) { o[pos++] = b; }
+  __device__ void put_varint(uint64_t x) {
+    do {
+      uint8_t b = x & 0x7F;
+      x >>= 7;
+      put(x ? (b | 0x80) : b);
+    } while (x);
+  }
+  __device__ void put_bytes(const uint8_t* p, uint32_t n) {
+    for (uint32_t k = 0; k < n; ++k) put(p[k]);
+  }
+  __device__ void put_le(uint64_t x, int nbytes) {
+    for (int k = 0; k < nbytes; ++k) put((uint8_t)(x >> (8 * k)));
+  }
+  __device__ void put_decimal(uint64_t x) {
+    uint8_t d[20];
+    int nd = 0;
+    do {
+      d[nd++] = (uint8_t)('0' + x % 10);
+      x /= 10;
+    } while (x);
+    while (nd) put(d[--nd]);
+  }
+};
+
+__device__ void put_eip191_prefix(Cursor& c) {
+  const char pre[] = "\x19" "Ethereum Signed Message:\n";
+  for (int k = 0; k < 26; ++k) c.put((uint8_t)pre[k]);
+}
+
+__global__ void k_build_msgs(hlc_votes v, uint64_t n, const uint8_t* bytes, const uint64_t* pay_off,
+                             const uint32_t* pay_len, int mode, const uint64_t* sha_off,
+                             const uint64_t* sha_sz, uint8_t* sha_buf, const uint64_t* kec_off,
+                             const uint64_t* kec_sz, uint8_t* kec_buf) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (mode == MSG_VOTE) {
+    // SHA-256 input of compute_vote_hash (utils.rs:39-45) + FIPS 180-4 padding
+    Cursor c{sha_buf + sha_off[i], 0};
+    c.put_le(v.vote_id[i], 4);
+    c.put_bytes(fptr(v, i, HLC_F_OWNER), flen(v, i, HLC_F_OWNER));
+    c.put_le(v.proposal_id[i], 4);
+    c.put_le(v.timestamp[i], 8);
+    c.put(v.vote[i] ? 1 : 0);
+    c.put_bytes(fptr(v, i, HLC_F_PARENT), flen(v, i, HLC_F_PARENT));
+    c.put_bytes(fptr(v, i, HLC_F_RECEIVED), flen(v, i, HLC_F_RECEIVED));
+    uint64_t len = c.pos, sz = sha_sz[i];
+    c.put(0x80);
+    while (c.pos < sz - 8) c.put(0);
+    uint64_t bits = len * 8;
+    for (int k = 7; k >= 0; --k) c.put((uint8_t)(bits >> (8 * k)));
+  }
+  // EIP-191 message: "\x19Ethereum Signed Message:\n" || decimal(len) || payload, keccak pad
+  Cursor c{kec_buf + kec_off[i], 0};
+  put_eip191_prefix(c);
+  if (mode == MSG_VOTE) {
+    c.put_decimal(vote_enc_len(v, i));
+    uint32_t id = v.vote_id[i], pid = v.proposal_id[i];
+    uint64_t ts = v.timestamp[i];
+    if (id) { c.put(0xA0); c.put(0x01); c.put_varint(id); }
+    uint32_t lo = flen(v, i, HLC_F_OWNER);
+    if (lo) { c.put(0xAA); c.put(0x01); c.put_varint(lo); c.put_bytes(fptr(v, i, HLC_F_OWNER), lo); }
+    if (pid) { c.put(0xB0); c.put(0x01); c.put_varint(pid); }
+    if (ts) { c.put(0xB8); c.put(0x01); c.put_varint(ts); }
+    if (v.vote[i]) { c.put(0xC0); c.put(0x01); c.put(0x01); }
+    const uint8_t keys[3] = {0xCA, 0xD2, 0xDA};
+    for (int f = HLC_F_PARENT; f <= HLC_F_VOTE_HASH; ++f) {
+      uint32_t l = flen(v, i, f);
+      if (l) { c.put(keys[f - HLC_F_PARENT]); c.put(0x01); c.put_varint(l); c.put_bytes(fptr(v, i, f), l); }
+    }
+  } else {
+    uint32_t pl = pay_len[i];
+    c.put_decimal(pl);
+    c.put_bytes(bytes + pay_off[i], pl);
+  }
+  uint64_t sz = kec_sz[i];
+  c.put(0x01);
+  while (c.pos < sz) c.put(0);
+  c.o[sz - 1] |= 0x80;
+}
+
+__global__ void k_sha_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, const uint8_t* buf,
+                             uint32_t* out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h[8];
+  sha256_init(h);
+  const uint32_t* m = reinterpret_cast<const uint32_t*>(buf + off[i]);
+  uint64_t nb = sz[i] / 64;
+  for (uint64_t b = 0; b < nb; ++b) {
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = bswap32(m[b * 16 + k]);
+    sha256_compress(h, w);
+  }
+  // digest as memory-order words (bytes 4k..4k+3 little-endian in word k)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[i * 8 + k] = bswap32(h[k]);
+}
+
+__global__ void k_keccak_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, const uint8_t* buf,
+                                uint32_t* out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t st[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) st[k] = 0;
+  const uint64_t* m = reinterpret_cast<const uint64_t*>(buf + off[i]);
+  uint64_t nb = sz[i] / 136;
+  for (uint64_t b = 0; b < nb; ++b) {
+#pragma unroll
+    for (int k = 0; k < 17; ++k) st[k] ^= m[b * 17 + k];
+    keccak_f1600(st);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    out[i * 8 + 2 * k] = (uint32_t)st[k];
+    out[i * 8 + 2 * k + 1] = (uint32_t)(st[k] >> 32);
+  }
+}
+
+// validate_vote checks that precede Signer::verify (utils.rs:133-148) and the scheme's
+// length checks (signing/ethereum.rs:71-82), after the proposal_id match (utils.rs:113-115).
+__global__ void k_pre_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                             const uint32_t* sha, uint8_t* pre, uint8_t* pre_reason) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st, rs = 0;
+  uint32_t p = vote_prop ? vote_prop[i] : 0;
+  if (vote_prop && p == NO_PROP) {
+    st = PRE_SKIP;
+  } else if (v.proposal_id[i] != props[p].proposal_id) {
+    st = HLC_VOTE_PROPOSAL_ID_MISMATCH;
+  } else if (flen(v, i, HLC_F_OWNER) == 0) {
+    st = HLC_EMPTY_VOTE_OWNER;
+  } else if (flen(v, i, HLC_F_VOTE_HASH) == 0) {
+    st = HLC_EMPTY_VOTE_HASH;
+  } else if (flen(v, i, HLC_F_SIGNATURE) == 0) {
+    st = HLC_EMPTY_SIGNATURE;
+  } else {
+    bool eq = flen(v, i, HLC_F_VOTE_HASH) == 32;
+    if (eq) {
+      const uint8_t* h = fptr(v, i, HLC_F_VOTE_HASH);
+      for (int k = 0; k < 32 && eq; ++k) eq = h[k] == (uint8_t)(sha[i * 8 + k / 4] >> (8 * (k & 3)));
+    }
+    if (!eq) {
+      st = HLC_INVALID_VOTE_HASH;
+    } else if (flen(v, i, HLC_F_SIGNATURE) != 65) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = HLC_SCHEME_SIG_LEN;
+    } else if (flen(v, i, HLC_F_OWNER) != 20) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = HLC_SCHEME_ID_LEN;
+    } else {
+      st = PRE_PENDING;
+    }
+  }
+  pre[i] = st;
+  pre_reason[i] = rs;
+}
+
+// validate_vote tail (utils.rs:154-168): scheme result, then timestamps
+__global__ void k_vote_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                              uint64_t now, const uint8_t* pre, const uint8_t* pre_reason,
+                              const uint8_t* verify, uint8_t* status, uint8_t* reason) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = pre[i], rs = pre_reason[i];
+  if (st == PRE_PENDING) {
+    uint8_t vr = verify[i];
+    const hlc_proposal& p = props[vote_prop[i]];
+    uint64_t ts = v.timestamp[i];
+    if (vr >= 2) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = vr - 1;
+    } else if (vr == HLC_VERIFY_FALSE) {
+      st = HLC_INVALID_VOTE_SIGNATURE;
+    } else if (ts < p.timestamp) {
+      st = HLC_TIMESTAMP_OLDER_THAN_CREATION;
+    } else if (ts > p.expiration_timestamp || now > p.expiration_timestamp) {
+      st = HLC_VOTE_EXPIRED;
+    } else {
+      st = HLC_OK;
+    }
+  }
+  status[i] = st;
+  reason[i] = rs;
+}
+
+// ---------------- chain / duplicate tables ----------------
+__device__ __forceinline__ uint32_t key_hash(uint32_t p, const uint8_t* b, uint32_t len) {
+  uint32_t h = 2166136261u ^ (p * 0x9E3779B1u);
+  for (uint32_t k = 0; k < len; ++k) h = (h ^ b[k]) * 16777619u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h;
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+  if (al != bl) return false;
+  for (uint32_t k = 0; k < al; ++k)
+    if (a[k] != b[k]) return false;
+  return true;
+}
+
+template <bool LAST_WINS>
+__device__ void table_insert(uint32_t* tab, uint32_t mask, const hlc_votes& v, const uint32_t* vote_prop,
+                             uint32_t idx, int f) {
+  const uint32_t p = vote_prop[idx];
+  const uint8_t* kb = fptr(v, idx, f);
+  const uint32_t kl = flen(v, idx, f);
+  uint32_t h = key_hash(p, kb, kl) & mask;
+  for (;;) {
+    uint32_t cur = atomicCAS(&tab[h], EMPTY_SLOT, idx);
+    if (cur == EMPTY_SLOT) return;
+    if (vote_prop[cur] == p && bytes_eq(fptr(v, cur, f), flen(v, cur, f), kb, kl)) {
+      if (LAST_WINS) atomicMax(&tab[h], idx);
+      else atomicMin(&tab[h], idx);
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__global__ void k_tables(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                         uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t p = vote_prop[i];
+  if (p == NO_PROP) return;
+  // HashMap<vote_hash, (owner, ts, idx)>: last index wins (utils.rs:180-183)
+  if (props[p].vote_count > 1) table_insert<true>(chain_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_VOTE_HASH);
+  // seen_owners HashSet: the first occurrence is the one later duplicates collide with
+  table_insert<false>(dup_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_OWNER);
+}
+
+__device__ __forceinline__ uint32_t table_find(const uint32_t* tab, uint32_t mask, const hlc_votes& v,
+                                               const uint32_t* vote_prop, uint32_t p, const uint8_t* kb,
+                                               uint32_t kl, int f) {
+  uint32_t h = key_hash(p, kb, kl) & mask;
+  for (;;) {
+    uint32_t cur = tab[h];
+    if (cur == EMPTY_SLOT) return EMPTY_SLOT;
+    if (vote_prop[cur] == p && bytes_eq(fptr(v, cur, f), flen(v, cur, f), kb, kl)) return cur;
+    h = (h + 1) & mask;
+  }
+}
+
+// red layout per proposal: [0] first bad vote (local idx), [1] first chain error, [2] first dup, [3] yes
+__global__ void k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                              const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
+                              uint32_t mask, uint8_t* chain_code, uint32_t* red) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t p = i < n ? vote_prop[i] : NO_PROP;
+  bool yes = false;
+  if (p != NO_PROP) {
+    const hlc_proposal d = props[p];
+    const uint32_t j = (uint32_t)(i - d.vote_begin);
+    uint8_t cc = HLC_OK;
+    if (d.vote_count > 1) {
+      // received link (utils.rs:188-198)
+      if (j > 0 && flen(v, i, HLC_F_RECEIVED) != 0) {
+        if (!bytes_eq(fptr(v, i, HLC_F_RECEIVED), flen(v, i, HLC_F_RECEIVED), fptr(v, i - 1, HLC_F_VOTE_HASH),
+                      flen(v, i - 1, HLC_F_VOTE_HASH)) ||
+            v.timestamp[i - 1] > v.timestamp[i])
+          cc = HLC_RECEIVED_HASH_MISMATCH;
+      }
+      // parent link (utils.rs:202-211)
+      if (cc == HLC_OK && flen(v, i, HLC_F_PARENT) != 0) {
+        uint32_t hit = table_find(chain_tab, mask, v, vote_prop, p, fptr(v, i, HLC_F_PARENT),
+                                  flen(v, i, HLC_F_PARENT), HLC_F_VOTE_HASH);
+        if (hit == EMPTY_SLOT ||
+            !(bytes_eq(fptr(v, hit, HLC_F_OWNER), flen(v, hit, HLC_F_OWNER), fptr(v, i, HLC_F_OWNER),
+                       flen(v, i, HLC_F_OWNER)) &&
+              v.timestamp[hit] <= v.timestamp[i] && hit < i))
+          cc = HLC_PARENT_HASH_MISMATCH;
+      }
+    }
+    chain_code[i] = cc;
+    if (status[i] != HLC_OK) atomicMin(&red[4 * p + 0], j);
+    if (cc != HLC_OK) atomicMin(&red[4 * p + 1], j);
+    uint32_t first = table_find(dup_tab, mask, v, vote_prop, p, fptr(v, i, HLC_F_OWNER),
+                                flen(v, i, HLC_F_OWNER), HLC_F_OWNER);
+    if (first != (uint32_t)i) atomicMin(&red[4 * p + 2], j);
+    yes = v.vote[i] != 0;
+  }
+  // YES count: one atomic per wave when the whole wave shares a proposal (large proposals)
+  const uint32_t p0 = __builtin_amdgcn_readfirstlane(p);
+  const uint64_t same = __ballot(p == p0);
+  if (same == ~0ull) {
+    const uint64_t y = __ballot(yes);
+    if (p0 != NO_PROP && (threadIdx.x & 63) == 0 && y) atomicAdd(&red[4 * p0 + 3], (uint32_t)__popcll(y));
+  } else if (yes) {
+    atomicAdd(&red[4 * p + 3], 1u);
+  }
+}
+
+// utils.rs:307-313
+__device__ uint32_t threshold_value(uint32_t n, double t) {
+  if (fabs(t - 2.0 / 3.0) < 2.220446049250313e-16) {
+    uint32_t two_n = 2u * n;  // u32 wrap as in a release build
+    return two_n / 3u + (two_n % 3u != 0);
+  }
+  double x = ceil((double)n * t);
+  if (!(x > 0)) return 0;
+  if (x >= 4294967295.0) return 0xFFFFFFFFu;
+  return (uint32_t)x;
+}
+
+// utils.rs:227-286 (is_timeout = false) -> -1 None / 0 / 1
+__device__ int consensus_result(uint32_t total, uint32_t yes, uint32_t n, double t, bool liveness) {
+  uint32_t no = total > yes ? total - yes : 0;
+  uint32_t silent = n > total ? n - total : 0;
+  if (n <= 2) {
+    if (total < n) return -1;
+    return yes == n;
+  }
+  uint32_t req = threshold_value(n, t);
+  if (total < req) return -1;
+  uint32_t yw = yes + (liveness ? silent : 0), nw = no + (liveness ? 0 : silent);
+  if (yw >= req && yw > nw) return 1;
+  if (nw >= req && nw > yw) return 0;
+  if (total == n && yw == nw) return liveness ? 1 : 0;
+  return -1;
+}
+
+// from_proposal outcome (SURVEY.md Appendix B order)
+__global__ void k_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
+                           const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red,
+                           hlc_result* out) {
+  uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  const hlc_proposal d = props[p];
+  hlc_result r;
+  r.status = HLC_OK;
+  r.transition = HLC_STILL_ACTIVE;
+  r.scheme_reason = 0;
+  r._pad = 0;
+  r.bad_index = 0xFFFFFFFFu;
+  r.yes = 0;
+  r.total = 0;
+  const uint32_t fb = red[4 * p], fc = red[4 * p + 1], fd = red[4 * p + 2];
+  if (now >= d.expiration_timestamp) {  // utils.rs:110
+    r.status = HLC_PROPOSAL_EXPIRED;
+  } else if (fb != 0xFFFFFFFFu) {  // first failing vote, utils.rs:112-117
+    r.status = status[d.vote_begin + fb];
+    r.scheme_reason = reason[d.vote_begin + fb];
+    r.bad_index = fb;
+  } else if (fc != 0xFFFFFFFFu) {  // chain, utils.rs:118
+    r.status = chain_code[d.vote_begin + fc];
+    r.bad_index = fc;
+  } else if (d.vote_count == 0) {  // session.rs:266-268
+  } else if (fd != 0xFFFFFFFFu) {  // session.rs:270-275
+    r.status = HLC_DUPLICATE_VOTE;
+    r.bad_index = fd;
+  } else if (d.vote_count > d.expected_voters_count) {  // session.rs:279-282
+    r.status = HLC_MAX_ROUNDS_EXCEEDED;
+  } else {
+    // check_round_limit at round 1 (session.rs:306-344, 120-128)
+    uint32_t projected = d.use_gossipsub_rounds ? 2u : d.vote_count;
+    uint32_t limit = d.use_gossipsub_rounds
+                         ? d.max_rounds
+                         : (d.max_rounds ? d.max_rounds : threshold_value(d.expected_voters_count, d.consensus_threshold));
+    if (projected > limit) {
+      r.status = HLC_MAX_ROUNDS_EXCEEDED;
+    } else {
+      r.total = d.vote_count;
+      r.yes = red[4 * p + 3];
+      int c = consensus_result(r.total, r.yes, d.expected_voters_count, d.consensus_threshold,
+                               d.liveness_criteria_yes != 0);  // session.rs:372-387
+      r.transition = c < 0 ? HLC_STILL_ACTIVE : (c ? HLC_REACHED_YES : HLC_REACHED_NO);
+    }
+  }
+  out[p] = r;
+}
+
+__global__ void k_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
+                             uint8_t* verify_out) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (sig_len[i] != 65) {
+    pre[i] = 0;
+    verify_out[i] = 1 + HLC_SCHEME_SIG_LEN;
+  } else if (id_len[i] != 20) {
+    pre[i] = 0;
+    verify_out[i] = 1 + HLC_SCHEME_ID_LEN;
+  } else {
+    pre[i] = PRE_PENDING;
+  }
+}
+
+inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB); }
+
+}  // namespace
+
+void launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
+                           hipStream_t s) {
+  hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
+}
+
+void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
+                       uint8_t* verify_out, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_verify_pre, dim3(blocks_for(n)), dim3(TPB), 0, s, n, sig_len, id_len, pre, verify_out);
+}
+
+void launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv,
+                         hipStream_t s) {
+  if (nv) hipMemsetAsync(vote_prop, 0xFF, nv * sizeof(uint32_t), s);
+  if (np) hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np), dim3(TPB), 0, s, props, vote_prop);
+}
+
+void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
+                      int mode, uint64_t* sha_sz, uint64_t* kec_sz, hipStream_t s) {
+  if (!n) return;
+  hlc_votes vv = v ? *v : hlc_votes{};
+  hipLaunchKernelGGL(k_msg_sizes, dim3(blocks_for(n)), dim3(TPB), 0, s, vv, n, pay_off, pay_len, mode, sha_sz,
+                     kec_sz);
+}
+
+void launch_build_msgs(const hlc_votes* v, uint64_t n, const uint8_t* bytes, const uint64_t* pay_off,
+                       const uint32_t* pay_len, int mode, const uint64_t* sha_off, const uint64_t* sha_sz,
+                       uint8_t* sha_buf, const uint64_t* kec_off, const uint64_t* kec_sz, uint8_t* kec_buf,
+                       hipStream_t s) {
+  if (!n) return;
+  hlc_votes vv = v ? *v : hlc_votes{};
+  hipLaunchKernelGGL(k_build_msgs, dim3(blocks_for(n)), dim3(TPB), 0, s, vv, n, bytes, pay_off, pay_len, mode,
+                     sha_off, sha_sz, sha_buf, kec_off, kec_sz, kec_buf);
+}
+
+void launch_sha_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, const uint8_t* buf, uint32_t* out,
+                       hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_sha_blocks, dim3(blocks_for(n)), dim3(TPB), 0, s, n, off, sz, buf, out);
+}
+
+void launch_keccak_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, const uint8_t* buf, uint32_t* out,
+                          hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_keccak_blocks, dim3(blocks_for(n)), dim3(TPB), 0, s, n, off, sz, buf, out);
+}
+
+void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                       const uint32_t* sha_digest, uint8_t* pre, uint8_t* pre_reason, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_pre_status, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, sha_digest,
+                       pre, pre_reason);
+}
+
+void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                        uint64_t now, const uint8_t* pre, const uint8_t* pre_reason, const uint8_t* verify,
+                        uint8_t* status, uint8_t* reason, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_vote_status, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, now, pre,
+                       pre_reason, verify, status, reason);
+}
+
+void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, hipStream_t s) {
+  if (!n) return;
+  hipMemsetAsync(chain_tab, 0xFF, ((size_t)mask + 1) * sizeof(uint32_t), s);
+  hipMemsetAsync(dup_tab, 0xFF, ((size_t)mask + 1) * sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_tables, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, chain_tab, dup_tab,
+                     mask);
+}
+
+void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                        const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab, uint32_t mask,
+                        uint8_t* chain_code, uint32_t* red, uint64_t np, hipStream_t s) {
+  if (!np) return;
+  hipMemsetAsync(red, 0xFF, np * 4 * sizeof(uint32_t), s);
+  // yes counters start at zero: clear word 3 of each record with a strided memset kernel-free pass
+  hipMemset2DAsync(red + 3, 4 * sizeof(uint32_t), 0, sizeof(uint32_t), np, s);
+  if (n)
+    hipLaunchKernelGGL(k_chain_check, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, status,
+                       chain_tab, dup_tab, mask, chain_code, red);
+}
+
+void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
+                     const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red, hlc_result* out,
+                     hipStream_t s) {
+  if (np)
+    hipLaunchKernelGGL(k_finalize, dim3(blocks_for(np)), dim3(TPB), 0, s, props, np, now, status, reason,
+                       chain_code, red, out);
+}
+
+}  // namespace hlc

@@ -1,0 +1,155 @@
+"""ctypes view of the C ABI in include/hlc.h and the loader for the in-tree libhlc.so.
+
+The library is the product: a HIP (gfx950) build.  There is no CPU fallback -- if the
+shared object is missing or cannot be loaded the import of the GPU entry points fails
+loudly (`HlcUnavailable`).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_uint8, c_uint32, c_uint64, c_void_p
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhlc.so")
+
+HLC_NFIELDS = 5
+F_OWNER, F_PARENT, F_RECEIVED, F_VOTE_HASH, F_SIGNATURE = range(5)
+
+
+class HlcUnavailable(RuntimeError):
+    pass
+
+
+class HlcError(RuntimeError):
+    pass
+
+
+class hlc_votes(ctypes.Structure):
+    _fields_ = [
+        ("n", c_uint64),
+        ("vote_id", POINTER(c_uint32)),
+        ("proposal_id", POINTER(c_uint32)),
+        ("timestamp", POINTER(c_uint64)),
+        ("vote", POINTER(c_uint8)),
+        ("bytes", POINTER(c_uint8)),
+        ("bytes_len", c_uint64),
+        ("field_off", POINTER(c_uint64)),
+        ("field_len", POINTER(c_uint32)),
+    ]
+
+
+class hlc_proposal(ctypes.Structure):
+    _fields_ = [
+        ("vote_begin", c_uint64),
+        ("vote_count", c_uint32),
+        ("proposal_id", c_uint32),
+        ("timestamp", c_uint64),
+        ("expiration_timestamp", c_uint64),
+        ("expected_voters_count", c_uint32),
+        ("max_rounds", c_uint32),
+        ("consensus_threshold", c_double),
+        ("use_gossipsub_rounds", c_uint8),
+        ("liveness_criteria_yes", c_uint8),
+        ("_pad", c_uint8 * 6),
+    ]
+
+
+class hlc_result(ctypes.Structure):
+    _fields_ = [
+        ("status", c_uint8),
+        ("transition", c_uint8),
+        ("scheme_reason", c_uint8),
+        ("_pad", c_uint8),
+        ("bad_index", c_uint32),
+        ("yes", c_uint32),
+        ("total", c_uint32),
+    ]
+
+
+assert ctypes.sizeof(hlc_proposal) == 56
+assert ctypes.sizeof(hlc_result) == 16
+
+# numpy structured dtypes with the same layout (for zero-copy packing)
+try:
+    import numpy as np
+
+    PROPOSAL_DTYPE = np.dtype([
+        ("vote_begin", "<u8"), ("vote_count", "<u4"), ("proposal_id", "<u4"),
+        ("timestamp", "<u8"), ("expiration_timestamp", "<u8"),
+        ("expected_voters_count", "<u4"), ("max_rounds", "<u4"),
+        ("consensus_threshold", "<f8"), ("use_gossipsub_rounds", "u1"),
+        ("liveness_criteria_yes", "u1"), ("_pad", "u1", (6,)),
+    ])
+    RESULT_DTYPE = np.dtype([
+        ("status", "u1"), ("transition", "u1"), ("scheme_reason", "u1"), ("_pad", "u1"),
+        ("bad_index", "<u4"), ("yes", "<u4"), ("total", "<u4"),
+    ])
+    assert PROPOSAL_DTYPE.itemsize == 56 and RESULT_DTYPE.itemsize == 16
+except ImportError:  # pragma: no cover
+    np = None
+
+EXPORTED_SYMBOLS = (
+    "hlc_ctx_create", "hlc_ctx_destroy", "hlc_ctx_reserve", "hlc_last_error", "hlc_abi_version",
+    "hlc_compute_vote_hashes", "hlc_eth_verify_batch", "hlc_validate_proposals",
+    "hlc_validate_proposals_device", "hlc_eth_address_batch", "hlc_eth_sign_batch",
+)
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libhlc.so and declare the prototypes.  Raises HlcUnavailable if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HlcUnavailable(
+            f"libhlc.so not found at {path}; run `python __graft_entry__.py build` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    vp = c_void_p
+    u8p = POINTER(c_uint8)
+    u32p = POINTER(c_uint32)
+    u64p = POINTER(c_uint64)
+    lib.hlc_ctx_create.argtypes = [c_int, POINTER(vp)]
+    lib.hlc_ctx_create.restype = c_int
+    lib.hlc_ctx_destroy.argtypes = [vp]
+    lib.hlc_ctx_destroy.restype = None
+    lib.hlc_ctx_reserve.argtypes = [vp, c_uint64, c_uint64, c_uint64]
+    lib.hlc_ctx_reserve.restype = c_int
+    lib.hlc_last_error.argtypes = []
+    lib.hlc_last_error.restype = c_char_p
+    lib.hlc_abi_version.argtypes = []
+    lib.hlc_abi_version.restype = c_int
+    lib.hlc_compute_vote_hashes.argtypes = [vp, POINTER(hlc_votes), u8p]
+    lib.hlc_compute_vote_hashes.restype = c_int
+    lib.hlc_eth_verify_batch.argtypes = [vp, c_uint64, u8p, c_uint64, u64p, u32p, u64p, u32p,
+                                         u64p, u32p, u8p, u8p]
+    lib.hlc_eth_verify_batch.restype = c_int
+    lib.hlc_validate_proposals.argtypes = [vp, POINTER(hlc_votes), POINTER(hlc_proposal), c_uint64,
+                                           c_uint64, POINTER(hlc_result), u8p, u8p, u8p]
+    lib.hlc_validate_proposals.restype = c_int
+    lib.hlc_validate_proposals_device.argtypes = [vp, POINTER(hlc_votes), POINTER(hlc_proposal),
+                                                  c_uint64, c_uint64, POINTER(hlc_result), u8p,
+                                                  u8p, u8p, vp]
+    lib.hlc_validate_proposals_device.restype = c_int
+    lib.hlc_eth_address_batch.argtypes = [vp, c_uint64, u8p, u8p]
+    lib.hlc_eth_address_batch.restype = c_int
+    lib.hlc_eth_sign_batch.argtypes = [vp, c_uint64, u8p, u8p, c_uint64, u64p, u32p, u8p]
+    lib.hlc_eth_sign_batch.restype = c_int
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = _lib.hlc_last_error().decode(errors="replace") if _lib is not None else ""
+        raise HlcError(f"libhlc call failed with {rc}: {msg}")
+
+
+def ptr(arr, ctype):
+    """ctypes pointer to a numpy array's data (None for None)."""
+    if arr is None:
+        return None
+    return arr.ctypes.data_as(POINTER(ctype))

@@ -1,0 +1,129 @@
+"""Engine: a device context of libhlc.so with numpy-level batch entry points.
+
+Every call goes through the C ABI of include/hlc.h into the gfx950 kernels; nothing here
+computes a hash, a signature or a consensus outcome on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from ctypes import c_uint8, c_uint32, c_uint64, c_void_p
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _ffi
+from .batch import VoteBatch, proposals_ptr, results_ptr
+
+
+def _arena(chunks: Sequence[bytes]):
+    lens = np.fromiter((len(c) for c in chunks), dtype=np.uint32, count=len(chunks))
+    off = np.zeros(len(chunks), dtype=np.uint64)
+    if len(chunks):
+        off[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+    data = b"".join(chunks)
+    arena = np.frombuffer(data, dtype=np.uint8).copy() if data else np.zeros(1, np.uint8)
+    return arena, off, lens, len(data)
+
+
+class Engine:
+    """One libhlc context on HIP device `device` (default 0)."""
+
+    _default: Optional["Engine"] = None
+    _lock = threading.Lock()
+
+    def __init__(self, device: int = 0):
+        self.lib = _ffi.load_library()
+        h = c_void_p()
+        _ffi.check(self.lib.hlc_ctx_create(device, ctypes.byref(h)))
+        self.ctx = h
+        self.device = device
+
+    @classmethod
+    def default(cls) -> "Engine":
+        """Process-global lazily-initialised context: what the static `Signer::verify` of
+        signing.rs:69 needs (no instance is available at the call site)."""
+        with cls._lock:
+            if cls._default is None:
+                cls._default = Engine(0)
+            return cls._default
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.hlc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, max_votes: int, max_proposals: int, max_bytes: int = 0) -> None:
+        _ffi.check(self.lib.hlc_ctx_reserve(self.ctx, max_votes, max_proposals, max_bytes))
+
+    # ---- hot path ---------------------------------------------------------------------
+    def validate_proposals(self, batch: VoteBatch, desc: np.ndarray, now: int,
+                           want_votes: bool = True, want_recovered: bool = False):
+        """hlc_validate_proposals -> (results[np] structured, vote_status[n], vote_reason[n],
+        recovered[n,20] or None)."""
+        n = batch.n
+        res = np.zeros(desc.shape[0], dtype=_ffi.RESULT_DTYPE)
+        vst = np.zeros(max(n, 1), np.uint8) if want_votes else None
+        vrs = np.zeros(max(n, 1), np.uint8) if want_votes else None
+        rec = np.zeros((max(n, 1), 20), np.uint8) if want_recovered else None
+        view = batch.view()
+        desc = np.ascontiguousarray(desc)
+        _ffi.check(self.lib.hlc_validate_proposals(
+            self.ctx, ctypes.byref(view), proposals_ptr(desc), desc.shape[0], now, results_ptr(res),
+            _ffi.ptr(vst, c_uint8), _ffi.ptr(vrs, c_uint8), _ffi.ptr(rec, c_uint8)))
+        return (res, vst[:n] if vst is not None else None, vrs[:n] if vrs is not None else None,
+                rec[:n] if rec is not None else None)
+
+    def compute_vote_hashes(self, batch: VoteBatch) -> np.ndarray:
+        out = np.zeros((max(batch.n, 1), 32), np.uint8)
+        view = batch.view()
+        _ffi.check(self.lib.hlc_compute_vote_hashes(self.ctx, ctypes.byref(view), _ffi.ptr(out, c_uint8)))
+        return out[:batch.n]
+
+    def eth_verify_batch(self, identities: Sequence[bytes], payloads: Sequence[bytes],
+                         signatures: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+        """Batched EthereumConsensusSigner::verify -> (status[n], recovered[n,20])."""
+        n = len(identities)
+        assert len(payloads) == n and len(signatures) == n
+        arena, off, lens, total = _arena(list(identities) + list(payloads) + list(signatures))
+        st = np.zeros(max(n, 1), np.uint8)
+        addr = np.zeros((max(n, 1), 20), np.uint8)
+        io, il = off[:n].copy(), lens[:n].copy()
+        po, pl = off[n:2 * n].copy(), lens[n:2 * n].copy()
+        so, sl = off[2 * n:].copy(), lens[2 * n:].copy()
+        _ffi.check(self.lib.hlc_eth_verify_batch(
+            self.ctx, n, _ffi.ptr(arena, c_uint8), total, _ffi.ptr(io, c_uint64), _ffi.ptr(il, c_uint32),
+            _ffi.ptr(po, c_uint64), _ffi.ptr(pl, c_uint32), _ffi.ptr(so, c_uint64), _ffi.ptr(sl, c_uint32),
+            _ffi.ptr(st, c_uint8), _ffi.ptr(addr, c_uint8)))
+        return st[:n], addr[:n]
+
+    # ---- signing side -------------------------------------------------------------------
+    def address_batch(self, priv: np.ndarray) -> np.ndarray:
+        priv = np.ascontiguousarray(priv, dtype=np.uint8).reshape(-1, 32)
+        n = priv.shape[0]
+        out = np.zeros((max(n, 1), 20), np.uint8)
+        _ffi.check(self.lib.hlc_eth_address_batch(self.ctx, n, _ffi.ptr(priv, c_uint8), _ffi.ptr(out, c_uint8)))
+        return out[:n]
+
+    def sign_batch(self, priv: np.ndarray, payloads: Sequence[bytes]) -> np.ndarray:
+        priv = np.ascontiguousarray(priv, dtype=np.uint8).reshape(-1, 32)
+        n = priv.shape[0]
+        arena, off, lens, total = _arena(list(payloads))
+        return self.sign_batch_arena(priv, arena, off, lens, total)
+
+    def sign_batch_arena(self, priv: np.ndarray, arena: np.ndarray, off: np.ndarray, lens: np.ndarray,
+                         total: int) -> np.ndarray:
+        n = priv.shape[0]
+        out = np.zeros((max(n, 1), 65), np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        _ffi.check(self.lib.hlc_eth_sign_batch(
+            self.ctx, n, _ffi.ptr(priv, c_uint8), _ffi.ptr(arena, c_uint8), total, _ffi.ptr(off, c_uint64),
+            _ffi.ptr(lens, c_uint32), _ffi.ptr(out, c_uint8)))
+        return out[:n]

@@ -1,0 +1,186 @@
+/*
+ * hlc.h — C ABI of the MI355X batch vote-validation engine (libhlc.so).
+ *
+ * Drop-in boundary for the hot path of vacp2p/hashgraph-like-consensus v0.6.0
+ * (`ConsensusService::process_incoming_proposal`, /root/reference/src/service.rs:263-279).
+ * Every entry point cites the reference interface it replaces.  No torch / HIP types
+ * appear in the signatures: plain pointers, sizes and an opaque context.
+ *
+ * Ownership: the caller owns every buffer it passes; the library owns the device
+ * workspace inside `hlc_ctx`; no pointer is retained after a call returns.
+ * Threading: a context serialises its calls with an internal mutex (the reference's
+ * service is `Send + Sync`, CHANGELOG.md 0.5.0); use one context per thread for
+ * concurrency.  Host-buffer entry points are blocking (mirror the sync Rust API).
+ * Return value: 0 on success, negative HLC_E* on API / device failure.  Item-level
+ * outcomes (reject codes) are only ever reported through the output arrays.
+ */
+#ifndef HLC_H
+#define HLC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HLC_ABI_VERSION 1
+
+/* ---- API return codes -------------------------------------------------------- */
+#define HLC_SUCCESS 0
+#define HLC_EINVAL (-1)   /* bad argument (NULL pointer, out-of-range offsets, ...) */
+#define HLC_EDEVICE (-2)  /* HIP runtime / kernel failure */
+#define HLC_ENOMEM (-3)   /* device allocation failed */
+#define HLC_ENODEV (-4)   /* no usable gfx950 device */
+
+/* ---- Item status codes: the hot-path subset of `ConsensusError`
+ *      (/root/reference/src/error.rs:11-74).  Values are ABI. ------------------- */
+#define HLC_OK 0
+#define HLC_PROPOSAL_EXPIRED 1                 /* error.rs:39 */
+#define HLC_VOTE_PROPOSAL_ID_MISMATCH 2        /* error.rs:41 */
+#define HLC_EMPTY_VOTE_OWNER 3                 /* error.rs:33 */
+#define HLC_EMPTY_VOTE_HASH 4                  /* error.rs:37 */
+#define HLC_EMPTY_SIGNATURE 5                  /* error.rs:25 */
+#define HLC_INVALID_VOTE_HASH 6                /* error.rs:35 */
+#define HLC_SIGNATURE_SCHEME 7                 /* error.rs:72-73, ConsensusSchemeError::Verify */
+#define HLC_INVALID_VOTE_SIGNATURE 8           /* error.rs:23 */
+#define HLC_TIMESTAMP_OLDER_THAN_CREATION 9    /* error.rs:49 */
+#define HLC_VOTE_EXPIRED 10                    /* error.rs:31 */
+#define HLC_RECEIVED_HASH_MISMATCH 11          /* error.rs:43 */
+#define HLC_PARENT_HASH_MISMATCH 12            /* error.rs:45 */
+#define HLC_DUPLICATE_VOTE 13                  /* error.rs:27 */
+#define HLC_MAX_ROUNDS_EXCEEDED 14             /* error.rs:65 */
+#define HLC_PROPOSAL_ALREADY_EXIST 15          /* error.rs:57 (host-side, storage) */
+
+/* Sub-reason of HLC_SIGNATURE_SCHEME (the reference's Verify(String) message class). */
+#define HLC_SCHEME_NONE 0
+#define HLC_SCHEME_SIG_LEN 1        /* signing/ethereum.rs:71-76 */
+#define HLC_SCHEME_ID_LEN 2         /* signing/ethereum.rs:77-82 */
+#define HLC_SCHEME_BAD_PARITY 3     /* alloy Signature::from_raw_array / normalize_v (ethereum.rs:86) */
+#define HLC_SCHEME_SCALAR_RANGE 4   /* r or s zero or >= n (k256 from_scalars via to_k256) */
+#define HLC_SCHEME_NO_POINT 5       /* R = decompress(r) does not exist */
+#define HLC_SCHEME_INFINITY 6       /* recovered key is the identity */
+
+/* Outcome of `ConsensusSignatureScheme::verify` (signing.rs:60-73) per item. */
+#define HLC_VERIFY_TRUE 0           /* Ok(true)  */
+#define HLC_VERIFY_FALSE 1          /* Ok(false) */
+/* values >= 2: Err(ConsensusSchemeError::Verify), value - 1 == HLC_SCHEME_* reason */
+
+/* SessionTransition (types.rs:29-34) */
+#define HLC_STILL_ACTIVE 0
+#define HLC_REACHED_NO 1
+#define HLC_REACHED_YES 2
+
+/* ---- Vote batch (struct-of-arrays view of `Vec<Vote>`, consensus.proto:19-29) ---- */
+#define HLC_F_OWNER 0
+#define HLC_F_PARENT 1
+#define HLC_F_RECEIVED 2
+#define HLC_F_VOTE_HASH 3
+#define HLC_F_SIGNATURE 4
+#define HLC_NFIELDS 5
+
+typedef struct hlc_votes {
+  uint64_t n;                 /* number of votes */
+  const uint32_t* vote_id;    /* [n]  Vote.vote_id      (tag 20) */
+  const uint32_t* proposal_id;/* [n]  Vote.proposal_id  (tag 22) */
+  const uint64_t* timestamp;  /* [n]  Vote.timestamp    (tag 23) */
+  const uint8_t* vote;        /* [n]  Vote.vote (0/1)   (tag 24) */
+  const uint8_t* bytes;       /* arena holding every bytes field */
+  uint64_t bytes_len;
+  const uint64_t* field_off;  /* [n][HLC_NFIELDS] offset of owner/parent/received/vote_hash/signature */
+  const uint32_t* field_len;  /* [n][HLC_NFIELDS] length (0 = empty bytes) */
+} hlc_votes;
+
+/* One proposal = a contiguous run of votes plus the scalars `resolve_config`
+ * (service.rs:444-484) and the Proposal message (consensus.proto:5-16) contribute. */
+typedef struct hlc_proposal {
+  uint64_t vote_begin;            /* index of the proposal's first vote in hlc_votes */
+  uint32_t vote_count;
+  uint32_t proposal_id;           /* Proposal.proposal_id */
+  uint64_t timestamp;             /* Proposal.timestamp (creation time) */
+  uint64_t expiration_timestamp;  /* Proposal.expiration_timestamp */
+  uint32_t expected_voters_count; /* Proposal.expected_voters_count */
+  uint32_t max_rounds;            /* ConsensusConfig.max_rounds (P2P: 0 = ceil(2n/3)) */
+  double consensus_threshold;     /* ConsensusConfig.consensus_threshold */
+  uint8_t use_gossipsub_rounds;   /* ConsensusConfig.use_gossipsub_rounds */
+  uint8_t liveness_criteria_yes;  /* Proposal.liveness_criteria_yes */
+  uint8_t _pad[6];
+} hlc_proposal; /* 56 bytes */
+
+/* Per-proposal result of `ConsensusSession::from_proposal` (session.rs:198-221). */
+typedef struct hlc_result {
+  uint8_t status;        /* HLC_OK or the first error (SURVEY.md Appendix B order) */
+  uint8_t transition;    /* HLC_STILL_ACTIVE / HLC_REACHED_NO / HLC_REACHED_YES (status == OK) */
+  uint8_t scheme_reason; /* HLC_SCHEME_* when status == HLC_SIGNATURE_SCHEME */
+  uint8_t _pad;
+  uint32_t bad_index;    /* index (within the proposal) of the failing vote, or 0xFFFFFFFF */
+  uint32_t yes;          /* YES votes in the owner->vote map (status == OK) */
+  uint32_t total;        /* votes in the owner->vote map (status == OK) */
+} hlc_result; /* 16 bytes */
+
+typedef struct hlc_ctx hlc_ctx;
+
+/* ---- Context -------------------------------------------------------------------- */
+/* Creates a context on HIP device `device` (process-global lazily-initialised device
+ * state is what the static `Signer::verify` of signing.rs:69 needs). */
+int hlc_ctx_create(int device, hlc_ctx** out);
+void hlc_ctx_destroy(hlc_ctx* ctx);
+/* Pre-sizes the device workspace so later calls allocate nothing (graph-capture safe). */
+int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, uint64_t max_bytes);
+const char* hlc_last_error(void);
+int hlc_abi_version(void);
+
+/* ---- Hot-path entry points (host buffers, blocking) ----------------------------- */
+
+/* Replaces `utils::compute_vote_hash` (utils.rs:37-47) over a batch: out[n][32]. */
+int hlc_compute_vote_hashes(hlc_ctx* ctx, const hlc_votes* votes, uint8_t* out_hash32);
+
+/* Replaces `EthereumConsensusSigner::verify` (signing/ethereum.rs:66-97), the static
+ * `ConsensusSignatureScheme::verify` of signing.rs:69-73, over a batch of n items.
+ * Item i: identity = bytes[id_off[i] .. +id_len[i]], payload likewise, signature likewise.
+ * out_status[i] = HLC_VERIFY_TRUE / HLC_VERIFY_FALSE / 1 + HLC_SCHEME_* (Err).
+ * out_addr (optional, n*20) receives the recovered address when one exists. */
+int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_t bytes_len,
+                         const uint64_t* id_off, const uint32_t* id_len,
+                         const uint64_t* payload_off, const uint32_t* payload_len,
+                         const uint64_t* sig_off, const uint32_t* sig_len,
+                         uint8_t* out_status, uint8_t* out_addr);
+
+/* Validate-many: `ConsensusSession::from_proposal` (session.rs:198-221) for every
+ * proposal, i.e. validate_proposal (utils.rs:106-120) + initialize_with_votes
+ * (session.rs:253-298), as called by process_incoming_proposal (service.rs:273-274).
+ * out_results[p]: per-proposal outcome.  out_vote_status[v] (optional): the per-vote
+ * status of validate_proposal's loop body for that vote alone (proposal_id match, then
+ * validate_vote, utils.rs:112-117, 127-171), with no short-circuit across votes.
+ * out_vote_reason (optional): HLC_SCHEME_* per vote.  out_recovered (optional, n*20):
+ * recovered signer address per vote (zeros when none). */
+int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,
+                           uint64_t n_proposals, uint64_t now, hlc_result* out_results,
+                           uint8_t* out_vote_status, uint8_t* out_vote_reason,
+                           uint8_t* out_recovered);
+
+/* Same, but every pointer (inside `votes`, `proposals`, and the outputs) is DEVICE memory
+ * of the context's device, and the work is enqueued on `stream` (a hipStream_t, or NULL for
+ * the context's stream) without host synchronisation.  Used when inputs are already
+ * resident in HBM (bench.py). */
+int hlc_validate_proposals_device(hlc_ctx* ctx, const hlc_votes* votes,
+                                  const hlc_proposal* proposals, uint64_t n_proposals,
+                                  uint64_t now, hlc_result* out_results,
+                                  uint8_t* out_vote_status, uint8_t* out_vote_reason,
+                                  uint8_t* out_recovered, void* stream);
+
+/* ---- Signing side (generator / embedders simulating many peers) -- */
+
+/* EthereumConsensusSigner::identity (ethereum.rs:54-56) for n private keys: out[n][20]. */
+int hlc_eth_address_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, uint8_t* out_addr20);
+
+/* EthereumConsensusSigner::sign (ethereum.rs:58-64): EIP-191 prehash + RFC 6979 +
+ * low-s + v in {27,28}, over n payloads; out_sig[n][65].  Keys must be in [1, n-1]. */
+int hlc_eth_sign_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, const uint8_t* bytes,
+                       uint64_t bytes_len, const uint64_t* payload_off,
+                       const uint32_t* payload_len, uint8_t* out_sig65);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HLC_H */
