@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Headline benchmark: verified votes/s of the batch vote-validation engine (BASELINE.json).
+
+One "step" = one `hlc_validate_proposals_device` pass (the `ConsensusSession::from_proposal`
+semantics of /root/reference/src/session.rs:198-221 for every proposal) over one batch of
+synthetic signed votes already resident in HBM: SHA-256 vote-hash recompute, prost encoding,
+EIP-191 keccak, secp256k1 ecrecover + address compare, timestamp checks, chain-link hash
+table, duplicate-owner table, per-proposal tally/threshold/round limit.
+
+Workload (the largest single-GPU config of BASELINE.json):
+10,000 proposals x 64 voters (Gossipsub, n = 64) = 640,000 votes per GPU, deterministic,
+generated and signed on the GPU by the engine's own signer (RFC 6979, EthereumConsensusSigner).
+Multi-GPU (torch.distributed.run, one process per GPU, RCCL): every rank validates its own
+proposal shard (weak scaling, no data-path collective); the per-proposal results (16 B each)
+are all-gathered over RCCL once per step, the exchange the north star names.
+
+cpu_baseline: the C restatement of validate_vote (recover + k256's re-verify, as upstream) on
+the host cores, rank 0 at N = 1 only, on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
+
+METRIC = "verified votes/sec (ecrecover+chain check) at 1/2/4/8 MI355X vs host CPU"
+# algorithmic work per vote, frozen before kernel tuning (Appendix D):
+# 2,480 modmul x ~550 int32 ops + 3 keccak-f + 2 SHA-256 compressions.
+W_INT32_OPS_PER_VOTE = 1.39e6
+# MI355X int32 VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (full-rate ops; v_mad_u64_u32
+# is half rate, profiles/r01_ubench_int.txt).
+VALU_INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(workload, sample_proposals: int) -> dict:
+    """Times the oracle's C restatement (oracle/, the checker) on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle  # noqa: E402  (test infrastructure; cpu_baseline leg only)
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    desc = workload.desc[:sample_proposals].copy()
+    votes = int(desc["vote_count"].sum())
+    t0 = time.perf_counter()
+    ok = coracle.validate_votes_only(workload.batch, desc, workload.now, threads, reverify=True)
+    dt = time.perf_counter() - t0
+    assert ok == votes, f"CPU baseline rejected {votes - ok} valid votes"
+    return {
+        "value": votes / dt,
+        "unit": "votes/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sample_proposals} proposals x {votes // max(sample_proposals, 1)} votes = {votes} votes of the "
+                  f"same workload; validate_vote restated in C (SHA-256 + prost + EIP-191 keccak + ecrecover + "
+                  f"k256 re-verify + timestamp checks), {threads} threads, {dt:.2f} s wall",
+        "cpu_model": cpu_model(),
+        "seconds": dt,
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--proposals", type=int, default=10_000)
+    ap.add_argument("--votes-per-proposal", type=int, default=64)
+    ap.add_argument("--cpu-sample-proposals", type=int, default=10_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from hashgraph_like_consensus import synth
+    from hashgraph_like_consensus.device import DeviceBatch
+    from hashgraph_like_consensus.engine import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    else:
+        torch.cuda.set_device(local_rank)
+    dev = f"cuda:{local_rank}"
+
+    eng = Engine(local_rank)
+    P, V = args.proposals, args.votes_per_proposal
+    t_gen = time.perf_counter()
+    addr_fn, sign_fn = synth.engine_signers(eng)
+    w = synth.generate(P, V, V, True, synth.config_seed(2), addr_fn, sign_fn, start_proposal=rank * P,
+                       name="config2")
+    t_gen = time.perf_counter() - t_gen
+    db = DeviceBatch(w.batch, w.desc, w.now, device=dev)
+    eng.reserve(db.n, P, int(w.batch.arena.size))
+    stream = torch.cuda.Stream(device=dev)
+    handle = stream.cuda_stream
+    gathered = None
+    if dist is not None:
+        gathered = [torch.empty_like(db.results) for _ in range(world)]
+
+    def step():
+        eng.validate_proposals_device(db, handle)
+        if dist is not None:
+            with torch.cuda.stream(stream):
+                dist.all_gather(gathered, db.results)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # guard: every synthetic vote is valid, every proposal validates (no silent breakage)
+    res = db.results_numpy()
+    st = db.status_numpy()
+    assert (st == 0).all(), f"{int((st != 0).sum())} valid votes rejected"
+    assert (res["status"] == 0).all() and (res["total"] == V).all()
+
+    eng.set_kernel_timing(True)
+    eng.take_kernel_time()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    rec_ms, rec_n, call_ms, calls = eng.take_kernel_time()
+    eng.set_kernel_timing(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    votes_total = db.n * world * args.steps
+    value = votes_total / elapsed
+    rec_avg_s = rec_ms / max(rec_n, 1) / 1e3
+    achieved = W_INT32_OPS_PER_VOTE * db.n / rec_avg_s / 1e12
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "votes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: deterministic signed votes (SURVEY §8d spec), generated + RFC6979-signed on the GPU",
+        "config": {
+            "workload": "config2: 10k proposals x 64 voters (Gossipsub, n=64) per GPU, full from_proposal validation",
+            "proposals_per_gpu": P,
+            "votes_per_proposal": V,
+            "votes_per_step_per_gpu": db.n,
+            "parallelism": f"proposal-sharded x{world}" + (", RCCL all_gather of results" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "valu",
+            "kernel": "k_recover",
+            "achieved": achieved,
+            "peak": VALU_INT32_PEAK_TOPS,
+            "unit": "Tops/s (int32 lane-ops)",
+            "frac": achieved / VALU_INT32_PEAK_TOPS,
+            "traffic": None,
+            "work_per_vote_int32_ops": W_INT32_OPS_PER_VOTE,
+            "kernel_ms_avg": rec_avg_s * 1e3,
+            "kernel_launches": rec_n,
+            "call_ms_avg": call_ms / max(calls, 1),
+            "kernel_share_of_step": rec_ms / max(call_ms, 1e-9),
+        },
+        "gen_seconds": t_gen,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(w, min(args.cpu_sample_proposals, P))
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    eng.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

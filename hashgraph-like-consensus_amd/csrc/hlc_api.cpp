@@ -76,6 +76,25 @@ struct hlc_ctx {
   // outputs staged on device
   DBuf out_res, out_status, out_reason, out_rec, out_misc;
   // internal workspace
+  // measurement hooks
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, call_ev;
+  hipEvent_t take_event() {
+    if (ev_pool.empty()) {
+      hipEvent_t e = nullptr;
+      (void)hipEventCreate(&e);
+      return e;
+    }
+    hipEvent_t e = ev_pool.back();
+    ev_pool.pop_back();
+    return e;
+  }
+  ~hlc_ctx() {
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
+    for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  }
   DBuf vote_prop, sha_sz, sha_off, kec_sz, kec_off, sha_buf, kec_buf, sha_dig, kec_dig, pre, pre_reason,
       verify, status, reason, chain_code, chain_tab, dup_tab, red, scan_tmp, totals;
 };
@@ -142,7 +161,7 @@ int run_prehash(hlc_ctx* c, const hlc_votes* dv, uint64_t n, int mode, const uin
 int ensure_recover_scratch(hlc_ctx* c) {
   if (c->rec_lanes) return 0;
   uint64_t lanes = hlc::recover_grid_lanes();
-  CHK(c->rec_scratch.ensure(lanes * (uint64_t)(8 * 24 + 4 * 33) * sizeof(uint32_t)));
+  CHK(c->rec_scratch.ensure(lanes * hlc::recover_scratch_words() * sizeof(uint32_t)));
   c->rec_lanes = lanes;
   return 0;
 }
@@ -161,6 +180,12 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
                     hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s) {
   const uint64_t n = dv->n;
   if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
+  hipEvent_t call0 = nullptr, call1 = nullptr;
+  if (c->timing) {
+    call0 = c->take_event();
+    call1 = c->take_event();
+    HIPCHK(hipEventRecord(call0, s));
+  }
   CHK(c->vote_prop.ensure(n * 4 + 4));
   hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, s);
   uint8_t* status = dstatus;
@@ -182,10 +207,20 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
                            c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
     CHK(ensure_recover_scratch(c));
     if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
+    hipEvent_t r0 = nullptr, r1 = nullptr;
+    if (c->timing) {
+      r0 = c->take_event();
+      r1 = c->take_event();
+      HIPCHK(hipEventRecord(r0, s));
+    }
     hlc::launch_recover(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
                         dv->field_off + HLC_F_SIGNATURE, dv->field_off + HLC_F_OWNER, HLC_NFIELDS,
                         c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(), c->rec_lanes,
                         c->verify.as<uint8_t>(), drec, s);
+    if (c->timing) {
+      HIPCHK(hipEventRecord(r1, s));
+      c->rec_ev.emplace_back(r0, r1);
+    }
     hlc::launch_vote_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, now, c->pre.as<uint8_t>(),
                             c->pre_reason.as<uint8_t>(), c->verify.as<uint8_t>(), status, reason, s);
   }
@@ -202,6 +237,10 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
                           c->red.as<uint32_t>(), np, s);
   hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
   HIPCHK(hipGetLastError());
+  if (c->timing) {
+    HIPCHK(hipEventRecord(call1, s));
+    c->call_ev.emplace_back(call0, call1);
+  }
   return 0;
 }
 
@@ -303,6 +342,41 @@ int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, ui
   CHK(ctx->chain_tab.ensure(cap * 4));
   CHK(ctx->dup_tab.ensure(cap * 4));
   CHK(ctx->red.ensure(max_proposals * 16 + 16));
+  return 0;
+}
+
+int hlc_ctx_set_kernel_timing(hlc_ctx* ctx, int enable) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->timing = enable != 0;
+  return 0;
+}
+
+int hlc_ctx_take_kernel_time(hlc_ctx* ctx, double* recover_ms, uint64_t* recover_launches, double* call_ms,
+                             uint64_t* calls) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  double rsum = 0, csum = 0;
+  for (auto* vec : {&ctx->rec_ev, &ctx->call_ev}) {
+    for (auto& pr : *vec) {
+      HIPCHK(hipEventSynchronize(pr.second));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+      (vec == &ctx->rec_ev ? rsum : csum) += ms;
+    }
+  }
+  if (recover_ms) *recover_ms = rsum;
+  if (recover_launches) *recover_launches = ctx->rec_ev.size();
+  if (call_ms) *call_ms = csum;
+  if (calls) *calls = ctx->call_ev.size();
+  for (auto* vec : {&ctx->rec_ev, &ctx->call_ev}) {
+    for (auto& pr : *vec) {
+      ctx->ev_pool.push_back(pr.first);
+      ctx->ev_pool.push_back(pr.second);
+    }
+    vec->clear();
+  }
   return 0;
 }
 

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "hlc_modinv.hpp"
+
 #define HLC_DEV __device__ __forceinline__
 
 namespace hlc {
@@ -278,19 +280,8 @@ HLC_DEV void fe_chain223(const fe& a, fe& x2, fe& x3, fe& x22, fe& x223) {
   fe_mul(x223, t, x3);
 }
 
-// r = a^(p-2) = a^-1 (a != 0)
-HLC_DEV void fe_inv(fe& r, const fe& a) {
-  fe x2, x3, x22, x223, t;
-  fe_chain223(a, x2, x3, x22, x223);
-  fe_sqr_n(t, x223, 23);
-  fe_mul(t, t, x22);
-  fe_sqr_n(t, t, 5);
-  fe_mul(t, t, a);
-  fe_sqr_n(t, t, 3);
-  fe_mul(t, t, x2);
-  fe_sqr_n(t, t, 2);
-  fe_mul(r, t, a);
-}
+// r = a^-1 mod p (a != 0): safegcd divsteps (hlc_modinv.hpp), ~5x cheaper than a^(p-2)
+HLC_DEV void fe_inv(fe& r, const fe& a) { modinv_safegcd(r.v, a.v, modinfo_p()); }
 
 // r = a^((p+1)/4); returns whether r^2 == a (a is a quadratic residue)
 HLC_DEV bool fe_sqrt(fe& r, const fe& a) {
@@ -399,28 +390,15 @@ HLC_DEV void sc_r2(fe& r) {
   for (int i = 0; i < 8; ++i) r.v[i] = k[i];
 }
 
-// r = a^-1 * R mod n given am = a*R mod n (Montgomery in, Montgomery out), a != 0.
-// Fermat: a^(n-2), left-to-right 4-bit fixed window over the constant exponent.
-HLC_DEV void sc_mont_inv(fe& r, const fe& am) {
-  // n - 2 in 4-bit digits, most significant first
-  // n-2 = FFFFFFFF FFFFFFFF FFFFFFFF FFFFFFFE BAAEDCE6 AF48A03B BFD25E8C D036413F
-  const uint32_t e[8] = {0xD036413Fu, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
-                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  fe tab[16];
-  // tab[0] = R mod n (Montgomery one)
-  const uint32_t one[8] = {0x2FC9BEBFu, 0x402DA173u, 0x50B75FC4u, 0x45512319u, 1u, 0u, 0u, 0u};
-#pragma unroll
-  for (int i = 0; i < 8; ++i) tab[0].v[i] = one[i];
-  tab[1] = am;
-  for (int i = 2; i < 16; ++i) sc_mont_mul(tab[i], tab[i - 1], am);
-  fe acc = tab[0];
-  for (int w = 63; w >= 0; --w) {
-    for (int k = 0; k < 4; ++k) sc_mont_mul(acc, acc, acc);
-    uint32_t d = (e[w >> 3] >> (4 * (w & 7))) & 15u;
-    fe m = tab[d];  // dynamic index: small table, tolerable (scalar inversion is rare)
-    sc_mont_mul(acc, acc, m);
-  }
-  r = acc;
+// r = a^-1 mod n (a in [1, n)): safegcd divsteps
+HLC_DEV void sc_inv(fe& r, const fe& a) { modinv_safegcd(r.v, a.v, modinfo_n()); }
+
+// r = a*b mod n (plain domain) = mont(mont(a, b), R^2)
+HLC_DEV void sc_mul(fe& r, const fe& a, const fe& b) {
+  fe t, r2;
+  sc_mont_mul(t, a, b);
+  sc_r2(r2);
+  sc_mont_mul(r, t, r2);
 }
 
 // big-endian 32 bytes <-> limbs

@@ -49,6 +49,7 @@ void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, co
                     const uint32_t* gtab, uint32_t* scratch, uint64_t scratch_lanes,
                     uint8_t* verify_out, uint8_t* addr_out, hipStream_t s);
 uint64_t recover_grid_lanes();
+uint64_t recover_scratch_words();  // per-lane workspace words of k_recover
 void launch_build_gtab(uint32_t* gtab, hipStream_t s);
 
 // ---- validation tail ----

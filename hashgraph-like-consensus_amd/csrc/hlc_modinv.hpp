@@ -1,0 +1,209 @@
+// hlc_modinv.hpp -- modular inversion by Bernstein-Yang "safegcd" divsteps, 30-bit signed limbs.
+//
+// Constant-time formulation (20 batches x 30 divsteps = 600 >= 590, the bound for 256-bit
+// moduli with the half-delta variant), so every lane of a wave runs the same instruction
+// stream: no SIMT divergence.  Replaces the Fermat chains a^(m-2) that the recovery needs for
+// r^-1 mod n and Z^-1 mod p (k256 uses the same algorithm family since 0.13).
+//
+// Compiles for host and device (HLC_HD) so tests/ can check it exhaustively on the CPU
+// (hashgraph-like-consensus_amd/csrc/hlc_modinv_test.cpp).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define HLC_HD __host__ __device__ __forceinline__
+#else
+#define HLC_HD inline
+#endif
+
+namespace hlc {
+
+struct s30 {
+  int32_t v[9];  // value = sum v[i] * 2^(30 i); v[0..7] usually in [0, 2^30), v[8] signed
+};
+
+struct modinfo30 {
+  s30 modulus;
+  uint32_t modulus_inv30;  // modulus^-1 mod 2^30
+};
+
+static constexpr int32_t M30 = (int32_t)(0x3FFFFFFFu);
+
+// p = 2^256 - 2^32 - 977
+HLC_HD modinfo30 modinfo_p() {
+  modinfo30 m = {{{-0x3D1, -4, 0, 0, 0, 0, 0, 0, 65536}}, 0x2DDACACFu};
+  return m;
+}
+// n = group order
+HLC_HD modinfo30 modinfo_n() {
+  modinfo30 m = {{{0x10364141, 0x3F497A33, 0x348A03BB, 0x2BB739AB, -0x146, 0, 0, 0, 65536}}, 0x2A774EC1u};
+  return m;
+}
+
+// 8 x 32-bit little-endian limbs -> 9 x 30-bit limbs (value < 2^256)
+HLC_HD void to_s30(s30& r, const uint32_t a[8]) {
+  const uint32_t mask = 0x3FFFFFFFu;
+  r.v[0] = (int32_t)(a[0] & mask);
+  r.v[1] = (int32_t)(((a[0] >> 30) | (a[1] << 2)) & mask);
+  r.v[2] = (int32_t)(((a[1] >> 28) | (a[2] << 4)) & mask);
+  r.v[3] = (int32_t)(((a[2] >> 26) | (a[3] << 6)) & mask);
+  r.v[4] = (int32_t)(((a[3] >> 24) | (a[4] << 8)) & mask);
+  r.v[5] = (int32_t)(((a[4] >> 22) | (a[5] << 10)) & mask);
+  r.v[6] = (int32_t)(((a[5] >> 20) | (a[6] << 12)) & mask);
+  r.v[7] = (int32_t)(((a[6] >> 18) | (a[7] << 14)) & mask);
+  r.v[8] = (int32_t)(a[7] >> 16);
+}
+
+// 9 x 30-bit limbs (normalised: all in [0, 2^30), value < 2^256) -> 8 x 32-bit
+HLC_HD void from_s30(uint32_t r[8], const s30& a) {
+  const uint32_t* v = reinterpret_cast<const uint32_t*>(a.v);
+  r[0] = v[0] | (v[1] << 30);
+  r[1] = (v[1] >> 2) | (v[2] << 28);
+  r[2] = (v[2] >> 4) | (v[3] << 26);
+  r[3] = (v[3] >> 6) | (v[4] << 24);
+  r[4] = (v[4] >> 8) | (v[5] << 22);
+  r[5] = (v[5] >> 10) | (v[6] << 20);
+  r[6] = (v[6] >> 12) | (v[7] << 18);
+  r[7] = (v[7] >> 14) | (v[8] << 16);
+}
+
+struct trans2x2 {
+  int32_t u, v, q, r;
+};
+
+// 30 branch-free divsteps on the low bits of f and g; returns the updated zeta = -(delta+1/2).
+HLC_HD int32_t divsteps_30(int32_t zeta, uint32_t f0, uint32_t g0, trans2x2& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t f = f0, g = g0, x, y, z;
+  int32_t c1, c2;
+  for (int i = 0; i < 30; ++i) {
+    c1 = zeta >> 31;                 // delta > 0
+    c2 = -(int32_t)(g & 1u);         // g odd
+    x = (f ^ (uint32_t)c1) - (uint32_t)c1;
+    y = (u ^ (uint32_t)c1) - (uint32_t)c1;
+    z = (v ^ (uint32_t)c1) - (uint32_t)c1;
+    g += x & (uint32_t)c2;
+    q += y & (uint32_t)c2;
+    r += z & (uint32_t)c2;
+    c1 &= c2;
+    zeta = (zeta ^ c1) - 1;
+    f += g & (uint32_t)c1;
+    u += q & (uint32_t)c1;
+    v += r & (uint32_t)c1;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return zeta;
+}
+
+// [d, e] <- t [d, e] / 2^30 (mod modulus), keeping d, e in (-2 modulus, modulus)
+HLC_HD void update_de_30(s30& d, s30& e, const trans2x2& t, const modinfo30& mi) {
+  const int32_t u = t.u, v = t.v, q = t.q, r = t.r;
+  int32_t di, ei, md, me, sd, se;
+  int64_t cd, ce;
+  sd = d.v[8] >> 31;
+  se = e.v[8] >> 31;
+  md = (u & sd) + (v & se);
+  me = (q & sd) + (r & se);
+  di = d.v[0];
+  ei = e.v[0];
+  cd = (int64_t)u * di + (int64_t)v * ei;
+  ce = (int64_t)q * di + (int64_t)r * ei;
+  md -= (int32_t)((mi.modulus_inv30 * (uint32_t)cd + (uint32_t)md) & (uint32_t)M30);
+  me -= (int32_t)((mi.modulus_inv30 * (uint32_t)ce + (uint32_t)me) & (uint32_t)M30);
+  cd += (int64_t)mi.modulus.v[0] * md;
+  ce += (int64_t)mi.modulus.v[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; ++i) {
+    di = d.v[i];
+    ei = e.v[i];
+    cd += (int64_t)u * di + (int64_t)v * ei;
+    ce += (int64_t)q * di + (int64_t)r * ei;
+    cd += (int64_t)mi.modulus.v[i] * md;
+    ce += (int64_t)mi.modulus.v[i] * me;
+    d.v[i - 1] = (int32_t)cd & M30;
+    cd >>= 30;
+    e.v[i - 1] = (int32_t)ce & M30;
+    ce >>= 30;
+  }
+  d.v[8] = (int32_t)cd;
+  e.v[8] = (int32_t)ce;
+}
+
+// [f, g] <- t [f, g] / 2^30 (exact)
+HLC_HD void update_fg_30(s30& f, s30& g, const trans2x2& t) {
+  const int32_t u = t.u, v = t.v, q = t.q, r = t.r;
+  int32_t fi, gi;
+  int64_t cf, cg;
+  fi = f.v[0];
+  gi = g.v[0];
+  cf = (int64_t)u * fi + (int64_t)v * gi;
+  cg = (int64_t)q * fi + (int64_t)r * gi;
+  cf >>= 30;
+  cg >>= 30;
+#pragma unroll
+  for (int i = 1; i < 9; ++i) {
+    fi = f.v[i];
+    gi = g.v[i];
+    cf += (int64_t)u * fi + (int64_t)v * gi;
+    cg += (int64_t)q * fi + (int64_t)r * gi;
+    f.v[i - 1] = (int32_t)cf & M30;
+    cf >>= 30;
+    g.v[i - 1] = (int32_t)cg & M30;
+    cg >>= 30;
+  }
+  f.v[8] = (int32_t)cf;
+  g.v[8] = (int32_t)cg;
+}
+
+// r in (-2 modulus, modulus) -> [0, modulus), negated first if sign < 0
+HLC_HD void normalize_30(s30& r, int32_t sign, const modinfo30& mi) {
+  int32_t cond_add = r.v[8] >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] += mi.modulus.v[i] & cond_add;
+  int32_t cond_negate = sign >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = (r.v[i] ^ cond_negate) - cond_negate;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r.v[i + 1] += r.v[i] >> 30;
+    r.v[i] &= M30;
+  }
+  cond_add = r.v[8] >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] += mi.modulus.v[i] & cond_add;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r.v[i + 1] += r.v[i] >> 30;
+    r.v[i] &= M30;
+  }
+}
+
+// out = a^-1 mod modulus (a in [0, modulus), 8 x 32-bit limbs); a == 0 gives 0.
+HLC_HD void modinv_safegcd(uint32_t out[8], const uint32_t a[8], const modinfo30& mi) {
+  s30 d = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
+  s30 e = {{1, 0, 0, 0, 0, 0, 0, 0, 0}};
+  s30 f = mi.modulus;
+  s30 g;
+  to_s30(g, a);
+  int32_t zeta = -1;
+  for (int i = 0; i < 20; ++i) {
+    trans2x2 t;
+    zeta = divsteps_30(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    update_de_30(d, e, t, mi);
+    update_fg_30(f, g, t);
+  }
+  // f = +-1 now; result = d * sign(f)
+  normalize_30(d, f.v[8], mi);
+  from_s30(out, d);
+}
+
+}  // namespace hlc

@@ -8,6 +8,9 @@ namespace hlc {
 namespace {
 
 constexpr int REC_TPB = 256;
+#ifndef HLC_REC_WAVES
+#define HLC_REC_WAVES 4  // waves per SIMD the register allocator must admit for k_recover
+#endif
 
 __device__ __forceinline__ uint32_t load_be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
@@ -36,7 +39,7 @@ __device__ __forceinline__ void fe_from_digest(fe& r, const uint32_t* w) {
   for (int i = 0; i < 8; ++i) r.v[7 - i] = bswap32(w[i]);
 }
 
-__global__ void __launch_bounds__(REC_TPB) k_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
+__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
                                                      const uint8_t* bytes, const uint64_t* sig_off,
                                                      const uint64_t* id_off, size_t off_stride,
                                                      const uint32_t* gtab_g, uint32_t* scratch, uint64_t lanes,
@@ -280,7 +283,9 @@ __global__ void k_sign(uint64_t n, const uint8_t* priv, const uint32_t* z_digest
   fe r2c, km, kinv, rR, rd, t, s;
   sc_r2(r2c);
   sc_mont_mul(km, k, r2c);
-  sc_mont_inv(kinv, km);
+  fe kinv_plain;
+  sc_inv(kinv_plain, k);
+  sc_mont_mul(kinv, kinv_plain, r2c);  // k^-1 * R
   sc_mont_mul(rR, r, r2c);
   sc_mont_mul(rd, rR, d);
   sc_add(t, z, rd);
@@ -301,6 +306,8 @@ __global__ void k_sign(uint64_t n, const uint8_t* priv, const uint32_t* z_digest
 inline unsigned blocks_for(uint64_t n, int tpb) { return (unsigned)((n + tpb - 1) / tpb); }
 
 }  // namespace
+
+uint64_t recover_scratch_words() { return SCRATCH_WORDS; }
 
 uint64_t recover_grid_lanes() {
   int dev = 0, cus = 256, per_cu = 0;

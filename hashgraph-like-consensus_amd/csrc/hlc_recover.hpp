@@ -12,8 +12,14 @@
 // Scalar multiplication: GLV endomorphism (lambda, beta) splits u1 and u2 into 128-bit
 // halves; one shared doubling chain of 129 steps adds
 //   u1: width-8 wNAF over odd multiples of G and lambda*G (affine, LDS-resident, 8 KB/block)
-//   u2: width-5 wNAF over odd multiples of R and lambda*R (Jacobian, per-lane table kept in a
-//       lane-interleaved HBM/L2 workspace, 192 words per lane).
+//   u2: width-5 wNAF over odd multiples of R and lambda*R, per lane, kept in a lane-interleaved
+//       HBM/L2 workspace (128 words per lane).  The R table is built on the isomorphic curve
+//       y^2 = x^3 + 7 C^6 (C = Z(2R)) and brought to one common Z ("effective affine", as
+//       libsecp256k1's ecmult_odd_multiples_table + ge_table_set_globalz), so every addition of
+//       the main loop -- G, lambda G, R, lambda R -- is one mixed Jacobian+affine add
+//       (7M + 4S) through a single code path; the G entries are mapped into that frame with
+//       two multiplications by Zg^2, Zg^3.
+// Inversions (r^-1 mod n, final Z^-1 mod p) use safegcd divsteps (hlc_modinv.hpp).
 #pragma once
 #include "hlc_hash.hpp"
 #include "hlc_point.hpp"
@@ -25,8 +31,9 @@ constexpr int WNAF_R = 5;                       // window for R / lambda R
 constexpr int GTAB_N = 1 << (WNAF_G - 2);       // 64 odd multiples
 constexpr int RTAB_N = 1 << (WNAF_R - 2);       // 8 odd multiples
 constexpr int WNAF_WORDS = 33;                  // 132 digit slots (4 int8 per word) per half
-constexpr int RTAB_WORDS = RTAB_N * 24;         // per lane
-constexpr int SCRATCH_WORDS = RTAB_WORDS + 4 * WNAF_WORDS;  // per lane workspace
+constexpr int RTAB_WORDS = RTAB_N * 16;         // per lane (affine, common-Z frame)
+constexpr int ZR_OFF = RTAB_WORDS + 4 * WNAF_WORDS;           // z-ratios of the table build
+constexpr int SCRATCH_WORDS = ZR_OFF + 8 * (RTAB_N - 1);      // per lane workspace
 
 enum { SCHEME_NONE = 0, SCHEME_SIG_LEN = 1, SCHEME_ID_LEN = 2, SCHEME_BAD_PARITY = 3,
        SCHEME_SCALAR_RANGE = 4, SCHEME_NO_POINT = 5, SCHEME_INFINITY = 6 };
@@ -144,23 +151,63 @@ HLC_DEV void load_ge_lds(ge& g, const uint32_t* lds_tab, int idx) {
   g.y.v[4] = d.x; g.y.v[5] = d.y; g.y.v[6] = d.z; g.y.v[7] = d.w;
 }
 
-HLC_DEV void store_gej_ws(const gej& p, uint32_t* ws, size_t stride) {
+HLC_DEV void store_ge_ws(const fe& x, const fe& y, uint32_t* ws, size_t stride) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    ws[(size_t)i * stride] = p.x.v[i];
-    ws[(size_t)(8 + i) * stride] = p.y.v[i];
-    ws[(size_t)(16 + i) * stride] = p.z.v[i];
+    ws[(size_t)i * stride] = x.v[i];
+    ws[(size_t)(8 + i) * stride] = y.v[i];
   }
 }
 
-HLC_DEV void load_gej_ws(gej& p, const uint32_t* ws, size_t stride) {
+HLC_DEV void store_fe_ws(const fe& x, uint32_t* ws, size_t stride) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ws[(size_t)i * stride] = x.v[i];
+}
+
+HLC_DEV void load_fe_ws(fe& x, const uint32_t* ws, size_t stride) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x.v[i] = ws[(size_t)i * stride];
+}
+
+// a += b (b affine, a finite, a != +-b: used only for the R-table build where (2i-1)R and 2R
+// are distinct, non-opposite multiples of a point of prime order n); zr = Z(a') / Z(a) = 2H.
+HLC_DEV void gej_madd_zr(gej& a, const ge& b, fe& zr) {
+  fe z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+  fe_sqr(z1z1, a.z);
+  fe_mul(u2, b.x, z1z1);
+  fe_mul(s2, b.y, a.z);
+  fe_mul(s2, s2, z1z1);
+  fe_sub(h, u2, a.x);
+  fe_sub(rr, s2, a.y);
+  fe_sqr(hh, h);
+  fe_dbl(i4, hh);
+  fe_dbl(i4, i4);
+  fe_mul(j, h, i4);
+  fe_dbl(rr, rr);
+  fe_mul(v, a.x, i4);
+  fe_dbl(zr, h);
+  fe_mul(a.z, a.z, zr);
+  fe x3;
+  fe_sqr(x3, rr);
+  fe_sub(x3, x3, j);
+  fe_dbl(t, v);
+  fe_sub(x3, x3, t);
+  fe_sub(t, v, x3);
+  fe y3;
+  fe_mul(y3, rr, t);
+  fe_mul(t, a.y, j);
+  fe_dbl(t, t);
+  fe_sub(a.y, y3, t);
+  a.x = x3;
+  a.inf = 0;
+}
+
+HLC_DEV void load_ge_ws(ge& p, const uint32_t* ws, size_t stride) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     p.x.v[i] = ws[(size_t)i * stride];
     p.y.v[i] = ws[(size_t)(8 + i) * stride];
-    p.z.v[i] = ws[(size_t)(16 + i) * stride];
   }
-  p.inf = 0;
 }
 
 // Recovered address as 5 big-endian u32 words (bytes 12..31 of the keccak of X||Y).
@@ -227,95 +274,109 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
     if (!fe_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
     if ((int)(R.y.v[0] & 1u) != parity) fe_neg(R.y, R.y);
   }
-  // u1 = -z/r, u2 = s/r (mod n), Montgomery domain for the inversion
+  // u1 = -z/r, u2 = s/r (mod n)
   fe u1, u2;
   {
-    fe r2c, rm, rinv;
+    fe r2c, rinv, rinvR;
+    sc_inv(rinv, r);               // safegcd
     sc_r2(r2c);
-    sc_mont_mul(rm, r, r2c);     // r*R
-    sc_mont_inv(rinv, rm);       // r^-1 * R
-    sc_mont_mul(u2, s, rinv);    // s * r^-1
-    sc_mont_mul(u1, z, rinv);    // z * r^-1
+    sc_mont_mul(rinvR, rinv, r2c);  // r^-1 * R (Montgomery form)
+    sc_mont_mul(u2, s, rinvR);      // s * r^-1
+    sc_mont_mul(u1, z, rinvR);      // z * r^-1
     sc_neg(u1, u1);
   }
   // GLV halves + wNAF digits into the workspace
+  int negs;
   {
     fe a1, a2, b1, b2;
     bool na1, na2, nb1, nb2;
     glv_split(u1, a1, na1, a2, na2);
     glv_split(u2, b1, nb1, b2, nb2);
     uint32_t* dws = ws + (size_t)RTAB_WORDS * stride;
-    // fold sign flags into the digits: negate the magnitude's digits by storing -d
     wnaf_store<WNAF_G>(a1, dws + 0 * WNAF_WORDS * stride, stride);
     wnaf_store<WNAF_G>(a2, dws + 1 * WNAF_WORDS * stride, stride);
     wnaf_store<WNAF_R>(b1, dws + 2 * WNAF_WORDS * stride, stride);
     wnaf_store<WNAF_R>(b2, dws + 3 * WNAF_WORDS * stride, stride);
-    // sign flags packed into one word kept in a register below
-    parity = (na1 ? 1 : 0) | (na2 ? 2 : 0) | (nb1 ? 4 : 0) | (nb2 ? 8 : 0);
+    negs = (na1 ? 1 : 0) | (na2 ? 2 : 0) | (nb1 ? 4 : 0) | (nb2 ? 8 : 0);
   }
-  const int negs = parity;
-  // R table: odd multiples 1R, 3R, ..., 15R (Jacobian) in the workspace
+  // R table on the isomorphic curve with C = Z(2R): entries (2i+1)R, i < 8, common Z
+  fe zg, zg2, zg3;  // zg = real Z of the table frame
   {
-    gej cur, d2;
-    gej_set_ge(cur, R);
-    store_gej_ws(cur, ws, stride);
-    gej_double(d2, cur);
+    gej d;
+    gej_set_ge(d, R);
+    gej_double(d, d);  // 2R = (X, Y, C); on the iso curve it is the affine point (X, Y)
+    ge dp;
+    dp.x = d.x;
+    dp.y = d.y;
+    fe c2, c3;
+    fe_sqr(c2, d.z);
+    fe_mul(c3, c2, d.z);
+    gej acc;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve
+    fe_mul(acc.x, R.x, c2);
+    fe_mul(acc.y, R.y, c3);
+    fe_set(acc.z, 1);
+    store_ge_ws(acc.x, acc.y, ws, stride);
+    uint32_t* zrws = ws + (size_t)ZR_OFF * stride;
     for (int i = 1; i < RTAB_N; ++i) {
-      gej_add(cur, cur, d2);
-      store_gej_ws(cur, ws + (size_t)(24 * i) * stride, stride);
+      fe zr;
+      gej_madd_zr(acc, dp, zr);  // (2i+1)R, Z_i = Z_{i-1} * zr
+      store_ge_ws(acc.x, acc.y, ws + (size_t)(16 * i) * stride, stride);
+      store_fe_ws(zr, zrws + (size_t)(8 * (i - 1)) * stride, stride);
     }
+    // common Z = Z_7: entry i scaled by s_i = Z_7 / Z_i = prod_{k > i} zr_k
+    fe sc;
+    fe_set(sc, 1);
+    for (int i = RTAB_N - 2; i >= 0; --i) {
+      fe zr, s2, s3;
+      load_fe_ws(zr, zrws + (size_t)(8 * i) * stride, stride);  // zr_{i+1}
+      fe_mul(sc, sc, zr);
+      fe_sqr(s2, sc);
+      fe_mul(s3, s2, sc);
+      ge e;
+      load_ge_ws(e, ws + (size_t)(16 * i) * stride, stride);
+      fe_mul(e.x, e.x, s2);
+      fe_mul(e.y, e.y, s3);
+      store_ge_ws(e.x, e.y, ws + (size_t)(16 * i) * stride, stride);
+    }
+    fe_mul(zg, acc.z, d.z);  // real Z of the frame: Z_7 * C
+    fe_sqr(zg2, zg);
+    fe_mul(zg3, zg2, zg);
   }
   fe beta;
   fe_beta(beta);
   const uint32_t* dws = ws + (size_t)RTAB_WORDS * stride;
   gej acc;
   gej_set_inf(acc);
-  uint32_t wa1 = 0, wa2 = 0, wb1 = 0, wb2 = 0;
+  uint32_t wd[4] = {0, 0, 0, 0};
   for (int i = 128; i >= 0; --i) {
     const int q = i >> 2, b = i & 3;
     if (b == 3 || i == 128) {
-      wa1 = dws[(size_t)(0 * WNAF_WORDS + q) * stride];
-      wa2 = dws[(size_t)(1 * WNAF_WORDS + q) * stride];
-      wb1 = dws[(size_t)(2 * WNAF_WORDS + q) * stride];
-      wb2 = dws[(size_t)(3 * WNAF_WORDS + q) * stride];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wd[k] = dws[(size_t)(k * WNAF_WORDS + q) * stride];
     }
     gej_double(acc, acc);
-    int d;
-    d = digit_at(wa1, b);
-    if (d != 0) {
-      ge g;
-      int idx = ((d < 0 ? -d : d) - 1) >> 1;
-      load_ge_lds(g, gtab, idx);
-      if ((d < 0) != ((negs & 1) != 0)) fe_neg(g.y, g.y);
-      gej_add_ge(acc, acc, g);
-    }
-    d = digit_at(wa2, b);
-    if (d != 0) {
-      ge g;
-      int idx = ((d < 0 ? -d : d) - 1) >> 1;
-      load_ge_lds(g, gtab, GTAB_N + idx);
-      if ((d < 0) != ((negs & 2) != 0)) fe_neg(g.y, g.y);
-      gej_add_ge(acc, acc, g);
-    }
-    d = digit_at(wb1, b);
-    if (d != 0) {
-      gej p;
-      int idx = ((d < 0 ? -d : d) - 1) >> 1;
-      load_gej_ws(p, ws + (size_t)(24 * idx) * stride, stride);
-      if ((d < 0) != ((negs & 4) != 0)) fe_neg(p.y, p.y);
-      gej_add(acc, acc, p);
-    }
-    d = digit_at(wb2, b);
-    if (d != 0) {
-      gej p;
-      int idx = ((d < 0 ? -d : d) - 1) >> 1;
-      load_gej_ws(p, ws + (size_t)(24 * idx) * stride, stride);
-      fe_mul(p.x, p.x, beta);
-      if ((d < 0) != ((negs & 8) != 0)) fe_neg(p.y, p.y);
-      gej_add(acc, acc, p);
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t wk = k == 0 ? wd[0] : k == 1 ? wd[1] : k == 2 ? wd[2] : wd[3];
+      const int d = digit_at(wk, b);
+      if (d != 0) {
+        ge g;
+        const int idx = ((d < 0 ? -d : d) - 1) >> 1;
+        if (k < 2) {
+          load_ge_lds(g, gtab, k * GTAB_N + idx);
+          fe_mul(g.x, g.x, zg2);
+          fe_mul(g.y, g.y, zg3);
+        } else {
+          load_ge_ws(g, ws + (size_t)(16 * idx) * stride, stride);
+          if (k == 3) fe_mul(g.x, g.x, beta);
+        }
+        if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
+        gej_add_ge(acc, acc, g);
+      }
     }
   }
   if (acc.inf) return SCHEME_INFINITY;
+  fe_mul(acc.z, acc.z, zg);  // back to the real curve
   fe qx, qy;
   gej_to_affine(qx, qy, acc);
   pubkey_address(qx, qy, addr);

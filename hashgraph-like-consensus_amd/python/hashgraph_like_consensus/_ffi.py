@@ -11,7 +11,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_uint8, c_uint32, c_uint64, c_void_p
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhlc.so")
+LIB_PATH = os.environ.get("HLC_LIB") or os.path.join(PKG_ROOT, "lib", "libhlc.so")
 
 HLC_NFIELDS = 5
 F_OWNER, F_PARENT, F_RECEIVED, F_VOTE_HASH, F_SIGNATURE = range(5)
@@ -93,6 +93,7 @@ EXPORTED_SYMBOLS = (
     "hlc_ctx_create", "hlc_ctx_destroy", "hlc_ctx_reserve", "hlc_last_error", "hlc_abi_version",
     "hlc_compute_vote_hashes", "hlc_eth_verify_batch", "hlc_validate_proposals",
     "hlc_validate_proposals_device", "hlc_eth_address_batch", "hlc_eth_sign_batch",
+    "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time",
 )
 
 _lib = None
@@ -138,6 +139,10 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_eth_address_batch.restype = c_int
     lib.hlc_eth_sign_batch.argtypes = [vp, c_uint64, u8p, u8p, c_uint64, u64p, u32p, u8p]
     lib.hlc_eth_sign_batch.restype = c_int
+    lib.hlc_ctx_set_kernel_timing.argtypes = [vp, c_int]
+    lib.hlc_ctx_set_kernel_timing.restype = c_int
+    lib.hlc_ctx_take_kernel_time.argtypes = [vp, POINTER(ctypes.c_double), u64p, POINTER(ctypes.c_double), u64p]
+    lib.hlc_ctx_take_kernel_time.restype = c_int
     _lib = lib
     return lib
 

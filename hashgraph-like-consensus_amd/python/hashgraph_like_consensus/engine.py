@@ -127,3 +127,23 @@ class Engine:
             self.ctx, n, _ffi.ptr(priv, c_uint8), _ffi.ptr(arena, c_uint8), total, _ffi.ptr(off, c_uint64),
             _ffi.ptr(lens, c_uint32), _ffi.ptr(out, c_uint8)))
         return out[:n]
+
+    # ---- device-resident path (inputs already in HBM) -----------------------------------
+    def validate_proposals_device(self, dbatch, stream_handle: int = 0) -> None:
+        """hlc_validate_proposals_device over a `device.DeviceBatch` (all pointers in HBM);
+        enqueued on `stream_handle` (a hipStream_t as int; 0 = the context's stream)."""
+        _ffi.check(self.lib.hlc_validate_proposals_device(
+            self.ctx, ctypes.byref(dbatch.view), dbatch.props_ptr, dbatch.n_proposals, dbatch.now,
+            dbatch.results_ptr, dbatch.status_ptr, dbatch.reason_ptr, None,
+            c_void_p(stream_handle) if stream_handle else None))
+
+    def set_kernel_timing(self, enable: bool) -> None:
+        _ffi.check(self.lib.hlc_ctx_set_kernel_timing(self.ctx, 1 if enable else 0))
+
+    def take_kernel_time(self):
+        """-> (recover_ms, recover_launches, call_ms, calls) since the previous take."""
+        rms, cms = ctypes.c_double(), ctypes.c_double()
+        rl, cl = c_uint64(), c_uint64()
+        _ffi.check(self.lib.hlc_ctx_take_kernel_time(self.ctx, ctypes.byref(rms), ctypes.byref(rl),
+                                                     ctypes.byref(cms), ctypes.byref(cl)))
+        return rms.value, rl.value, cms.value, cl.value

@@ -130,6 +130,15 @@ int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, ui
 const char* hlc_last_error(void);
 int hlc_abi_version(void);
 
+/* ---- Measurement hooks (bench.py roofline): HIP events on the launch stream ------ */
+/* enable != 0: every validate-many call records hipEvents around the signature-recovery
+ * kernel (k_recover) and around the whole call, on the stream the kernels run on. */
+int hlc_ctx_set_kernel_timing(hlc_ctx* ctx, int enable);
+/* Waits for the recorded events, returns the summed device time (ms) and launch count of
+ * k_recover and of whole validate-many calls since the previous take, then resets them. */
+int hlc_ctx_take_kernel_time(hlc_ctx* ctx, double* recover_ms, uint64_t* recover_launches,
+                             double* call_ms, uint64_t* calls);
+
 /* ---- Hot-path entry points (host buffers, blocking) ----------------------------- */
 
 /* Replaces `utils::compute_vote_hash` (utils.rs:37-47) over a batch: out[n][32]. */
