@@ -71,7 +71,7 @@ void launch_address(uint64_t n, const uint8_t* priv, const uint32_t* fbtab, uint
 void launch_sign(uint64_t n, const uint8_t* priv, const uint32_t* z_digest, const uint32_t* fbtab,
                  uint8_t* sig, hipStream_t s);
 
-constexpr size_t GTAB_WORDS = 2 * 64 * 16;      // odd multiples of G and lambda*G, affine
+constexpr size_t GTAB_WORDS = 2 * 128 * 16;     // odd multiples 1..255 of G and lambda*G, affine
 constexpr size_t FBTAB_WORDS = 32 * 256 * 16;   // fixed-base comb: 32 windows x 256 affine points
 
 }  // namespace hlc

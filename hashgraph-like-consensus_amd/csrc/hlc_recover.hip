@@ -94,7 +94,7 @@ __device__ void scalar_mul_g(gej& acc, const fe& k) {
   }
 }
 
-// odd multiples (2i+1)G and lambda*(2i+1)G, i < 64, affine
+// odd multiples (2i+1)G and lambda*(2i+1)G, i < GTAB_N, affine
 __global__ void k_build_gtab(uint32_t* gtab) {
   int i = threadIdx.x;
   if (i >= GTAB_N) return;
@@ -331,7 +331,7 @@ void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, co
 }
 
 void launch_build_gtab(uint32_t* gtab, hipStream_t s) {
-  hipLaunchKernelGGL(k_build_gtab, dim3(1), dim3(64), 0, s, gtab);
+  hipLaunchKernelGGL(k_build_gtab, dim3(1), dim3(GTAB_N), 0, s, gtab);
 }
 
 void launch_build_fbtab(uint32_t* fbtab, hipStream_t s) {

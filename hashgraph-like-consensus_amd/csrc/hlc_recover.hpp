@@ -26,14 +26,24 @@
 
 namespace hlc {
 
-constexpr int WNAF_G = 8;                       // window for G / lambda G
-constexpr int WNAF_R = 5;                       // window for R / lambda R
-constexpr int GTAB_N = 1 << (WNAF_G - 2);       // 64 odd multiples
-constexpr int RTAB_N = 1 << (WNAF_R - 2);       // 8 odd multiples
-constexpr int WNAF_WORDS = 33;                  // 132 digit slots (4 int8 per word) per half
+// Fixed-window "regular" signed-digit recoding (every digit odd, never zero): every lane adds at
+// the same bit positions, so a wave executes exactly one addition per window and half-scalar.
+// (A sparse wNAF is useless in SIMT: a wave runs an addition whenever ANY of its 64 lanes has a
+// non-zero digit, i.e. at nearly every position -- measured 3.0M VALU instructions per vote.)
+constexpr int W_G = 8;                          // window for G / lambda G (u1 halves)
+constexpr int W_R = 5;                          // window for R / lambda R (u2 halves)
+constexpr int M_G = 17;                         // windows: 17 * 8 = 136 >= 129 bits
+constexpr int M_R = 26;                         // windows: 26 * 5 = 130 >= 129 bits
+constexpr int TOP_BIT = 128;                    // first (most significant) chain position
+constexpr int GTAB_N = 1 << (W_G - 1);          // 128 odd multiples 1..255 (LDS, shared)
+constexpr int RTAB_N = 1 << (W_R - 1);          // 16 odd multiples 1..31 (per lane)
+constexpr int DIG_G_WORDS = (M_G + 1) / 2;      // int16 digits, 2 per word
+constexpr int DIG_R_WORDS = (M_R + 1) / 2;
 constexpr int RTAB_WORDS = RTAB_N * 16;         // per lane (affine, common-Z frame)
-constexpr int ZR_OFF = RTAB_WORDS + 4 * WNAF_WORDS;           // z-ratios of the table build
-constexpr int SCRATCH_WORDS = ZR_OFF + 8 * (RTAB_N - 1);      // per lane workspace
+constexpr int DIG_OFF = RTAB_WORDS;             // digits: a1, a2 (G), b1, b2 (R)
+constexpr int DIG_WORDS = 2 * DIG_G_WORDS + 2 * DIG_R_WORDS;
+constexpr int ZR_OFF = DIG_OFF + DIG_WORDS;     // z-ratios of the table build
+constexpr int SCRATCH_WORDS = ZR_OFF + 8 * (RTAB_N - 1);  // per lane workspace words
 
 enum { SCHEME_NONE = 0, SCHEME_SIG_LEN = 1, SCHEME_ID_LEN = 2, SCHEME_BAD_PARITY = 3,
        SCHEME_SCALAR_RANGE = 4, SCHEME_NO_POINT = 5, SCHEME_INFINITY = 6 };
@@ -106,41 +116,48 @@ HLC_DEV void glv_split(const fe& k, fe& k1, bool& neg1, fe& k2, bool& neg2) {
   fe_cmov(k2, m2, neg2);
 }
 
-// Width-W wNAF of a (< 2^129) value, LSB first, 4 signed int8 digits per word; written to a
-// lane-interleaved workspace column (word q of this lane at ws[q * stride]).
-template <int W>
-HLC_DEV void wnaf_store(const fe& k, uint32_t* ws, size_t stride) {
+// Regular signed-digit recoding of k (< 2^129): k' = k | 1 (skew = 1 if k was even) written as
+// sum d_i 2^(W i), i < M, every d_i odd with |d_i| < 2^W.  Digits go to the lane's workspace
+// column as int16 pairs.  Returns the skew.
+template <int W, int M>
+HLC_DEV uint32_t recode_regular(const fe& k, uint32_t* ws, size_t stride) {
   uint32_t x0 = k.v[0], x1 = k.v[1], x2 = k.v[2], x3 = k.v[3], x4 = k.v[4];
-  for (int q = 0; q < WNAF_WORDS; ++q) {
+  const uint32_t skew = (x0 & 1u) ^ 1u;
+  x0 |= 1u;
+#pragma unroll
+  for (int q = 0; q < (M + 1) / 2; ++q) {
     uint32_t packed = 0;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int h = 0; h < 2; ++h) {
+      const int i = 2 * q + h;
       int d = 0;
-      if (x0 & 1u) {
-        d = (int)(x0 & ((1u << W) - 1u));
-        if (d >= (1 << (W - 1))) d -= (1 << W);
-        // x -= d (two's complement add of -d over 160 bits)
-        uint32_t nd = (uint32_t)(-d);
-        uint32_t ext = (d > 0) ? 0xFFFFFFFFu : 0u;
+      if (i < M - 1) {
+        d = (int)(x0 & ((1u << (W + 1)) - 1u)) - (1 << W);
+        // x -= d, then x >>= W (x - d == 2^W mod 2^(W+1), so the quotient stays odd)
+        const uint32_t nd = (uint32_t)(-d);
+        const uint32_t ext = d > 0 ? 0xFFFFFFFFu : 0u;
         uint32_t c = 0;
         x0 = add_cc(x0, nd, c);
         x1 = add_cc(x1, ext, c);
         x2 = add_cc(x2, ext, c);
         x3 = add_cc(x3, ext, c);
         x4 = add_cc(x4, ext, c);
+        x0 = __builtin_amdgcn_alignbit(x1, x0, W);
+        x1 = __builtin_amdgcn_alignbit(x2, x1, W);
+        x2 = __builtin_amdgcn_alignbit(x3, x2, W);
+        x3 = __builtin_amdgcn_alignbit(x4, x3, W);
+        x4 = x4 >> W;
+      } else if (i == M - 1) {
+        d = (int)x0;  // remaining value: small and odd
       }
-      packed |= ((uint32_t)(d & 0xFF)) << (8 * b);
-      x0 = __builtin_amdgcn_alignbit(x1, x0, 1);
-      x1 = __builtin_amdgcn_alignbit(x2, x1, 1);
-      x2 = __builtin_amdgcn_alignbit(x3, x2, 1);
-      x3 = __builtin_amdgcn_alignbit(x4, x3, 1);
-      x4 = x4 >> 1;
+      packed |= ((uint32_t)d & 0xFFFFu) << (16 * h);
     }
     ws[(size_t)q * stride] = packed;
   }
+  return skew;
 }
 
-HLC_DEV int digit_at(uint32_t word, int b) { return (int)(int8_t)(word >> (8 * b)); }
+HLC_DEV int digit16(uint32_t word, int h) { return (int)(int16_t)(word >> (16 * h)); }
 
 HLC_DEV void load_ge_lds(ge& g, const uint32_t* lds_tab, int idx) {
   const uint4* p = reinterpret_cast<const uint4*>(lds_tab + idx * 16);
@@ -285,19 +302,20 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
     sc_mont_mul(u1, z, rinvR);      // z * r^-1
     sc_neg(u1, u1);
   }
-  // GLV halves + wNAF digits into the workspace
-  int negs;
+  // GLV halves + regular digits into the workspace
+  int negs, skews;
   {
     fe a1, a2, b1, b2;
     bool na1, na2, nb1, nb2;
     glv_split(u1, a1, na1, a2, na2);
     glv_split(u2, b1, nb1, b2, nb2);
-    uint32_t* dws = ws + (size_t)RTAB_WORDS * stride;
-    wnaf_store<WNAF_G>(a1, dws + 0 * WNAF_WORDS * stride, stride);
-    wnaf_store<WNAF_G>(a2, dws + 1 * WNAF_WORDS * stride, stride);
-    wnaf_store<WNAF_R>(b1, dws + 2 * WNAF_WORDS * stride, stride);
-    wnaf_store<WNAF_R>(b2, dws + 3 * WNAF_WORDS * stride, stride);
+    uint32_t* dws = ws + (size_t)DIG_OFF * stride;
+    uint32_t s0 = recode_regular<W_G, M_G>(a1, dws, stride);
+    uint32_t s1 = recode_regular<W_G, M_G>(a2, dws + (size_t)DIG_G_WORDS * stride, stride);
+    uint32_t s2 = recode_regular<W_R, M_R>(b1, dws + (size_t)(2 * DIG_G_WORDS) * stride, stride);
+    uint32_t s3 = recode_regular<W_R, M_R>(b2, dws + (size_t)(2 * DIG_G_WORDS + DIG_R_WORDS) * stride, stride);
     negs = (na1 ? 1 : 0) | (na2 ? 2 : 0) | (nb1 ? 4 : 0) | (nb2 ? 8 : 0);
+    skews = (int)(s0 | (s1 << 1) | (s2 << 2) | (s3 << 3));
   }
   // R table on the isomorphic curve with C = Z(2R): entries (2i+1)R, i < 8, common Z
   fe zg, zg2, zg3;  // zg = real Z of the table frame
@@ -344,36 +362,49 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
   }
   fe beta;
   fe_beta(beta);
-  const uint32_t* dws = ws + (size_t)RTAB_WORDS * stride;
+  const uint32_t* dws = ws + (size_t)DIG_OFF * stride;
   gej acc;
   gej_set_inf(acc);
-  uint32_t wd[4] = {0, 0, 0, 0};
-  for (int i = 128; i >= 0; --i) {
-    const int q = i >> 2, b = i & 3;
-    if (b == 3 || i == 128) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) wd[k] = dws[(size_t)(k * WNAF_WORDS + q) * stride];
-    }
-    gej_double(acc, acc);
+  for (int i = TOP_BIT; i >= 0; --i) {
+    if (i != TOP_BIT) gej_double(acc, acc);
+    // half k adds at positions that are multiples of its window (uniform across the wave)
 #pragma unroll 1
     for (int k = 0; k < 4; ++k) {
-      const uint32_t wk = k == 0 ? wd[0] : k == 1 ? wd[1] : k == 2 ? wd[2] : wd[3];
-      const int d = digit_at(wk, b);
-      if (d != 0) {
-        ge g;
-        const int idx = ((d < 0 ? -d : d) - 1) >> 1;
-        if (k < 2) {
-          load_ge_lds(g, gtab, k * GTAB_N + idx);
-          fe_mul(g.x, g.x, zg2);
-          fe_mul(g.y, g.y, zg3);
-        } else {
-          load_ge_ws(g, ws + (size_t)(16 * idx) * stride, stride);
-          if (k == 3) fe_mul(g.x, g.x, beta);
-        }
-        if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
-        gej_add_ge(acc, acc, g);
+      const bool isg = k < 2;
+      const int w = isg ? W_G : W_R;
+      if (i % w != 0) continue;
+      const int win = i / w;
+      const size_t base = isg ? (size_t)(k * DIG_G_WORDS) : (size_t)(2 * DIG_G_WORDS + (k - 2) * DIG_R_WORDS);
+      const int d = digit16(dws[(base + (size_t)(win >> 1)) * stride], win & 1);
+      const int idx = ((d < 0 ? -d : d) - 1) >> 1;
+      ge g;
+      if (isg) {
+        load_ge_lds(g, gtab, k * GTAB_N + idx);
+        fe_mul(g.x, g.x, zg2);
+        fe_mul(g.y, g.y, zg3);
+      } else {
+        load_ge_ws(g, ws + (size_t)(16 * idx) * stride, stride);
+        if (k == 3) fe_mul(g.x, g.x, beta);
       }
+      if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
+      gej_add_ge(acc, acc, g);
     }
+  }
+  // skew corrections: the digits encoded |k| + 1 for even |k|; subtract one (signed) base point
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {
+    if (((skews >> k) & 1) == 0) continue;
+    ge g;
+    if (k < 2) {
+      load_ge_lds(g, gtab, k * GTAB_N);
+      fe_mul(g.x, g.x, zg2);
+      fe_mul(g.y, g.y, zg3);
+    } else {
+      load_ge_ws(g, ws, stride);
+      if (k == 3) fe_mul(g.x, g.x, beta);
+    }
+    if (((negs >> k) & 1) == 0) fe_neg(g.y, g.y);  // add -(sign * P)
+    gej_add_ge(acc, acc, g);
   }
   if (acc.inf) return SCHEME_INFINITY;
   fe_mul(acc.z, acc.z, zg);  // back to the real curve

@@ -1,0 +1,182 @@
+"""a config-2-shaped workload with ~1/3 Byzantine votes, split evenly
+over the mutation kinds below, built with the CPU restatements (test infrastructure).
+
+Mutation kinds (expected first outcome in brackets):
+  wrong_key     signed by another key                        [InvalidVoteSignature]
+  flip_rs       one bit of r or s flipped                     [InvalidVoteSignature / scheme]
+  bad_v         v in {2, 29, 34}                               [SignatureScheme: parity]
+  high_s        s -> n - s, parity flipped (still valid)      [Ok]
+  no_point      r with x^3+7 a non-residue                    [SignatureScheme: no point]
+  infinity      crafted R = kG, s = z/k  =>  Q = infinity     [SignatureScheme: infinity]
+  tamper_hash   vote_hash bit flipped                         [InvalidVoteHash]
+  bad_received  received_hash replaced, vote re-hashed+signed [ReceivedHashMismatch]
+  parent_other  parent_hash -> another owner's vote, re-signed [ParentHashMismatch]
+  ts_regress    timestamp below the previous vote, re-signed  [ReceivedHashMismatch]
+  ts_old        timestamp before proposal creation, re-signed [TimestampOlderThanCreationTime]
+  duplicate     a second vote by an earlier voter, re-signed  [DuplicateVote]
+  wrong_pid     proposal_id changed, re-signed                [VoteProposalIdMismatch]
+  empty         owner / vote_hash / signature emptied         [Empty*]
+  sig_len       signature truncated / extended                [SignatureScheme: length]
+"""
+from __future__ import annotations
+
+import random
+from typing import List, Tuple
+
+import numpy as np
+
+import coracle
+import pyoracle as po
+from hashgraph_like_consensus.batch import pack_votes
+
+KINDS = ["wrong_key", "flip_rs", "bad_v", "high_s", "no_point", "infinity", "tamper_hash", "bad_received",
+         "parent_other", "ts_regress", "ts_old", "duplicate", "wrong_pid", "empty", "sig_len"]
+
+
+def batch_to_votes(batch) -> List[po.Vote]:
+    out = []
+    for i in range(batch.n):
+        f = [batch.field(i, k) for k in range(5)]
+        out.append(po.Vote(vote_id=int(batch.vote_id[i]), vote_owner=f[0], proposal_id=int(batch.proposal_id[i]),
+                           timestamp=int(batch.timestamp[i]), vote=bool(batch.vote[i]), parent_hash=f[1],
+                           received_hash=f[2], vote_hash=f[3], signature=f[4]))
+    return out
+
+
+def c_sign(priv: int, v: po.Vote) -> bytes:
+    h = coracle.eip191_hash(po.signed_payload(v))
+    key = np.frombuffer(priv.to_bytes(32, "big"), np.uint8).reshape(1, 32)
+    return coracle.sign_batch(key, np.frombuffer(h, np.uint8).reshape(1, 32), 1)[0].tobytes()
+
+
+def resign(v: po.Vote, priv: int, rehash: bool = True) -> None:
+    if rehash:
+        v.vote_hash = po.compute_vote_hash(v)
+    v.signature = b""
+    v.signature = c_sign(priv, v)
+
+
+_NO_POINT_R = None
+
+
+def no_point_r() -> int:
+    global _NO_POINT_R
+    if _NO_POINT_R is None:
+        r = 2**255 + 12345
+        while po.decompress(r, False) is not None:
+            r += 1
+        _NO_POINT_R = r
+    return _NO_POINT_R
+
+
+def mutate(votes: List[po.Vote], privs: List[int], i: int, j: int, kind: str, rnd: random.Random,
+           begin: int) -> None:
+    """Mutate votes[i] (index j within its proposal starting at `begin`)."""
+    v = votes[i]
+    priv = privs[i]
+    if kind == "wrong_key":
+        v.signature = c_sign(rnd.randrange(1, po.N), v)
+    elif kind == "flip_rs":
+        s = bytearray(v.signature)
+        s[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+        v.signature = bytes(s)
+    elif kind == "bad_v":
+        s = bytearray(v.signature)
+        s[64] = rnd.choice([2, 29, 34])
+        v.signature = bytes(s)
+    elif kind == "high_s":
+        s = bytearray(v.signature)
+        sv = int.from_bytes(s[32:64], "big")
+        s[32:64] = (po.N - sv).to_bytes(32, "big")
+        s[64] = 55 - s[64]
+        v.signature = bytes(s)
+    elif kind == "no_point":
+        s = bytearray(v.signature)
+        s[0:32] = no_point_r().to_bytes(32, "big")
+        v.signature = bytes(s)
+    elif kind == "infinity":
+        z = int.from_bytes(coracle.eip191_hash(po.signed_payload(v)), "big") % po.N
+        k = rnd.randrange(1, po.N)
+        R = po.point_mul(k, po.G)
+        r = R[0] % po.N
+        s = z * pow(k, -1, po.N) % po.N
+        if s == 0:
+            s = 1
+        v.signature = r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([27 + (R[1] & 1)])
+    elif kind == "tamper_hash":
+        h = bytearray(v.vote_hash)
+        h[rnd.randrange(32)] ^= 0x10
+        v.vote_hash = bytes(h)
+    elif kind == "bad_received":
+        v.received_hash = bytes(rnd.randrange(256) for _ in range(32))
+        resign(v, priv)
+    elif kind == "parent_other":
+        if j >= 2:
+            other = votes[begin + rnd.randrange(j - 1)]
+            v.parent_hash = other.vote_hash
+        else:
+            v.parent_hash = bytes(32)
+        resign(v, priv)
+    elif kind == "ts_regress":
+        v.timestamp = max(votes[i - 1].timestamp - 1, 0) if j > 0 else v.timestamp
+        resign(v, priv)
+    elif kind == "ts_old":
+        v.timestamp = v.timestamp - 10_000
+        resign(v, priv)
+    elif kind == "duplicate":
+        if j >= 1:
+            src = begin + rnd.randrange(j)
+            v.vote_owner = votes[src].vote_owner
+            privs[i] = privs[src]
+            resign(v, privs[i])
+    elif kind == "wrong_pid":
+        v.proposal_id = (v.proposal_id + 1) & 0xFFFFFFFF
+        resign(v, priv)
+    elif kind == "empty":
+        which = rnd.randrange(3)
+        if which == 0:
+            v.vote_owner = b""
+        elif which == 1:
+            v.vote_hash = b""
+        else:
+            v.signature = b""
+    elif kind == "sig_len":
+        v.signature = v.signature[:64] if rnd.random() < 0.5 else v.signature + b"\x00"
+    else:
+        raise ValueError(kind)
+
+
+def byzantine(workload, fraction: float = 1 / 3, seed: int = 5) -> Tuple[object, np.ndarray, List[str]]:
+    """-> (VoteBatch with mutations, desc, per-vote kind or '')."""
+    rnd = random.Random(seed)
+    votes = batch_to_votes(workload.batch)
+    privs = [int.from_bytes(bytes(k), "big") for k in workload.priv]
+    kinds = [""] * len(votes)
+    desc = workload.desc
+    k = 0
+    for p in range(desc.shape[0]):
+        b, c = int(desc[p]["vote_begin"]), int(desc[p]["vote_count"])
+        for j in range(c):
+            if rnd.random() < fraction:
+                kind = KINDS[k % len(KINDS)]
+                k += 1
+                mutate(votes, privs, b + j, j, kind, rnd, b)
+                kinds[b + j] = kind
+    return pack_votes(votes), desc, kinds
+
+
+def proposals_from_batch(batch, desc) -> List[po.Proposal]:
+    votes = batch_to_votes(batch)
+    out = []
+    for d in desc:
+        b, c = int(d["vote_begin"]), int(d["vote_count"])
+        out.append(po.Proposal(proposal_id=int(d["proposal_id"]), votes=votes[b:b + c],
+                               expected_voters_count=int(d["expected_voters_count"]), timestamp=int(d["timestamp"]),
+                               expiration_timestamp=int(d["expiration_timestamp"]),
+                               liveness_criteria_yes=bool(d["liveness_criteria_yes"])))
+    return out
+
+
+def config_of(d) -> po.ConsensusConfig:
+    return po.ConsensusConfig(float(d["consensus_threshold"]), int(d["max_rounds"]), bool(d["use_gossipsub_rounds"]),
+                              bool(d["liveness_criteria_yes"]))
