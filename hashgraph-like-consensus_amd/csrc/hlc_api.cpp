@@ -96,7 +96,7 @@ struct hlc_ctx {
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   }
   DBuf vote_prop, sha_sz, sha_off, kec_sz, kec_off, sha_buf, kec_buf, sha_dig, kec_dig, pre, pre_reason,
-      verify, status, reason, chain_code, chain_tab, dup_tab, red, scan_tmp, totals;
+      verify, status, reason, chain_code, chain_tab, dup_tab, red, scan_tmp, totals, flag;
 };
 
 namespace {
@@ -199,12 +199,22 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     reason = c->reason.as<uint8_t>();
   }
   if (n) {
-    CHK(run_prehash(c, dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
     CHK(c->pre.ensure(n));
     CHK(c->pre_reason.ensure(n));
     CHK(c->verify.ensure(n));
-    hlc::launch_pre_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->sha_dig.as<uint32_t>(),
-                           c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
+    CHK(c->kec_dig.ensure(n * 32));
+    CHK(c->flag.ensure(16));
+    HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(uint32_t), s));
+    hlc::launch_prehash_fused(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->kec_dig.as<uint32_t>(),
+                              c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
+    uint32_t general = 0;
+    HIPCHK(hipMemcpyAsync(&general, c->flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (general) {  // some votes exceed the LDS window: general global-memory pipeline for those
+      CHK(run_prehash(c, dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
+      hlc::launch_pre_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->sha_dig.as<uint32_t>(),
+                             c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
+    }
     CHK(ensure_recover_scratch(c));
     if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
     hipEvent_t r0 = nullptr, r1 = nullptr;

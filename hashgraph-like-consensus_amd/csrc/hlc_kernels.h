@@ -13,6 +13,7 @@ constexpr uint32_t EMPTY_SLOT = 0xFFFFFFFFu;
 // pre_status values beyond the public HLC_* codes
 constexpr uint8_t PRE_PENDING = 0xFE;  // needs signature recovery
 constexpr uint8_t PRE_SKIP = 0xFF;     // vote not covered by any proposal
+constexpr uint8_t PRE_GENERAL = 0xFD;  // too long for the fused LDS path: general pipeline decides
 
 // message-building modes
 enum MsgMode { MSG_VOTE = 0, MSG_PAYLOAD = 1 };
@@ -38,6 +39,11 @@ void launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* 
 // hlc_eth_verify_batch length checks (ethereum.rs:71-82): pre[i] = PRE_PENDING or verify_out set
 void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
                        uint8_t* verify_out, hipStream_t s);
+// fused byte stage (sizes + SHA-256 compare + EIP-191 keccak + pre-status) for votes whose
+// messages fit the per-lane LDS window; others get PRE_GENERAL and *general is set non-zero
+void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                          uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason, uint32_t* general, hipStream_t s);
+// general-path pre-status: decides only the votes marked PRE_GENERAL
 void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                        const uint32_t* sha_digest, uint8_t* pre, uint8_t* pre_reason, hipStream_t s);
 

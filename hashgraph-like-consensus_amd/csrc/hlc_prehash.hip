@@ -214,6 +214,7 @@ __global__ void k_pre_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop,
                              const uint32_t* sha, uint8_t* pre, uint8_t* pre_reason) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (pre[i] != PRE_GENERAL) return;  // decided by k_prehash_fused
   uint8_t st, rs = 0;
   uint32_t p = vote_prop ? vote_prop[i] : 0;
   if (vote_prop && p == NO_PROP) {
@@ -464,6 +465,159 @@ __global__ void k_finalize(const hlc_proposal* props, uint64_t np, uint64_t now,
   out[p] = r;
 }
 
+// ---------------- fused fast path: one kernel for the whole byte stage ----------------
+// Per lane, the SHA-256 input of compute_vote_hash and then the EIP-191 message of the
+// prost-encoded vote are materialised in a private LDS window (FBUF bytes, enough for every
+// canonical vote and for fields up to ~80 B) and hashed straight from it: no global scratch, no
+// size scan, no host round trip.  Votes whose messages do not fit are flagged PRE_GENERAL and
+// handled by the general pipeline above (same semantics, global-memory staging).
+constexpr int FUSED_TPB = 128;
+constexpr int FBUF = 280;  // bytes per lane; 70 words: conflict-free ds_read_b32/b64 across lanes
+
+struct LdsCursor {
+  uint8_t* o;
+  uint32_t pos;
+  __device__ void put(uint8_t b) { o[pos++] = b; }
+  __device__ void put_varint(uint64_t x) {
+    do {
+      uint8_t b = x & 0x7F;
+      x >>= 7;
+      put(x ? (b | 0x80) : b);
+    } while (x);
+  }
+  __device__ void put_bytes(const uint8_t* p, uint32_t n) {
+    for (uint32_t k = 0; k < n; ++k) put(p[k]);
+  }
+  __device__ void put_le(uint64_t x, int nbytes) {
+    for (int k = 0; k < nbytes; ++k) put((uint8_t)(x >> (8 * k)));
+  }
+};
+
+__global__ void __launch_bounds__(FUSED_TPB) k_prehash_fused(hlc_votes v, uint64_t n, const uint32_t* vote_prop,
+                                                             const hlc_proposal* props, uint32_t* kec_dig,
+                                                             uint8_t* pre, uint8_t* pre_reason, uint32_t* general) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[FUSED_TPB * FBUF];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t* lb = lds + threadIdx.x * FBUF;
+  const uint32_t p = vote_prop[i];
+  uint8_t st = PRE_PENDING, rs = 0;
+  const uint32_t lo = flen(v, i, HLC_F_OWNER), lp = flen(v, i, HLC_F_PARENT), lr = flen(v, i, HLC_F_RECEIVED);
+  const uint32_t lh = flen(v, i, HLC_F_VOTE_HASH), ls = flen(v, i, HLC_F_SIGNATURE);
+  if (p == NO_PROP) {
+    st = PRE_SKIP;
+  } else if (v.proposal_id[i] != props[p].proposal_id) {
+    st = HLC_VOTE_PROPOSAL_ID_MISMATCH;
+  } else if (lo == 0) {
+    st = HLC_EMPTY_VOTE_OWNER;
+  } else if (lh == 0) {
+    st = HLC_EMPTY_VOTE_HASH;
+  } else if (ls == 0) {
+    st = HLC_EMPTY_SIGNATURE;
+  } else {
+    const uint64_t sha_len = 17ull + lo + lp + lr;
+    const uint64_t sha_sz = ((sha_len + 8) / 64 + 1) * 64;
+    const uint64_t el = vote_enc_len(v, i);
+    const uint64_t kec_len = 26 + dec_digits(el) + el;
+    const uint64_t kec_sz = (kec_len / 136 + 1) * 136;
+    if (sha_sz > FBUF || kec_sz > FBUF) {
+      pre[i] = PRE_GENERAL;
+      pre_reason[i] = 0;
+      atomicOr(general, 1u);
+      return;
+    }
+    // SHA-256 input (utils.rs:39-45) + padding, then compress from LDS
+    LdsCursor c{lb, 0};
+    c.put_le(v.vote_id[i], 4);
+    c.put_bytes(fptr(v, i, HLC_F_OWNER), lo);
+    c.put_le(v.proposal_id[i], 4);
+    c.put_le(v.timestamp[i], 8);
+    c.put(v.vote[i] ? 1 : 0);
+    c.put_bytes(fptr(v, i, HLC_F_PARENT), lp);
+    c.put_bytes(fptr(v, i, HLC_F_RECEIVED), lr);
+    c.put(0x80);
+    while (c.pos < sha_sz - 8) c.put(0);
+    {
+      const uint64_t bits = sha_len * 8;
+      for (int k = 7; k >= 0; --k) c.put((uint8_t)(bits >> (8 * k)));
+    }
+    uint32_t h[8];
+    sha256_init(h);
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lb);
+    for (uint32_t b = 0; b < (uint32_t)(sha_sz / 64); ++b) {
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = bswap32(lw[b * 16 + k]);
+      sha256_compress(h, w);
+    }
+    bool eq = lh == 32;
+    if (eq) {
+      const uint8_t* hb = fptr(v, i, HLC_F_VOTE_HASH);
+      uint32_t diff = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t want = (uint32_t)hb[4 * k] << 24 | (uint32_t)hb[4 * k + 1] << 16 |
+                              (uint32_t)hb[4 * k + 2] << 8 | (uint32_t)hb[4 * k + 3];
+        diff |= want ^ h[k];
+      }
+      eq = diff == 0;
+    }
+    if (!eq) {
+      st = HLC_INVALID_VOTE_HASH;
+    } else if (ls != 65) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = HLC_SCHEME_SIG_LEN;
+    } else if (lo != 20) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = HLC_SCHEME_ID_LEN;
+    } else {
+      // EIP-191 message of the prost encoding with the signature cleared (utils.rs:150-152)
+      LdsCursor k{lb, 0};
+      const char prefix[] = "\x19" "Ethereum Signed Message:\n";
+      for (int q = 0; q < 26; ++q) k.put((uint8_t)prefix[q]);
+      {
+        uint8_t d[20];
+        int nd = 0;
+        uint64_t x = el;
+        do {
+          d[nd++] = (uint8_t)('0' + x % 10);
+          x /= 10;
+        } while (x);
+        while (nd) k.put(d[--nd]);
+      }
+      const uint32_t id = v.vote_id[i], pid = v.proposal_id[i];
+      const uint64_t ts = v.timestamp[i];
+      if (id) { k.put(0xA0); k.put(0x01); k.put_varint(id); }
+      k.put(0xAA); k.put(0x01); k.put_varint(lo); k.put_bytes(fptr(v, i, HLC_F_OWNER), lo);
+      if (pid) { k.put(0xB0); k.put(0x01); k.put_varint(pid); }
+      if (ts) { k.put(0xB8); k.put(0x01); k.put_varint(ts); }
+      if (v.vote[i]) { k.put(0xC0); k.put(0x01); k.put(0x01); }
+      if (lp) { k.put(0xCA); k.put(0x01); k.put_varint(lp); k.put_bytes(fptr(v, i, HLC_F_PARENT), lp); }
+      if (lr) { k.put(0xD2); k.put(0x01); k.put_varint(lr); k.put_bytes(fptr(v, i, HLC_F_RECEIVED), lr); }
+      k.put(0xDA); k.put(0x01); k.put_varint(lh); k.put_bytes(fptr(v, i, HLC_F_VOTE_HASH), lh);
+      k.put(0x01);
+      while (k.pos < kec_sz) k.put(0);
+      lb[kec_sz - 1] |= 0x80;
+      uint64_t sk[25];
+#pragma unroll
+      for (int q = 0; q < 25; ++q) sk[q] = 0;
+      const uint64_t* l8 = reinterpret_cast<const uint64_t*>(lb);
+      for (uint32_t b = 0; b < (uint32_t)(kec_sz / 136); ++b) {
+#pragma unroll
+        for (int q = 0; q < 17; ++q) sk[q] ^= l8[b * 17 + q];
+        keccak_f1600(sk);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        kec_dig[i * 8 + 2 * q] = (uint32_t)sk[q];
+        kec_dig[i * 8 + 2 * q + 1] = (uint32_t)(sk[q] >> 32);
+      }
+    }
+  }
+  pre[i] = st;
+  pre_reason[i] = rs;
+}
+
 __global__ void k_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
                              uint8_t* verify_out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -486,6 +640,13 @@ inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB);
 void launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
                            hipStream_t s) {
   hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
+}
+
+void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                          uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason, uint32_t* general, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_prehash_fused, dim3((unsigned)((n + FUSED_TPB - 1) / FUSED_TPB)), dim3(FUSED_TPB), 0, s, *v,
+                       n, vote_prop, props, kec_dig, pre, pre_reason, general);
 }
 
 void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,

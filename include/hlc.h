@@ -160,7 +160,9 @@ int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_
  * (session.rs:253-298), as called by process_incoming_proposal (service.rs:273-274).
  * out_results[p]: per-proposal outcome.  out_vote_status[v] (optional): the per-vote
  * status of validate_proposal's loop body for that vote alone (proposal_id match, then
- * validate_vote, utils.rs:112-117, 127-171), with no short-circuit across votes.
+ * validate_vote, utils.rs:112-117, 127-171), with no short-circuit across votes; votes that no
+ * proposal's [vote_begin, vote_begin + vote_count) range covers are not evaluated (status 0xFF).
+ * Proposal ranges must not overlap.
  * out_vote_reason (optional): HLC_SCHEME_* per vote.  out_recovered (optional, n*20):
  * recovered signer address per vote (zeros when none). */
 int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,

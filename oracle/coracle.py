@@ -130,7 +130,7 @@ def validate_proposals(batch, desc: np.ndarray, now: int, threads: int = 8, reve
     from hashgraph_like_consensus import _ffi  # struct layout only
     n = batch.n
     res = np.zeros(desc.shape[0], dtype=_ffi.RESULT_DTYPE)
-    vst = np.zeros(max(n, 1), np.uint8)
+    vst = np.full(max(n, 1), 0xFF, np.uint8)  # votes outside every proposal: 0xFF (not evaluated)
     vrs = np.zeros(max(n, 1), np.uint8)
     rec = np.zeros((max(n, 1), 20), np.uint8)
     view = batch.view()

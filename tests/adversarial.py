@@ -69,9 +69,17 @@ def no_point_r() -> int:
     return _NO_POINT_R
 
 
+def relink_after(votes: List[po.Vote], privs: List[int], i: int, end: int) -> None:
+    """Re-chain votes i+1 .. end-1 after vote i's hash changed: received_hash -> previous vote,
+    then re-hash and re-sign, so the chain stays valid (the mutation's own class surfaces)."""
+    for k in range(i + 1, end):
+        votes[k].received_hash = votes[k - 1].vote_hash
+        resign(votes[k], privs[k])
+
+
 def mutate(votes: List[po.Vote], privs: List[int], i: int, j: int, kind: str, rnd: random.Random,
-           begin: int) -> None:
-    """Mutate votes[i] (index j within its proposal starting at `begin`)."""
+           begin: int, end: int = 0) -> None:
+    """Mutate votes[i] (index j within its proposal [begin, end))."""
     v = votes[i]
     priv = privs[i]
     if kind == "wrong_key":
@@ -129,6 +137,7 @@ def mutate(votes: List[po.Vote], privs: List[int], i: int, j: int, kind: str, rn
             v.vote_owner = votes[src].vote_owner
             privs[i] = privs[src]
             resign(v, privs[i])
+            relink_after(votes, privs, i, end)
     elif kind == "wrong_pid":
         v.proposal_id = (v.proposal_id + 1) & 0xFFFFFFFF
         resign(v, priv)
@@ -146,8 +155,9 @@ def mutate(votes: List[po.Vote], privs: List[int], i: int, j: int, kind: str, rn
         raise ValueError(kind)
 
 
-def byzantine(workload, fraction: float = 1 / 3, seed: int = 5) -> Tuple[object, np.ndarray, List[str]]:
-    """-> (VoteBatch with mutations, desc, per-vote kind or '')."""
+def byzantine(workload, fraction: float = 1 / 3, seed: int = 5, kinds_pool=None) -> Tuple[object, np.ndarray, List[str]]:
+    """-> (VoteBatch with mutations, desc, per-vote kind or '').  kinds_pool restricts the kinds."""
+    pool = list(kinds_pool) if kinds_pool else KINDS
     rnd = random.Random(seed)
     votes = batch_to_votes(workload.batch)
     privs = [int.from_bytes(bytes(k), "big") for k in workload.priv]
@@ -158,9 +168,9 @@ def byzantine(workload, fraction: float = 1 / 3, seed: int = 5) -> Tuple[object,
         b, c = int(desc[p]["vote_begin"]), int(desc[p]["vote_count"])
         for j in range(c):
             if rnd.random() < fraction:
-                kind = KINDS[k % len(KINDS)]
+                kind = pool[k % len(pool)]
                 k += 1
-                mutate(votes, privs, b + j, j, kind, rnd, b)
+                mutate(votes, privs, b + j, j, kind, rnd, b, b + c)
                 kinds[b + j] = kind
     return pack_votes(votes), desc, kinds
 

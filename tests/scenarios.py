@@ -148,7 +148,7 @@ def scenarios() -> List[Tuple[str, po.Proposal, po.ConsensusConfig, int, int]]:
     s[64] = s[64] - 27
     p.votes[0].signature = bytes(s)
     s = bytearray(p.votes[1].signature)
-    s[64] = 35 + (s[64] - 27) * 1 + 2 * 7  # odd/even preserved: 27->49? (v-35)%2 = parity
+    s[64] = 49 + (s[64] - 27)  # EIP-155 style v: (v - 35) % 2 is the parity
     p.votes[1].signature = bytes(s)
     out.append(("v_raw_and_eip155", p, G, now, po.OK))
     # non-canonical lengths: 19-byte owner -> scheme id-length error after hash check
@@ -162,6 +162,17 @@ def scenarios() -> List[Tuple[str, po.Proposal, po.ConsensusConfig, int, int]]:
     p = chain(new_proposal(125, 3), [(1, True)])
     p.votes[0].vote_hash = p.votes[0].vote_hash + b"\x00"
     out.append(("vote_hash_33_bytes", p, G, now, po.INVALID_VOTE_HASH))
+    # oversize fields (beyond the fused kernel's LDS window: exercised on the general GPU path)
+    p = chain(new_proposal(126, 3), [(1, True), (2, True)])
+    p.votes[1].parent_hash = bytes(range(256)) + bytes(44)
+    resign(p.votes[1], key(2))
+    out.append(("long_parent_hash", p, G, now, po.PARENT_HASH_MISMATCH))
+    p = new_proposal(127, 3)
+    v = po.Vote(vote_id=9, vote_owner=bytes(200), proposal_id=127, timestamp=T0 + 1, vote=True)
+    v.vote_hash = po.compute_vote_hash(v)
+    v.signature = c_sign(key(4), v)
+    p.votes.append(v)
+    out.append(("owner_200_bytes", p, G, now, po.SIGNATURE_SCHEME))
     # zero ids / zero timestamp encode as omitted proto3 defaults (pid 0, vote_id 0)
     p = new_proposal(0, 2, now=0)
     p.votes.append(mk_vote(p, True, 1, 0, 0))
