@@ -1,0 +1,260 @@
+"""Host-side mirror of the reference's entry points onto the hot path.
+
+* `ConsensusConfig`         session.rs:25-160 (gossipsub()/p2p() presets, validated builders)
+* `validate_proposal(s)`    utils.rs:106-225 (`validate_proposal`, `validate_vote_chain`, `validate_vote`)
+* `compute_vote_hash(es)`   utils.rs:37-52
+* `build_vote`              utils.rs:55-104
+* `ConsensusService.process_incoming_proposal(s)`  service.rs:263-279 -> session.rs:198-300
+
+Only the slice of `ConsensusService` that sits on the validation path is mirrored: the
+duplicate-session check (`ProposalAlreadyExist`), config resolution (service.rs:444-484) and
+`ConsensusSession::from_proposal`.  The event bus, storage trait, scope management and timeout
+handling are the reference's control plane and are out of scope (DESIGN.md §Out of scope); the
+accepted sessions are kept in a plain dict so a second delivery of the same proposal id is
+rejected exactly as the reference's storage lookup does.
+
+Every hash, signature and tally is computed on the GPU through libhlc.so (engine.py); this module
+only marshals and maps status codes to exceptions.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import errors
+from .batch import ProposalConfig, pack_proposals, pack_votes
+from .engine import Engine
+from .protos import Proposal, Vote
+
+GOSSIPSUB, P2P = "gossipsub", "p2p"
+DEFAULT_THRESHOLD = 2.0 / 3.0
+DEFAULT_TIMEOUT_S = 60
+
+TRANSITION_STILL_ACTIVE, TRANSITION_CONSENSUS_REACHED = 0, 1
+
+
+@dataclass(frozen=True)
+class ConsensusConfig:
+    """session.rs:25-44.  Defaults are `ConsensusConfig::gossipsub()` (scope_config.rs defaults:
+    threshold 2/3, timeout 60 s, max_rounds 2, liveness_criteria_yes true)."""
+    consensus_threshold: float = DEFAULT_THRESHOLD
+    consensus_timeout: int = DEFAULT_TIMEOUT_S
+    max_rounds: int = 2
+    use_gossipsub_rounds: bool = True
+    liveness_criteria: bool = True
+
+    @staticmethod
+    def gossipsub() -> "ConsensusConfig":
+        return ConsensusConfig()
+
+    @staticmethod
+    def p2p() -> "ConsensusConfig":
+        """max_rounds 0 = derive ceil(2n/3)-style cap from expected_voters_count (session.rs:120-128)."""
+        return ConsensusConfig(max_rounds=0, use_gossipsub_rounds=False)
+
+    def with_threshold(self, t: float) -> "ConsensusConfig":
+        if not (0.0 <= t <= 1.0):          # utils.rs:331-336
+            raise errors.InvalidConsensusThreshold()
+        return dataclasses.replace(self, consensus_threshold=float(t))
+
+    def with_timeout(self, seconds: int) -> "ConsensusConfig":
+        if seconds <= 0:                    # utils.rs:339-344
+            raise errors.InvalidTimeout()
+        return dataclasses.replace(self, consensus_timeout=int(seconds))
+
+    def with_liveness_criteria(self, yes: bool) -> "ConsensusConfig":
+        return dataclasses.replace(self, liveness_criteria=bool(yes))
+
+    def with_max_rounds(self, max_rounds: int) -> "ConsensusConfig":
+        return dataclasses.replace(self, max_rounds=int(max_rounds))
+
+    def to_proposal_config(self) -> ProposalConfig:
+        return ProposalConfig(self.consensus_threshold, self.max_rounds, self.use_gossipsub_rounds)
+
+
+def resolve_config(base: ConsensusConfig, proposal: Proposal, explicit: bool = False) -> ConsensusConfig:
+    """service.rs:444-484: timeout from the proposal's expiration unless explicitly overridden;
+    liveness from the proposal."""
+    timeout = base.consensus_timeout
+    if not explicit and proposal.expiration_timestamp > proposal.timestamp:
+        timeout = proposal.expiration_timestamp - proposal.timestamp
+    return dataclasses.replace(base, consensus_timeout=timeout, liveness_criteria=proposal.liveness_criteria_yes)
+
+
+@dataclass
+class ProposalOutcome:
+    """One proposal's result from the batch path: `error` is None on `Ok`, else the
+    ConsensusError the reference returns; `transition` / `yes` / `total` are meaningful on Ok."""
+    proposal_id: int
+    error: Optional[errors.ConsensusError]
+    transition: int = TRANSITION_STILL_ACTIVE
+    consensus: Optional[bool] = None
+    yes: int = 0
+    total: int = 0
+    bad_index: int = -1
+
+    @property
+    def ok(self) -> bool:
+        return self.error is None
+
+
+def _outcomes(proposals: Sequence[Proposal], res: np.ndarray) -> List[ProposalOutcome]:
+    out = []
+    for p, r in zip(proposals, res):
+        st = int(r["status"])
+        err = None if st == 0 else errors.from_status(st, int(r["scheme_reason"]))
+        tr = int(r["transition"])
+        cons = None
+        if st == 0 and tr == 2:      # HLC_REACHED_YES
+            cons = True
+        elif st == 0 and tr == 1:    # HLC_REACHED_NO
+            cons = False
+        bad = int(r["bad_index"])
+        out.append(ProposalOutcome(p.proposal_id, err, TRANSITION_CONSENSUS_REACHED if tr else TRANSITION_STILL_ACTIVE,
+                                   cons, int(r["yes"]), int(r["total"]), bad if bad != 0xFFFFFFFF else -1))
+    return out
+
+
+def validate_proposals(proposals: Sequence[Proposal], now: int, configs: Optional[Sequence[ConsensusConfig]] = None,
+                       engine: Optional[Engine] = None) -> List[ProposalOutcome]:
+    """Batched `ConsensusSession::from_proposal` validation (session.rs:198-300 incl. utils.rs:106-225):
+    one GPU call for every proposal."""
+    eng = engine or Engine.default()
+    cfgs = [(configs[i] if configs is not None else ConsensusConfig()).to_proposal_config() for i in range(len(proposals))]
+    batch, desc = pack_proposals(proposals, cfgs)
+    res, _, _, _ = eng.validate_proposals(batch, desc, now, want_votes=False)
+    return _outcomes(proposals, res)
+
+
+def validate_proposal(proposal: Proposal, now: int, config: Optional[ConsensusConfig] = None,
+                      engine: Optional[Engine] = None) -> ProposalOutcome:
+    """utils.rs:106 + session.rs:198: raises the reference's ConsensusError on rejection."""
+    o = validate_proposals([proposal], now, [config] if config else None, engine)[0]
+    if o.error is not None:
+        raise o.error
+    return o
+
+
+def compute_vote_hashes(votes: Sequence[Vote], engine: Optional[Engine] = None) -> List[bytes]:
+    """utils.rs:37-52 over a batch (GPU SHA-256)."""
+    eng = engine or Engine.default()
+    if not votes:
+        return []
+    h = eng.compute_vote_hashes(pack_votes(votes))
+    return [bytes(x) for x in h]
+
+
+def compute_vote_hash(vote: Vote, engine: Optional[Engine] = None) -> bytes:
+    return compute_vote_hashes([vote], engine)[0]
+
+
+def build_vote(proposal: Proposal, vote: bool, signer, now: int, engine: Optional[Engine] = None) -> Vote:
+    """utils.rs:55-104: chain onto the proposal's last vote, hash, sign (EIP-191) with `signer`."""
+    from .protos import encode_vote
+    owner = signer.identity()
+    parent_hash = b""
+    received_hash = b""
+    if proposal.votes:
+        received_hash = proposal.votes[-1].vote_hash
+        for v in proposal.votes:
+            if v.vote_owner == owner:
+                parent_hash = v.vote_hash
+    v = Vote(vote_id=_vote_id(owner, proposal.proposal_id, now), vote_owner=owner, proposal_id=proposal.proposal_id,
+             timestamp=now, vote=vote, parent_hash=parent_hash, received_hash=received_hash)
+    v.vote_hash = compute_vote_hash(v, engine)
+    v.signature = signer.sign(encode_vote(v))
+    return v
+
+
+def _vote_id(owner: bytes, proposal_id: int, now: int) -> int:
+    """The reference draws vote_id from `generate_id()` (utils.rs:79); any u32 is valid on the path."""
+    import uuid
+    return uuid.uuid4().int & 0xFFFFFFFF
+
+
+@dataclass
+class SessionRecord:
+    """What the service keeps per accepted proposal (the subset of session.rs:160-190 the path
+    produces): the proposal, the resolved config and the tally after initial validation."""
+    proposal: Proposal
+    config: ConsensusConfig
+    transition: int
+    consensus: Optional[bool]
+    yes: int
+    total: int
+    created_at: int
+
+
+class ConsensusService:
+    """service.rs:63-280 restricted to the incoming-proposal path (see module docstring)."""
+
+    def __init__(self, engine: Optional[Engine] = None, default_config: Optional[ConsensusConfig] = None):
+        self.engine = engine or Engine.default()
+        self.default_config = default_config or ConsensusConfig.gossipsub()
+        self.scope_configs: Dict[bytes, ConsensusConfig] = {}
+        self.sessions: Dict[Tuple[bytes, int], SessionRecord] = {}
+
+    def set_scope_config(self, scope: Union[str, bytes], config: ConsensusConfig) -> None:
+        self.scope_configs[_scope_key(scope)] = config
+
+    def get_session(self, scope: Union[str, bytes], proposal_id: int) -> SessionRecord:
+        try:
+            return self.sessions[(_scope_key(scope), proposal_id)]
+        except KeyError:
+            raise errors.SessionNotFound() from None
+
+    def process_incoming_proposal(self, scope: Union[str, bytes], proposal: Proposal, now: int) -> None:
+        """service.rs:263-279: raises the reference's error or stores the session."""
+        o = self.process_incoming_proposals(scope, [proposal], now)[0]
+        if o.error is not None:
+            raise o.error
+
+    def process_incoming_proposals(self, scope: Union[str, bytes], proposals: Sequence[Proposal],
+                                   now: int) -> List[ProposalOutcome]:
+        """The batched form the GPU path exists for: each proposal gets exactly the outcome the
+        reference's per-proposal `process_incoming_proposal` returns when they are delivered in
+        order.  A proposal id that is already stored (or repeats earlier in this batch) is
+        rejected with ProposalAlreadyExist before validation, as service.rs:269-271 does."""
+        key = _scope_key(scope)
+        base = self.scope_configs.get(key, self.default_config)
+        outcomes: List[Optional[ProposalOutcome]] = [None] * len(proposals)
+        todo: List[int] = []
+        seen = set()
+        for i, p in enumerate(proposals):
+            if (key, p.proposal_id) in self.sessions or p.proposal_id in seen:
+                outcomes[i] = ProposalOutcome(p.proposal_id, errors.ProposalAlreadyExist())
+            else:
+                todo.append(i)
+                seen.add(p.proposal_id)
+        cfgs = [resolve_config(base, proposals[i]) for i in todo]
+        sub = [proposals[i] for i in todo]
+        if sub:
+            res = validate_proposals(sub, now, cfgs, self.engine)
+            # an id that fails validation is not stored, so a later copy in the batch would be
+            # validated in the reference; re-run those (rare) in a second pass.
+            retry: List[int] = []
+            for i, cfg, o in zip(todo, cfgs, res):
+                outcomes[i] = o
+                if o.ok:
+                    self._store(key, proposals[i], cfg, o, now)
+            for i, p in enumerate(proposals):
+                if outcomes[i] is not None and isinstance(outcomes[i].error, errors.ProposalAlreadyExist) \
+                        and (key, p.proposal_id) not in self.sessions:
+                    retry.append(i)
+            if retry:
+                for i in retry:
+                    outcomes[i] = None
+                rest = self.process_incoming_proposals(scope, [proposals[i] for i in retry], now)
+                for i, o in zip(retry, rest):
+                    outcomes[i] = o
+        return outcomes  # type: ignore[return-value]
+
+    def _store(self, key: bytes, p: Proposal, cfg: ConsensusConfig, o: ProposalOutcome, now: int) -> None:
+        self.sessions[(key, p.proposal_id)] = SessionRecord(p, cfg, o.transition, o.consensus, o.yes, o.total, now)
+
+
+def _scope_key(scope: Union[str, bytes]) -> bytes:
+    return scope.encode() if isinstance(scope, str) else bytes(scope)

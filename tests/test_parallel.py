@@ -1,0 +1,99 @@
+"""Proposal-sharded multi-process path (parallel.py) on CPU: gloo, world size 2.
+
+Each rank validates its shard with an oracle-backed engine double (test infrastructure) and the
+gathered results must equal one whole-batch validation.  The same code runs over RCCL on GPUs
+(bench.py's N > 1 path shards the same way).
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import coracle
+from adversarial import byzantine
+from helpers import oracle_workload
+from hashgraph_like_consensus.parallel import shard_bounds, slice_shard
+
+
+class OracleEngine:
+    def validate_proposals(self, batch, desc, now, want_votes=True, want_recovered=False):
+        return coracle.validate_proposals(batch, desc, now, threads=2)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_bounds_balanced_and_total():
+    desc = np.zeros(10, dtype=__import__("hashgraph_like_consensus._ffi", fromlist=["x"]).PROPOSAL_DTYPE)
+    desc["vote_count"] = [100, 1, 1, 1, 1, 1, 1, 1, 1, 100]
+    b = shard_bounds(desc, 2)
+    assert b[0] == 0 and b[-1] == 10 and np.all(np.diff(b) >= 0)
+    w = [int(desc["vote_count"][b[r]:b[r + 1]].sum()) for r in range(2)]
+    assert abs(w[0] - w[1]) <= 100
+    assert list(shard_bounds(desc, 1)) == [0, 10]
+    b16 = shard_bounds(desc, 16)
+    assert len(b16) == 17 and b16[-1] == 10 and np.all(np.diff(b16) >= 0)
+    empty = desc[:0]
+    assert list(shard_bounds(empty, 4)) == [0, 0, 0, 0, 0]
+
+
+def test_slice_shard_equals_whole_batch():
+    w = oracle_workload(6, 5, 8, True, seed=41)
+    batch, desc, _ = byzantine(w, fraction=0.3, seed=3)
+    ref, vst_ref, _, _ = coracle.validate_proposals(batch, desc, w.now, threads=4)
+    b = shard_bounds(desc, 3)
+    parts = []
+    for r in range(3):
+        local, sub, idx = slice_shard(batch, desc, int(b[r]), int(b[r + 1]))
+        res, vst, _, _ = coracle.validate_proposals(local, sub, w.now, threads=2)
+        parts.append(res)
+        assert np.array_equal(vst, vst_ref[idx])
+    assert np.concatenate(parts).tobytes() == ref.tobytes()
+
+
+def _worker(rank, world, port, payload, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "hashgraph-like-consensus_amd", "python"),
+              os.path.join(os.path.dirname(here), "oracle"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from hashgraph_like_consensus.batch import VoteBatch
+    from hashgraph_like_consensus.parallel import validate_sharded
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        batch = VoteBatch(*payload["batch"])
+        res, st = validate_sharded(OracleEngine(), batch, payload["desc"], payload["now"], want_votes=True)
+        q.put((rank, res.tobytes(), st.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_equals_single():
+    w = oracle_workload(5, 7, 9, False, seed=42)
+    batch, desc, _ = byzantine(w, fraction=0.25, seed=9)
+    ref, vst_ref, _, _ = coracle.validate_proposals(batch, desc, w.now, threads=4)
+    payload = {"batch": (batch.vote_id, batch.proposal_id, batch.timestamp, batch.vote, batch.arena,
+                         batch.field_off, batch.field_len), "desc": desc, "now": w.now}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, payload, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res, st in got:
+        assert res == ref.tobytes(), f"rank {rank} results differ"
+        assert st == vst_ref.tobytes(), f"rank {rank} vote statuses differ"
