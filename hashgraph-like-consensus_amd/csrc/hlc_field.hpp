@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "hlc_field_asm.hpp"
 #include "hlc_modinv.hpp"
 
 #define HLC_DEV __device__ __forceinline__
@@ -106,39 +107,82 @@ HLC_DEV bool u256_lt(const fe& a, const fe& b) {
 }
 
 // ------------------------------------------------------------------------------------
-// mod p
+// mod p -- LAZY representation: a field value is any 256-bit integer congruent to it mod p
+// (i.e. in [0, 2^256), so possibly in [p, 2^256)).  Products, sums and differences are
+// reduced only back into [0, 2^256) with the fold 2^256 == K = 2^32 + 977; values are made
+// canonical (< p) only where a comparison, a parity or an output needs it (fe_normalize,
+// fe_is_zero_modp, fe_eq_modp).  Carry chains use __builtin_addc/subc (v_add_co/v_addc with
+// SGPR carries); the rare carry propagations past limb 1-2 sit behind a divergent branch that
+// the whole wave skips when no lane needs it.
 // ------------------------------------------------------------------------------------
-// r = x - p if x >= p (x < 2^256): x >= p  <=>  x + (2^32+977) overflows 2^256
-HLC_DEV void fe_final_sub(fe& r, const uint32_t x[8], uint32_t extra_carry) {
-  uint32_t c = 0, t[8];
-  t[0] = add_cc(x[0], 0x3D1u, c);
-  t[1] = add_cc(x[1], 0x1u, c);
+HLC_DEV uint32_t adc(uint32_t a, uint32_t b, uint32_t& c) {
+  uint32_t co;
+  uint32_t r = __builtin_addc(a, b, c, &co);
+  c = co;
+  return r;
+}
+HLC_DEV uint32_t sbb(uint32_t a, uint32_t b, uint32_t& c) {
+  uint32_t co;
+  uint32_t r = __builtin_subc(a, b, c, &co);
+  c = co;
+  return r;
+}
+
+// s += K (s < K on entry: cannot overflow)
+HLC_DEV void fe_add_k(uint32_t s[8]) {
+  uint32_t c = 0;
+  s[0] = adc(s[0], 0x3D1u, c);
+  s[1] = adc(s[1], 1u, c);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) t[i] = add_cc(x[i], 0u, c);
-  bool ge = (c | extra_carry) != 0;
+  for (int i = 2; i < 8; ++i) s[i] = adc(s[i], 0u, c);
+}
+
+// s (256 bits) + c*2^256 with c in {0, 1} -> [0, 2^256)
+HLC_DEV void fe_fold_carry(uint32_t s[8], uint32_t c) {
+  uint32_t c2 = 0;
+  s[0] = adc(s[0], c * 0x3D1u, c2);
+  s[1] = adc(s[1], c, c2);
+  if (c2) {  // rare: the fold carries past limb 1
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = ge ? t[i] : x[i];
+    for (int i = 2; i < 8; ++i) s[i] = adc(s[i], 0u, c2);
+    if (c2) fe_add_k(s);  // both operands were >= p: one more fold
+  }
+}
+
+// s (256 bits) - b*2^256 with b in {0, 1} -> [0, 2^256)
+HLC_DEV void fe_fold_borrow(uint32_t d[8], uint32_t b) {
+  uint32_t b2 = 0;
+  d[0] = sbb(d[0], b * 0x3D1u, b2);
+  d[1] = sbb(d[1], b, b2);
+  if (b2) {  // rare
+#pragma unroll
+    for (int i = 2; i < 8; ++i) d[i] = sbb(d[i], 0u, b2);
+    if (b2) {  // d was < K: subtract K once more (no further borrow)
+      uint32_t b3 = 0;
+      d[0] = sbb(d[0], 0x3D1u, b3);
+      d[1] = sbb(d[1], 1u, b3);
+#pragma unroll
+      for (int i = 2; i < 8; ++i) d[i] = sbb(d[i], 0u, b3);
+    }
+  }
 }
 
 HLC_DEV void fe_add(fe& r, const fe& a, const fe& b) {
   uint32_t c = 0, s[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s[i] = add_cc(a.v[i], b.v[i], c);
-  fe_final_sub(r, s, c);
+  for (int i = 0; i < 8; ++i) s[i] = adc(a.v[i], b.v[i], c);
+  fe_fold_carry(s, c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = s[i];
 }
 
 HLC_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
   uint32_t bw = 0, d[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) d[i] = sub_cc(a.v[i], b.v[i], bw);
-  // if borrow: d += p  (== d - (2^32+977) mod 2^256)
-  uint32_t bw2 = 0, t[8];
-  t[0] = sub_cc(d[0], 0x3D1u, bw2);
-  t[1] = sub_cc(d[1], 0x1u, bw2);
+  for (int i = 0; i < 8; ++i) d[i] = sbb(a.v[i], b.v[i], bw);
+  fe_fold_borrow(d, bw);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) t[i] = sub_cc(d[i], 0u, bw2);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = bw ? t[i] : d[i];
+  for (int i = 0; i < 8; ++i) r.v[i] = d[i];
 }
 
 HLC_DEV void fe_neg(fe& r, const fe& a) {
@@ -147,91 +191,123 @@ HLC_DEV void fe_neg(fe& r, const fe& a) {
   fe_sub(r, z, a);
 }
 
-HLC_DEV void fe_dbl(fe& r, const fe& a) { fe_add(r, a, a); }
+// r = 2^sh * a, 1 <= sh <= 3 (shift + fold of the sh top bits: e*2^256 == e*K, e < 8)
+template <int SH>
+HLC_DEV void fe_shl(fe& r, const fe& a) {
+  uint32_t s[8];
+  const uint32_t e = a.v[7] >> (32 - SH);
+#pragma unroll
+  for (int i = 7; i > 0; --i) s[i] = __builtin_amdgcn_alignbit(a.v[i], a.v[i - 1], 32 - SH);
+  s[0] = a.v[0] << SH;
+  uint32_t c2 = 0;
+  s[0] = adc(s[0], e * 0x3D1u, c2);
+  s[1] = adc(s[1], e, c2);
+  if (c2) {
+#pragma unroll
+    for (int i = 2; i < 8; ++i) s[i] = adc(s[i], 0u, c2);
+    if (c2) fe_add_k(s);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = s[i];
+}
 
-// reduce a 512-bit product t[16] mod p
+HLC_DEV void fe_dbl(fe& r, const fe& a) { fe_shl<1>(r, a); }
+
+// canonical representative (< p): a >= p  <=>  a + K overflows 2^256
+HLC_DEV void fe_normalize(fe& r, const fe& a) {
+  uint32_t c = 0, t[8];
+  t[0] = adc(a.v[0], 0x3D1u, c);
+  t[1] = adc(a.v[1], 1u, c);
+#pragma unroll
+  for (int i = 2; i < 8; ++i) t[i] = adc(a.v[i], 0u, c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = c ? t[i] : a.v[i];
+}
+
+// a == 0 (mod p), i.e. a in {0, p}
+HLC_DEV bool fe_is_zero_modp(const fe& a) {
+  uint32_t z = a.v[0], hi = a.v[2];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) z |= a.v[i];
+#pragma unroll
+  for (int i = 3; i < 8; ++i) hi &= a.v[i];
+  const bool is_p = (a.v[0] == 0xFFFFFC2Fu) & (a.v[1] == 0xFFFFFFFEu) & (hi == 0xFFFFFFFFu);
+  return (z == 0) | is_p;
+}
+
+HLC_DEV bool fe_eq_modp(const fe& a, const fe& b) {
+  fe d;
+  fe_sub(d, a, b);
+  return fe_is_zero_modp(d);
+}
+
+// Reduce a 512-bit integer T = L + H*2^256 (t[0..15]) into [0, 2^256):
+//   x = L + H*977 + H*2^32 (9 limbs, top e < 2^33), then y = x[0..7] + e*K.
 HLC_DEV void fe_reduce512(fe& r, const uint32_t t[16]) {
-  // x = lo + hi*977 + hi*2^32
-  uint32_t x[8];
-  uint64_t c = 0;
+  uint32_t ml[8], mh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)t[8 + i] * 977u + t[i];
-    if (i > 0) c += t[7 + i];
-    x[i] = (uint32_t)c;
-    c >>= 32;
+    const uint64_t m = (uint64_t)t[8 + i] * 977u;
+    ml[i] = (uint32_t)m;
+    mh[i] = (uint32_t)(m >> 32);
   }
-  c += t[15];  // T < 2^33: the part at 2^256
-  // fold T*(2^32 + 977) into x
-  uint64_t e = (c & 0xFFFFFFFFull) * 977u + x[0];
-  x[0] = (uint32_t)e;
-  e >>= 32;
-  e += (uint64_t)(uint32_t)(c >> 32) * 977u + (uint32_t)c + x[1];
-  x[1] = (uint32_t)e;
-  e >>= 32;
-  e += (uint32_t)(c >> 32) + (uint64_t)x[2];
-  x[2] = (uint32_t)e;
-  uint32_t cc = (uint32_t)(e >> 32);
+  uint32_t cA = 0, cB = 0, cC = 0, x[8];
+  x[0] = adc(t[0], ml[0], cA);
 #pragma unroll
-  for (int i = 3; i < 8; ++i) x[i] = add_cc(x[i], 0u, cc);
-  // overflow out of 2^256 (only possible when x was near 2^256): add 2^32+977 once more;
-  // the result is then tiny and cannot overflow again.
-  uint32_t c2 = 0, y[8];
-  y[0] = add_cc(x[0], cc ? 0x3D1u : 0u, c2);
-  y[1] = add_cc(x[1], cc ? 0x1u : 0u, c2);
+  for (int i = 1; i < 8; ++i) {
+    x[i] = adc(t[i], ml[i], cA);
+    x[i] = adc(x[i], mh[i - 1], cB);
+    x[i] = adc(x[i], t[7 + i], cC);
+  }
+  uint32_t e_lo = adc(mh[7], 0u, cA);
+  e_lo = adc(e_lo, 0u, cB);
+  e_lo = adc(e_lo, t[15], cC);
+  const uint32_t e_hi = cC;  // e = e_lo + e_hi*2^32
+  // e*K = e_lo*977 + (e_hi*977 + e_lo)*2^32 + e_hi*2^64
+  const uint64_t f = (uint64_t)e_lo * 977u;
+  const uint32_t g = (uint32_t)(f >> 32) + e_hi * 977u;  // < 2^11
+  uint32_t c1 = 0, c2 = 0, y[8];
+  y[0] = adc(x[0], (uint32_t)f, c1);
+  y[1] = adc(x[1], g, c1);
+  y[1] = adc(y[1], e_lo, c2);
+  y[2] = adc(x[2], e_hi, c1);
+  y[2] = adc(y[2], 0u, c2);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) y[i] = add_cc(x[i], 0u, c2);
-  fe_final_sub(r, y, 0);
+  for (int i = 3; i < 8; ++i) y[i] = x[i];
+  uint32_t c3 = c1 + c2;
+  if (c3) {  // rare: carries past limb 2
+    uint32_t c = 0;
+    y[3] = adc(y[3], c3, c);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) y[i] = adc(y[i], 0u, c);
+    if (c) fe_add_k(y);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = y[i];
 }
 
-HLC_DEV void mul512(uint32_t t[16], const fe& a, const fe& b) {
-  uint64_t acc = 0;
-  uint32_t hi = 0;
-#pragma unroll
-  for (int k = 0; k < 15; ++k) {
-#pragma unroll
-    for (int i = (k < 8 ? 0 : k - 7); i <= (k < 8 ? k : 7); ++i) mac(acc, hi, a.v[i], b.v[k - i]);
-    t[k] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
-  }
-  t[15] = (uint32_t)acc;
-}
+HLC_DEV void mul512(uint32_t t[16], const fe& a, const fe& b) { mul512_asm(t, a.v, b.v); }
 
-// Squaring: 28 off-diagonal MACs (product scanning over the strict upper triangle),
-// one 512-bit doubling (v_alignbit), then the 8 diagonal squares: 36 MACs instead of 64.
+// a^2: off-diagonal scan (28 products, asm), doubling, then the 8 diagonal squares.
 HLC_DEV void sqr512(uint32_t t[16], const fe& a) {
   uint32_t x[16];
-  uint64_t acc = 0;
-  uint32_t hi = 0;
-  x[0] = 0;
+  sqr_offdiag_asm(x, a.v);
+  uint32_t y[16];
+  y[15] = x[14] >> 31;
 #pragma unroll
-  for (int k = 1; k < 14; ++k) {
-#pragma unroll
-    for (int i = (k < 8 ? 0 : k - 7); i < k - i; ++i) mac(acc, hi, a.v[i], a.v[k - i]);
-    x[k] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
-  }
-  x[14] = (uint32_t)acc;
-  x[15] = (uint32_t)(acc >> 32);
-  // double
-#pragma unroll
-  for (int k = 15; k > 0; --k) x[k] = __builtin_amdgcn_alignbit(x[k], x[k - 1], 31);
-  x[0] = 0;
-  // add the diagonal squares a_i^2 at limb 2i with a carry chain
+  for (int k = 14; k > 1; --k) y[k] = __builtin_amdgcn_alignbit(x[k], x[k - 1], 31);
+  y[1] = x[1] << 1;
   uint32_t c = 0;
+  {
+    const uint64_t d = (uint64_t)a.v[0] * a.v[0];
+    t[0] = (uint32_t)d;
+    t[1] = adc(y[1], (uint32_t)(d >> 32), c);
+  }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t d = (uint64_t)x[2 * i] | ((uint64_t)x[2 * i + 1] << 32);
-    uint64_t sq = (uint64_t)a.v[i] * a.v[i];
-    uint64_t s = d + sq;
-    uint32_t c1 = s < sq;
-    uint64_t s2 = s + c;
-    uint32_t c2 = s2 < s;
-    t[2 * i] = (uint32_t)s2;
-    t[2 * i + 1] = (uint32_t)(s2 >> 32);
-    c = c1 + c2;
+  for (int i = 1; i < 8; ++i) {
+    const uint64_t d = (uint64_t)a.v[i] * a.v[i];
+    t[2 * i] = adc(y[2 * i], (uint32_t)d, c);
+    t[2 * i + 1] = adc(y[2 * i + 1], (uint32_t)(d >> 32), c);
   }
 }
 
@@ -253,7 +329,7 @@ HLC_DEV void fe_sqr_n(fe& r, const fe& a, int n) {
   for (int i = 0; i < n; ++i) fe_sqr(r, r);
 }
 
-// Addition-chain prefix shared by inversion (p-2) and square root ((p+1)/4).
+// Addition-chain prefix of the square root exponent (p+1)/4.
 HLC_DEV void fe_chain223(const fe& a, fe& x2, fe& x3, fe& x22, fe& x223) {
   fe t, x6, x9, x11, x44, x88, x176, x220;
   fe_sqr(t, a);
@@ -280,10 +356,14 @@ HLC_DEV void fe_chain223(const fe& a, fe& x2, fe& x3, fe& x22, fe& x223) {
   fe_mul(x223, t, x3);
 }
 
-// r = a^-1 mod p (a != 0): safegcd divsteps (hlc_modinv.hpp), ~5x cheaper than a^(p-2)
-HLC_DEV void fe_inv(fe& r, const fe& a) { modinv_safegcd(r.v, a.v, modinfo_p()); }
+// r = a^-1 mod p (a != 0 mod p), canonical: safegcd divsteps (hlc_modinv.hpp)
+HLC_DEV void fe_inv(fe& r, const fe& a) {
+  fe n;
+  fe_normalize(n, a);
+  modinv_safegcd(r.v, n.v, modinfo_p());
+}
 
-// r = a^((p+1)/4); returns whether r^2 == a (a is a quadratic residue)
+// r = a^((p+1)/4), canonical; returns whether r^2 == a (a is a quadratic residue)
 HLC_DEV bool fe_sqrt(fe& r, const fe& a) {
   fe x2, x3, x22, x223, t;
   fe_chain223(a, x2, x3, x22, x223);
@@ -292,8 +372,9 @@ HLC_DEV bool fe_sqrt(fe& r, const fe& a) {
   fe_sqr_n(t, t, 6);
   fe_mul(t, t, x2);
   fe_sqr_n(r, t, 2);
+  fe_normalize(r, r);
   fe_sqr(t, r);
-  return fe_eq(t, a);
+  return fe_eq_modp(t, a);
 }
 
 // ------------------------------------------------------------------------------------

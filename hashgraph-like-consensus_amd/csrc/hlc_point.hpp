@@ -91,8 +91,8 @@ HLC_DEV void gej_add_ge(gej& r, const gej& a, const ge& b) {
   fe_mul(s2, s2, z1z1);
   fe_sub(h, u2, a.x);
   fe_sub(rr, s2, a.y);
-  if (fe_is_zero(h)) {
-    if (fe_is_zero(rr)) {
+  if (fe_is_zero_modp(h)) {
+    if (fe_is_zero_modp(rr)) {
       gej_double(r, a);
     } else {
       gej_set_inf(r);
@@ -151,8 +151,8 @@ HLC_DEV void gej_add(gej& r, const gej& a, const gej& b) {
   fe_mul(s2, s2, z1z1);
   fe_sub(h, u2, u1);
   fe_sub(rr, s2, s1);
-  if (fe_is_zero(h)) {
-    if (fe_is_zero(rr)) {
+  if (fe_is_zero_modp(h)) {
+    if (fe_is_zero_modp(rr)) {
       gej_double(r, a);
     } else {
       gej_set_inf(r);
@@ -187,7 +187,7 @@ HLC_DEV void gej_add(gej& r, const gej& a, const gej& b) {
   r.inf = 0;
 }
 
-// affine coordinates of a (finite) Jacobian point
+// affine coordinates (canonical, < p) of a (finite) Jacobian point
 HLC_DEV void gej_to_affine(fe& x, fe& y, const gej& a) {
   fe zi, zi2, zi3;
   fe_inv(zi, a.z);
@@ -195,6 +195,8 @@ HLC_DEV void gej_to_affine(fe& x, fe& y, const gej& a) {
   fe_mul(zi3, zi2, zi);
   fe_mul(x, a.x, zi2);
   fe_mul(y, a.y, zi3);
+  fe_normalize(x, x);
+  fe_normalize(y, y);
 }
 
 }  // namespace hlc

@@ -33,9 +33,9 @@ KINDS = ["wrong_key", "flip_rs", "bad_v", "high_s", "no_point", "infinity", "tam
          "parent_other", "ts_regress", "ts_old", "duplicate", "wrong_pid", "empty", "sig_len"]
 
 
-def batch_to_votes(batch) -> List[po.Vote]:
+def batch_to_votes(batch, lo: int = 0, hi: int = -1) -> List[po.Vote]:
     out = []
-    for i in range(batch.n):
+    for i in range(lo, batch.n if hi < 0 else hi):
         f = [batch.field(i, k) for k in range(5)]
         out.append(po.Vote(vote_id=int(batch.vote_id[i]), vote_owner=f[0], proposal_id=int(batch.proposal_id[i]),
                            timestamp=int(batch.timestamp[i]), vote=bool(batch.vote[i]), parent_hash=f[1],

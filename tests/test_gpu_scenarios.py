@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import coracle
-from adversarial import KINDS, byzantine
+from adversarial import KINDS, batch_to_votes, byzantine, resign
 from golden_io import fixtures, load
 from hashgraph_like_consensus import synth
 from hashgraph_like_consensus.batch import VoteBatch
@@ -77,17 +77,38 @@ def test_gpu_config2_full_size_bit_exact(engine):
     assert (res["total"] == 64).all()
 
 
+@pytest.mark.timeout(420)
 def test_gpu_config3_million_vote_chain(engine):
     n = 1_000_000
     w = synth.generate(1, n, 1_500_000, False, synth.config_seed(3), *synth.engine_signers(engine))
     res, vst = compare(engine, w.batch, w.desc, w.now, "config3")
     assert int(res[0]["status"]) == 0 and int(res[0]["total"]) == n
-    # break one received link deep in the chain: the chain check must find exactly that index
-    j = 777_777
-    off = int(w.batch.field_off[j, 2])
-    w.batch.arena[off + 3] ^= 0x01  # also invalidates vote j's own hash -> first error at j
-    res2, _ = compare(engine, w.batch, w.desc, w.now, "config3-broken")
-    assert int(res2[0]["bad_index"]) == j
+    # The mutated runs below are checked by property (one oracle pass over 1M votes is enough):
+    # every other vote keeps its status, the first error lands exactly on the mutated index.
+    arena0 = w.batch.arena.copy()
+    # (1) re-link vote j to vote j-2 and re-sign it: j passes validate_vote, the chain check
+    #     (utils.rs:188-198) must report ReceivedHashMismatch at j (j+1 also breaks; first wins)
+    j = 555_555
+    po_v = batch_to_votes(w.batch, j - 2, j + 1)
+    v = po_v[2]
+    v.received_hash = po_v[0].vote_hash
+    resign(v, int.from_bytes(w.priv[j].tobytes(), "big"))
+    for f, val in ((2, v.received_hash), (3, v.vote_hash), (4, v.signature)):
+        off, ln = int(w.batch.field_off[j, f]), int(w.batch.field_len[j, f])
+        assert ln == len(val)
+        w.batch.arena[off:off + ln] = np.frombuffer(val, np.uint8)
+    res1, vst1, _, _ = engine.validate_proposals(w.batch, w.desc, w.now)
+    assert np.array_equal(vst1, vst), "re-signed vote must still pass validate_vote"
+    assert int(res1[0]["status"]) == 11 and int(res1[0]["bad_index"]) == j  # ReceivedHashMismatch
+    # (2) flip a received-hash byte without re-signing: vote j2's own hash breaks first
+    w.batch.arena[:] = arena0
+    j2 = 777_777
+    off = int(w.batch.field_off[j2, 2])
+    w.batch.arena[off + 3] ^= 0x01
+    res2, vst2, _, _ = engine.validate_proposals(w.batch, w.desc, w.now)
+    diff = np.nonzero(vst2 != vst)[0]
+    assert diff.tolist() == [j2] and int(vst2[j2]) == 6  # InvalidVoteHash
+    assert int(res2[0]["status"]) == 6 and int(res2[0]["bad_index"]) == j2
 
 
 def test_gpu_edge_batches(engine):
