@@ -312,11 +312,15 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
     delete c;
     return set_err(HLC_EDEVICE, "stream creation failed");
   }
-  if (c->gtab.ensure(hlc::GTAB_WORDS * sizeof(uint32_t)) != 0) {
+  // fixed-base tables: the signing comb (32 x 256 points) and the recovery's u1 G comb
+  // (16 x 32768 points, 32 MiB), built once per context
+  if (c->fbtab.ensure(hlc::FBTAB_WORDS * sizeof(uint32_t)) != 0 ||
+      c->gtab.ensure(hlc::gcomb_words() * sizeof(uint32_t)) != 0) {
     delete c;
     return HLC_ENOMEM;
   }
-  hlc::launch_build_gtab(c->gtab.as<uint32_t>(), c->stream);
+  hlc::launch_build_fbtab(c->fbtab.as<uint32_t>(), c->stream);
+  hlc::launch_build_gcomb(c->gtab.as<uint32_t>(), c->fbtab.as<uint32_t>(), c->stream);
   if (hipStreamSynchronize(c->stream) != hipSuccess) {
     delete c;
     return set_err(HLC_EDEVICE, "generator table construction failed");

@@ -56,7 +56,8 @@ void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, co
                     uint8_t* verify_out, uint8_t* addr_out, hipStream_t s);
 uint64_t recover_grid_lanes();
 uint64_t recover_scratch_words();  // per-lane workspace words of k_recover
-void launch_build_gtab(uint32_t* gtab, hipStream_t s);
+void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s);  // needs fbtab
+size_t gcomb_words();
 
 // ---- validation tail ----
 void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
@@ -77,7 +78,6 @@ void launch_address(uint64_t n, const uint8_t* priv, const uint32_t* fbtab, uint
 void launch_sign(uint64_t n, const uint8_t* priv, const uint32_t* z_digest, const uint32_t* fbtab,
                  uint8_t* sig, hipStream_t s);
 
-constexpr size_t GTAB_WORDS = 2 * 128 * 16;     // odd multiples 1..255 of G and lambda*G, affine
 constexpr size_t FBTAB_WORDS = 32 * 256 * 16;   // fixed-base comb: 32 windows x 256 affine points
 
 }  // namespace hlc

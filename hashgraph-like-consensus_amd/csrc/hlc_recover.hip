@@ -42,11 +42,8 @@ __device__ __forceinline__ void fe_from_digest(fe& r, const uint32_t* w) {
 __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
                                                      const uint8_t* bytes, const uint64_t* sig_off,
                                                      const uint64_t* id_off, size_t off_stride,
-                                                     const uint32_t* gtab_g, uint32_t* scratch, uint64_t lanes,
+                                                     const uint32_t* gcomb, uint32_t* scratch, uint64_t lanes,
                                                      uint8_t* verify_out, uint8_t* addr_out) {
-  __shared__ __attribute__((aligned(16))) uint32_t gtab[GTAB_WORDS];
-  for (int k = threadIdx.x; k < (int)GTAB_WORDS; k += blockDim.x) gtab[k] = gtab_g[k];
-  __syncthreads();
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
   for (uint64_t i = tid; i < n; i += lanes) {
@@ -57,7 +54,7 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, 
     fe_load_be(s, sig + 32);
     fe_from_digest(z, z_digest + 8 * i);
     uint32_t addr[5];
-    int code = ecrecover_lane(z, r, s, sig[64], addr, gtab, ws, lanes);
+    int code = ecrecover_lane(z, r, s, sig[64], addr, gcomb, ws, lanes);
     uint8_t vr;
     if (code != SCHEME_NONE) {
       vr = (uint8_t)(1 + code);
@@ -94,27 +91,6 @@ __device__ void scalar_mul_g(gej& acc, const fe& k) {
   }
 }
 
-// odd multiples (2i+1)G and lambda*(2i+1)G, i < GTAB_N, affine
-__global__ void k_build_gtab(uint32_t* gtab) {
-  int i = threadIdx.x;
-  if (i >= GTAB_N) return;
-  fe k;
-  fe_set(k, (uint32_t)(2 * i + 1));
-  gej p;
-  scalar_mul_g(p, k);
-  fe x, y, beta, bx;
-  gej_to_affine(x, y, p);
-  fe_beta(beta);
-  fe_mul(bx, x, beta);
-#pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    gtab[i * 16 + w] = x.v[w];
-    gtab[i * 16 + 8 + w] = y.v[w];
-    gtab[(GTAB_N + i) * 16 + w] = bx.v[w];
-    gtab[(GTAB_N + i) * 16 + 8 + w] = y.v[w];
-  }
-}
-
 // fixed-base comb for signing: T[w][j] = j * 2^(8w) * G, affine; j = 0 unused
 __global__ void k_build_fbtab(uint32_t* fb) {
   const int w = blockIdx.x, j = threadIdx.x;
@@ -138,15 +114,6 @@ __global__ void k_build_fbtab(uint32_t* fb) {
   }
 }
 
-__device__ void load_ge_global(ge& g, const uint32_t* t) {
-  const uint4* p = reinterpret_cast<const uint4*>(t);
-  uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-  g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
-  g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
-  g.y.v[0] = c.x; g.y.v[1] = c.y; g.y.v[2] = c.z; g.y.v[3] = c.w;
-  g.y.v[4] = d.x; g.y.v[5] = d.y; g.y.v[6] = d.z; g.y.v[7] = d.w;
-}
-
 // k*G via the 8-bit comb (k < n)
 __device__ void fixed_base_mul(gej& acc, const fe& k, const uint32_t* fb) {
   gej_set_inf(acc);
@@ -157,6 +124,38 @@ __device__ void fixed_base_mul(gej& acc, const fe& k, const uint32_t* fb) {
       load_ge_global(g, fb + (size_t)(w * 256 + j) * 16);
       gej_add_ge(acc, acc, g);
     }
+  }
+}
+
+// The u1 G comb of the recovery (hlc_recover.hpp): T[w][j] = (2j+1) 2^(16w) G, affine, and the
+// constant top point 2^256 G.  One thread per entry, from the signing comb fbtab.
+__global__ void k_build_gcomb(uint32_t* gcomb, const uint32_t* fb) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = (uint64_t)GC_WINDOWS * GC_ENTRIES + 1;
+  if (e >= total) return;
+  fe k;
+  fe_set(k, 0);
+  if (e == total - 1) {
+    // 2^256 mod n = 2^256 - n
+    uint32_t bw = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) k.v[q] = sub_cc(0u, n_limb(q), bw);
+  } else {
+    const int w = (int)(e / GC_ENTRIES), j = (int)(e % GC_ENTRIES);
+    const uint32_t m = 2u * (uint32_t)j + 1u;  // < 2^16
+    const int bit = GC_W * w;
+    k.v[bit >> 5] = m << (bit & 31);
+    if ((bit & 31) > 16 && (bit >> 5) < 7) k.v[(bit >> 5) + 1] = m >> (32 - (bit & 31));
+  }
+  gej p;
+  fixed_base_mul(p, k, fb);
+  fe x, y;
+  gej_to_affine(x, y, p);
+  uint32_t* o = gcomb + (e == total - 1 ? GC_TOP_OFF : e * 16);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    o[q] = x.v[q];
+    o[8 + q] = y.v[q];
   }
 }
 
@@ -319,7 +318,7 @@ uint64_t recover_grid_lanes() {
 }
 
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
-                    const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gtab,
+                    const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb,
                     uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verify_out, uint8_t* addr_out,
                     hipStream_t s) {
   if (!n) return;
@@ -327,12 +326,15 @@ void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, co
   uint64_t need = (n + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
   hipLaunchKernelGGL(k_recover, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, z_digest, bytes, sig_off,
-                     id_off, off_stride, gtab, scratch, (uint64_t)blocks * REC_TPB, verify_out, addr_out);
+                     id_off, off_stride, gcomb, scratch, (uint64_t)blocks * REC_TPB, verify_out, addr_out);
 }
 
-void launch_build_gtab(uint32_t* gtab, hipStream_t s) {
-  hipLaunchKernelGGL(k_build_gtab, dim3(1), dim3(GTAB_N), 0, s, gtab);
+void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s) {
+  const uint64_t total = (uint64_t)GC_WINDOWS * GC_ENTRIES + 1;
+  hipLaunchKernelGGL(k_build_gcomb, dim3(blocks_for(total, 128)), dim3(128), 0, s, gcomb, fbtab);
 }
+
+size_t gcomb_words() { return GCOMB_WORDS; }
 
 void launch_build_fbtab(uint32_t* fbtab, hipStream_t s) {
   hipLaunchKernelGGL(k_build_fbtab, dim3(32), dim3(256), 0, s, fbtab);

@@ -9,16 +9,20 @@
 // k256's post-recovery verify_prehash always succeeds on a recovered key (it re-derives R)
 // and is therefore not repeated.
 //
-// Scalar multiplication: GLV endomorphism (lambda, beta) splits u1 and u2 into 128-bit
-// halves; one shared doubling chain of 129 steps adds
-//   u1: width-8 wNAF over odd multiples of G and lambda*G (affine, LDS-resident, 8 KB/block)
-//   u2: width-5 wNAF over odd multiples of R and lambda*R, per lane, kept in a lane-interleaved
-//       HBM/L2 workspace (128 words per lane).  The R table is built on the isomorphic curve
-//       y^2 = x^3 + 7 C^6 (C = Z(2R)) and brought to one common Z ("effective affine", as
-//       libsecp256k1's ecmult_odd_multiples_table + ge_table_set_globalz), so every addition of
-//       the main loop -- G, lambda G, R, lambda R -- is one mixed Jacobian+affine add
-//       (7M + 4S) through a single code path; the G entries are mapped into that frame with
-//       two multiplications by Zg^2, Zg^3.
+// Scalar multiplication Q = u1 G + u2 R, in two independent parts:
+//   u2 R: GLV endomorphism (lambda, beta) splits u2 into 128-bit halves b1 + b2 lambda; one
+//       doubling chain of 125 steps adds, every 5 bits, one odd multiple of R and one of
+//       lambda R ("regular" signed digits: every lane adds at the same positions).  The 16
+//       odd multiples 1..31 R live per lane in a lane-interleaved HBM/L2 workspace.  The R
+//       table is built on the isomorphic curve y^2 = x^3 + 7 C^6 (C = Z(2R)) and brought to one
+//       common Z ("effective affine", as libsecp256k1's ecmult_odd_multiples_table +
+//       ge_table_set_globalz), so every chain addition is one mixed Jacobian+affine add.
+//   u1 G: a fixed-base comb with NO doublings over a 32 MiB table resident in HBM/MALL:
+//       16 windows of 16 bits, T[w][j] = (2j+1) 2^(16w) G (affine), regular signed digits of
+//       the odd representative of u1 (u1 or n - u1, the sign folded into the digits); the
+//       recoding's top digit is provably 1, so window 16 is the constant start point 2^256 G.
+//       16 mixed additions, each table entry prefetched one window ahead.
+//   Q = (u2 R) + (u1 G) with one Jacobian addition (exceptional cases exact).
 // Inversions (r^-1 mod n, final Z^-1 mod p) use safegcd divsteps (hlc_modinv.hpp).
 #pragma once
 #include "hlc_hash.hpp"
@@ -30,20 +34,23 @@ namespace hlc {
 // the same bit positions, so a wave executes exactly one addition per window and half-scalar.
 // (A sparse wNAF is useless in SIMT: a wave runs an addition whenever ANY of its 64 lanes has a
 // non-zero digit, i.e. at nearly every position -- measured 3.0M VALU instructions per vote.)
-constexpr int W_G = 8;                          // window for G / lambda G (u1 halves)
 constexpr int W_R = 5;                          // window for R / lambda R (u2 halves)
-constexpr int M_G = 17;                         // windows: 17 * 8 = 136 >= 129 bits
 constexpr int M_R = 26;                         // windows: 26 * 5 = 130 >= 129 bits
-constexpr int TOP_BIT = 128;                    // first (most significant) chain position
-constexpr int GTAB_N = 1 << (W_G - 1);          // 128 odd multiples 1..255 (LDS, shared)
+constexpr int TOP_BIT = W_R * (M_R - 1);        // first (most significant) chain position: 125
 constexpr int RTAB_N = 1 << (W_R - 1);          // 16 odd multiples 1..31 (per lane)
-constexpr int DIG_G_WORDS = (M_G + 1) / 2;      // int16 digits, 2 per word
-constexpr int DIG_R_WORDS = (M_R + 1) / 2;
+constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
 constexpr int RTAB_WORDS = RTAB_N * 16;         // per lane (affine, common-Z frame)
-constexpr int DIG_OFF = RTAB_WORDS;             // digits: a1, a2 (G), b1, b2 (R)
-constexpr int DIG_WORDS = 2 * DIG_G_WORDS + 2 * DIG_R_WORDS;
+constexpr int DIG_OFF = RTAB_WORDS;             // digits: b1, b2 (R, lambda R)
+constexpr int DIG_WORDS = 2 * DIG_R_WORDS;
 constexpr int ZR_OFF = DIG_OFF + DIG_WORDS;     // z-ratios of the table build
 constexpr int SCRATCH_WORDS = ZR_OFF + 8 * (RTAB_N - 1);  // per lane workspace words
+
+// fixed-base comb for u1 G (global memory, built once per context by k_build_gcomb)
+constexpr int GC_W = 16;                        // bits per window
+constexpr int GC_WINDOWS = 16;                  // 16 x 16 = 256 bits; window 16 is constant
+constexpr int GC_ENTRIES = 1 << (GC_W - 1);     // odd multiples 1 .. 2^16 - 1
+constexpr size_t GC_TOP_OFF = (size_t)GC_WINDOWS * GC_ENTRIES * 16;  // 2^256 G
+constexpr size_t GCOMB_WORDS = GC_TOP_OFF + 16;
 
 enum { SCHEME_NONE = 0, SCHEME_SIG_LEN = 1, SCHEME_ID_LEN = 2, SCHEME_BAD_PARITY = 3,
        SCHEME_SCALAR_RANGE = 4, SCHEME_NO_POINT = 5, SCHEME_INFINITY = 6 };
@@ -159,13 +166,55 @@ HLC_DEV uint32_t recode_regular(const fe& k, uint32_t* ws, size_t stride) {
 
 HLC_DEV int digit16(uint32_t word, int h) { return (int)(int16_t)(word >> (16 * h)); }
 
-HLC_DEV void load_ge_lds(ge& g, const uint32_t* lds_tab, int idx) {
-  const uint4* p = reinterpret_cast<const uint4*>(lds_tab + idx * 16);
+HLC_DEV void load_ge_global(ge& g, const uint32_t* t) {
+  const uint4* p = reinterpret_cast<const uint4*>(t);
   uint4 a = p[0], b = p[1], c = p[2], d = p[3];
   g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
   g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
   g.y.v[0] = c.x; g.y.v[1] = c.y; g.y.v[2] = c.z; g.y.v[3] = c.w;
   g.y.v[4] = d.x; g.y.v[5] = d.y; g.y.v[6] = d.z; g.y.v[7] = d.w;
+}
+
+// One step of the regular recoding of an odd 256-bit x with W = 16, least significant digit
+// first: d = (x mod 2^17) - 2^16 (odd, |d| < 2^16), x = (x - d) / 2^16 (stays odd).
+HLC_DEV int comb_digit(fe& x) {
+  const int d = (int)(x.v[0] & 0x1FFFFu) - 0x10000;
+  const uint32_t nd = (uint32_t)(-d);
+  const uint32_t ext = d > 0 ? 0xFFFFFFFFu : 0u;
+  uint32_t c = 0;
+  x.v[0] = adc(x.v[0], nd, c);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) x.v[i] = adc(x.v[i], ext, c);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) x.v[i] = __builtin_amdgcn_alignbit(x.v[i + 1], x.v[i], 16);
+  x.v[7] = x.v[7] >> 16;
+  return d;
+}
+
+HLC_DEV const uint32_t* comb_entry(const uint32_t* gcomb, int w, int d) {
+  const int idx = ((d < 0 ? -d : d) - 1) >> 1;
+  return gcomb + ((size_t)w * GC_ENTRIES + (size_t)idx) * 16;
+}
+
+// acc = k G for odd k < 2^256 (neg: acc = -k G), by the comb: 2^256 G + sum_w d_w 2^(16 w) G.
+HLC_DEV void comb_mul_g(gej& acc, fe k, bool neg, const uint32_t* gcomb) {
+  ge e;
+  load_ge_global(e, gcomb + GC_TOP_OFF);
+  if (neg) fe_neg(e.y, e.y);
+  gej_set_ge(acc, e);
+  int d = comb_digit(k);
+  load_ge_global(e, comb_entry(gcomb, 0, d));
+#pragma unroll 1
+  for (int w = 0; w < GC_WINDOWS; ++w) {
+    ge cur = e;
+    const int dc = d;
+    if (w + 1 < GC_WINDOWS) {  // prefetch the next window's entry
+      d = comb_digit(k);
+      load_ge_global(e, comb_entry(gcomb, w + 1, d));
+    }
+    if ((dc < 0) != neg) fe_neg(cur.y, cur.y);
+    gej_add_ge(acc, acc, cur);
+  }
 }
 
 HLC_DEV void store_ge_ws(const fe& x, const fe& y, uint32_t* ws, size_t stride) {
@@ -252,11 +301,11 @@ HLC_DEV void pubkey_address(const fe& x, const fe& y, uint32_t addr[5]) {
   addr[4] = (uint32_t)(st[3] >> 32);
 }
 
-// Full recovery for one lane.  gtab: LDS, 2*GTAB_N affine entries (G multiples then lambda-G
-// multiples).  ws: this lane's workspace column base, stride = total lanes.
+// Full recovery for one lane.  gcomb: the fixed-base comb table (global).  ws: this lane's
+// workspace column base, stride = total lanes.
 // Returns SCHEME_* (0 on success and addr filled).
 HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr[5],
-                           const uint32_t* gtab, uint32_t* ws, size_t stride) {
+                           const uint32_t* gcomb, uint32_t* ws, size_t stride) {
   // alloy normalize_v
   int parity;
   if (v == 0u || v == 27u) parity = 0;
@@ -302,23 +351,27 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
     sc_mont_mul(u1, z, rinvR);      // z * r^-1
     sc_neg(u1, u1);
   }
-  // GLV halves + regular digits into the workspace
+  // u1 for the comb: its odd representative (u1 or n - u1, sign carried separately)
+  const bool neg_g = (u1.v[0] & 1u) == 0u;
+  if (neg_g) {
+    uint32_t bw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u1.v[i] = sub_cc(n_limb(i), u1.v[i], bw);
+  }
+  // GLV halves of u2 + regular digits into the workspace
   int negs, skews;
   {
-    fe a1, a2, b1, b2;
-    bool na1, na2, nb1, nb2;
-    glv_split(u1, a1, na1, a2, na2);
+    fe b1, b2;
+    bool nb1, nb2;
     glv_split(u2, b1, nb1, b2, nb2);
     uint32_t* dws = ws + (size_t)DIG_OFF * stride;
-    uint32_t s0 = recode_regular<W_G, M_G>(a1, dws, stride);
-    uint32_t s1 = recode_regular<W_G, M_G>(a2, dws + (size_t)DIG_G_WORDS * stride, stride);
-    uint32_t s2 = recode_regular<W_R, M_R>(b1, dws + (size_t)(2 * DIG_G_WORDS) * stride, stride);
-    uint32_t s3 = recode_regular<W_R, M_R>(b2, dws + (size_t)(2 * DIG_G_WORDS + DIG_R_WORDS) * stride, stride);
-    negs = (na1 ? 1 : 0) | (na2 ? 2 : 0) | (nb1 ? 4 : 0) | (nb2 ? 8 : 0);
-    skews = (int)(s0 | (s1 << 1) | (s2 << 2) | (s3 << 3));
+    uint32_t s2 = recode_regular<W_R, M_R>(b1, dws, stride);
+    uint32_t s3 = recode_regular<W_R, M_R>(b2, dws + (size_t)DIG_R_WORDS * stride, stride);
+    negs = (nb1 ? 1 : 0) | (nb2 ? 2 : 0);
+    skews = (int)(s2 | (s3 << 1));
   }
-  // R table on the isomorphic curve with C = Z(2R): entries (2i+1)R, i < 8, common Z
-  fe zg, zg2, zg3;  // zg = real Z of the table frame
+  // R table on the isomorphic curve with C = Z(2R): entries (2i+1)R, i < 16, common Z
+  fe zg;  // real Z of the table frame
   {
     gej d;
     gej_set_ge(d, R);
@@ -341,7 +394,7 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
       store_ge_ws(acc.x, acc.y, ws + (size_t)(16 * i) * stride, stride);
       store_fe_ws(zr, zrws + (size_t)(8 * (i - 1)) * stride, stride);
     }
-    // common Z = Z_7: entry i scaled by s_i = Z_7 / Z_i = prod_{k > i} zr_k
+    // common Z = Z_15: entry i scaled by s_i = Z_15 / Z_i = prod_{k > i} zr_k
     fe sc;
     fe_set(sc, 1);
     for (int i = RTAB_N - 2; i >= 0; --i) {
@@ -356,9 +409,7 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
       fe_mul(e.y, e.y, s3);
       store_ge_ws(e.x, e.y, ws + (size_t)(16 * i) * stride, stride);
     }
-    fe_mul(zg, acc.z, d.z);  // real Z of the frame: Z_7 * C
-    fe_sqr(zg2, zg);
-    fe_mul(zg3, zg2, zg);
+    fe_mul(zg, acc.z, d.z);  // real Z of the frame: Z_15 * C
   }
   fe beta;
   fe_beta(beta);
@@ -367,47 +418,35 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
   gej_set_inf(acc);
   for (int i = TOP_BIT; i >= 0; --i) {
     if (i != TOP_BIT) gej_double(acc, acc);
-    // half k adds at positions that are multiples of its window (uniform across the wave)
+    if (i % W_R != 0) continue;
+    const int win = i / W_R;
+    // the two halves add at the same positions (uniform across the wave)
 #pragma unroll 1
-    for (int k = 0; k < 4; ++k) {
-      const bool isg = k < 2;
-      const int w = isg ? W_G : W_R;
-      if (i % w != 0) continue;
-      const int win = i / w;
-      const size_t base = isg ? (size_t)(k * DIG_G_WORDS) : (size_t)(2 * DIG_G_WORDS + (k - 2) * DIG_R_WORDS);
-      const int d = digit16(dws[(base + (size_t)(win >> 1)) * stride], win & 1);
+    for (int k = 0; k < 2; ++k) {
+      const int d = digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
       const int idx = ((d < 0 ? -d : d) - 1) >> 1;
       ge g;
-      if (isg) {
-        load_ge_lds(g, gtab, k * GTAB_N + idx);
-        fe_mul(g.x, g.x, zg2);
-        fe_mul(g.y, g.y, zg3);
-      } else {
-        load_ge_ws(g, ws + (size_t)(16 * idx) * stride, stride);
-        if (k == 3) fe_mul(g.x, g.x, beta);
-      }
+      load_ge_ws(g, ws + (size_t)(16 * idx) * stride, stride);
+      if (k == 1) fe_mul(g.x, g.x, beta);
       if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
       gej_add_ge(acc, acc, g);
     }
   }
-  // skew corrections: the digits encoded |k| + 1 for even |k|; subtract one (signed) base point
+  // skew corrections: the digits encoded |b| + 1 for even |b|; subtract one (signed) base point
 #pragma unroll 1
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 2; ++k) {
     if (((skews >> k) & 1) == 0) continue;
     ge g;
-    if (k < 2) {
-      load_ge_lds(g, gtab, k * GTAB_N);
-      fe_mul(g.x, g.x, zg2);
-      fe_mul(g.y, g.y, zg3);
-    } else {
-      load_ge_ws(g, ws, stride);
-      if (k == 3) fe_mul(g.x, g.x, beta);
-    }
+    load_ge_ws(g, ws, stride);
+    if (k == 1) fe_mul(g.x, g.x, beta);
     if (((negs >> k) & 1) == 0) fe_neg(g.y, g.y);  // add -(sign * P)
     gej_add_ge(acc, acc, g);
   }
+  if (!acc.inf) fe_mul(acc.z, acc.z, zg);  // u2 R back on the real curve
+  gej ag;
+  comb_mul_g(ag, u1, neg_g, gcomb);
+  gej_add(acc, acc, ag);
   if (acc.inf) return SCHEME_INFINITY;
-  fe_mul(acc.z, acc.z, zg);  // back to the real curve
   fe qx, qy;
   gej_to_affine(qx, qy, acc);
   pubkey_address(qx, qy, addr);
