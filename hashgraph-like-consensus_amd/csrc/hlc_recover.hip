@@ -46,6 +46,7 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, 
                                                      uint8_t* verify_out, uint8_t* addr_out) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
+  uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tid * RTAB_WORDS;
   for (uint64_t i = tid; i < n; i += lanes) {
     if (pre && pre[i] != PRE_PENDING) continue;
     const uint8_t* sig = bytes + sig_off[i * off_stride];
@@ -54,7 +55,7 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, 
     fe_load_be(s, sig + 32);
     fe_from_digest(z, z_digest + 8 * i);
     uint32_t addr[5];
-    int code = ecrecover_lane(z, r, s, sig[64], addr, gcomb, ws, lanes);
+    int code = ecrecover_lane(z, r, s, sig[64], addr, gcomb, ws, lanes, tab);
     uint8_t vr;
     if (code != SCHEME_NONE) {
       vr = (uint8_t)(1 + code);

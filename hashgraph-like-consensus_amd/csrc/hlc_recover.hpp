@@ -39,11 +39,17 @@ constexpr int M_R = 26;                         // windows: 26 * 5 = 130 >= 129 
 constexpr int TOP_BIT = W_R * (M_R - 1);        // first (most significant) chain position: 125
 constexpr int RTAB_N = 1 << (W_R - 1);          // 16 odd multiples 1..31 (per lane)
 constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
+// Per-lane workspace, two regions:
+//  * lane-interleaved (word w of lane t at w * lanes + t: every lane touches the same word, so
+//    each access is one coalesced 256-B row per wave): the signed digits and the z-ratios;
+//  * per-lane contiguous R table (RTAB_WORDS words, 64-B entries read by 16-B vector loads):
+//    entries are gathered at lane-dependent indices, so each lane's entry must be one block.
 constexpr int RTAB_WORDS = RTAB_N * 16;         // per lane (affine, common-Z frame)
-constexpr int DIG_OFF = RTAB_WORDS;             // digits: b1, b2 (R, lambda R)
+constexpr int DIG_OFF = 0;                      // digits: b1, b2 (R, lambda R)
 constexpr int DIG_WORDS = 2 * DIG_R_WORDS;
 constexpr int ZR_OFF = DIG_OFF + DIG_WORDS;     // z-ratios of the table build
-constexpr int SCRATCH_WORDS = ZR_OFF + 8 * (RTAB_N - 1);  // per lane workspace words
+constexpr int IL_WORDS = ZR_OFF + 8 * (RTAB_N - 1);       // interleaved words per lane
+constexpr int SCRATCH_WORDS = IL_WORDS + RTAB_WORDS;      // per lane workspace words
 
 // fixed-base comb for u1 G (global memory, built once per context by k_build_gcomb)
 constexpr int GC_W = 16;                        // bits per window
@@ -225,6 +231,14 @@ HLC_DEV void store_ge_ws(const fe& x, const fe& y, uint32_t* ws, size_t stride) 
   }
 }
 
+HLC_DEV void store_ge_tab(const fe& x, const fe& y, uint32_t* t) {
+  uint4* p = reinterpret_cast<uint4*>(t);
+  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  p[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+  p[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+  p[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
+}
+
 HLC_DEV void store_fe_ws(const fe& x, uint32_t* ws, size_t stride) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) ws[(size_t)i * stride] = x.v[i];
@@ -302,10 +316,10 @@ HLC_DEV void pubkey_address(const fe& x, const fe& y, uint32_t addr[5]) {
 }
 
 // Full recovery for one lane.  gcomb: the fixed-base comb table (global).  ws: this lane's
-// workspace column base, stride = total lanes.
+// interleaved workspace column base, stride = total lanes; tab: this lane's R table.
 // Returns SCHEME_* (0 on success and addr filled).
 HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr[5],
-                           const uint32_t* gcomb, uint32_t* ws, size_t stride) {
+                           const uint32_t* gcomb, uint32_t* ws, size_t stride, uint32_t* tab) {
   // alloy normalize_v
   int parity;
   if (v == 0u || v == 27u) parity = 0;
@@ -386,12 +400,12 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
     fe_mul(acc.x, R.x, c2);
     fe_mul(acc.y, R.y, c3);
     fe_set(acc.z, 1);
-    store_ge_ws(acc.x, acc.y, ws, stride);
+    store_ge_tab(acc.x, acc.y, tab);
     uint32_t* zrws = ws + (size_t)ZR_OFF * stride;
     for (int i = 1; i < RTAB_N; ++i) {
       fe zr;
       gej_madd_zr(acc, dp, zr);  // (2i+1)R, Z_i = Z_{i-1} * zr
-      store_ge_ws(acc.x, acc.y, ws + (size_t)(16 * i) * stride, stride);
+      store_ge_tab(acc.x, acc.y, tab + 16 * i);
       store_fe_ws(zr, zrws + (size_t)(8 * (i - 1)) * stride, stride);
     }
     // common Z = Z_15: entry i scaled by s_i = Z_15 / Z_i = prod_{k > i} zr_k
@@ -404,10 +418,10 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
       fe_sqr(s2, sc);
       fe_mul(s3, s2, sc);
       ge e;
-      load_ge_ws(e, ws + (size_t)(16 * i) * stride, stride);
+      load_ge_global(e, tab + 16 * i);
       fe_mul(e.x, e.x, s2);
       fe_mul(e.y, e.y, s3);
-      store_ge_ws(e.x, e.y, ws + (size_t)(16 * i) * stride, stride);
+      store_ge_tab(e.x, e.y, tab + 16 * i);
     }
     fe_mul(zg, acc.z, d.z);  // real Z of the frame: Z_15 * C
   }
@@ -426,7 +440,7 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
       const int d = digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
       const int idx = ((d < 0 ? -d : d) - 1) >> 1;
       ge g;
-      load_ge_ws(g, ws + (size_t)(16 * idx) * stride, stride);
+      load_ge_global(g, tab + 16 * idx);
       if (k == 1) fe_mul(g.x, g.x, beta);
       if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
       gej_add_ge(acc, acc, g);
@@ -437,7 +451,7 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
   for (int k = 0; k < 2; ++k) {
     if (((skews >> k) & 1) == 0) continue;
     ge g;
-    load_ge_ws(g, ws, stride);
+    load_ge_global(g, tab);
     if (k == 1) fe_mul(g.x, g.x, beta);
     if (((negs >> k) & 1) == 0) fe_neg(g.y, g.y);  // add -(sign * P)
     gej_add_ge(acc, acc, g);

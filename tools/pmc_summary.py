@@ -8,7 +8,7 @@ for f in sorted(glob.glob(f"{root}/pmc_*/run_counter_collection.csv")):
     disp = collections.defaultdict(set)
     meta = {}
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("hlc::(anonymous namespace)::", "")
+        k = r["Kernel_Name"].replace("hlc::(anonymous namespace)::", "").split("(")[0]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
         meta[k] = f"vgpr={r['VGPR_Count']} sgpr={r['SGPR_Count']} scratch={r['Scratch_Size']} lds={r['LDS_Block_Size']} grid={r['Grid_Size']}"
