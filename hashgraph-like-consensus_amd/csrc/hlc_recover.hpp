@@ -430,21 +430,33 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
   const uint32_t* dws = ws + (size_t)DIG_OFF * stride;
   gej acc;
   gej_set_inf(acc);
-  for (int i = TOP_BIT; i >= 0; --i) {
-    if (i != TOP_BIT) gej_double(acc, acc);
-    if (i % W_R != 0) continue;
-    const int win = i / W_R;
-    // the two halves add at the same positions (uniform across the wave)
+  // Additions in order (window 25, b1), (25, b2), 5 doublings, (24, b1), ... -- the two halves
+  // add at the same positions (uniform across the wave).  The next addition's table entry is
+  // loaded before the current one is added, so its latency hides behind >= 1 addition.
+  auto digit_at = [&](int step) {
+    const int win = M_R - 1 - (step >> 1), k = step & 1;
+    return digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
+  };
+  auto entry_of = [&](int d) { return tab + 16 * (((d < 0 ? -d : d) - 1) >> 1); };
+  int d_next = digit_at(0);
+  ge g_next;
+  load_ge_global(g_next, entry_of(d_next));
 #pragma unroll 1
-    for (int k = 0; k < 2; ++k) {
-      const int d = digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
-      const int idx = ((d < 0 ? -d : d) - 1) >> 1;
-      ge g;
-      load_ge_global(g, tab + 16 * idx);
-      if (k == 1) fe_mul(g.x, g.x, beta);
-      if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
-      gej_add_ge(acc, acc, g);
+  for (int step = 0; step < 2 * M_R; ++step) {
+    const int k = step & 1;
+    if (k == 0 && step != 0) {
+#pragma unroll 1
+      for (int q = 0; q < W_R; ++q) gej_double(acc, acc);
     }
+    ge g = g_next;
+    const int d = d_next;
+    if (step + 1 < 2 * M_R) {
+      d_next = digit_at(step + 1);
+      load_ge_global(g_next, entry_of(d_next));
+    }
+    if (k == 1) fe_mul(g.x, g.x, beta);
+    if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
+    gej_add_ge(acc, acc, g);
   }
   // skew corrections: the digits encoded |b| + 1 for even |b|; subtract one (signed) base point
 #pragma unroll 1
