@@ -29,12 +29,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
 
 METRIC = "verified votes/sec (ecrecover+chain check) at 1/2/4/8 MI355X vs host CPU"
-# algorithmic work per vote, frozen before kernel tuning (Appendix D):
-# 2,480 modmul x ~550 int32 ops + 3 keccak-f + 2 SHA-256 compressions.
-W_INT32_OPS_PER_VOTE = 1.39e6
-# MI355X int32 VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (full-rate ops; v_mad_u64_u32
-# is half rate, profiles/r01_ubench_int.txt).
-VALU_INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# Roofline of the dominant kernel (k_recover, integer-VALU bound, no MFMA): its arithmetic is
+# 32x32->64-bit limb products (v_mad_u64_u32).  Algorithmic work per vote, frozen in SURVEY.md
+# §8(d) before tuning: 2,480 modmul x 136 limb products (canonical 8x32 Montgomery CIOS).
+W_LIMB_PRODUCTS_PER_VOTE = 2480 * 136
+# The implemented algorithm needs fewer (GLV + regular windows, 16-bit G comb, pseudo-Mersenne
+# fold): tools/work_model.py counts its field operations -> reported beside, never as `achieved`.
+W_IMPL_LIMB_PRODUCTS_PER_VOTE = 129_328
+# Peak: v_mad_u64_u32 is quarter rate -- 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz
+# (profiles/r01_ubench_int.txt measures 35.6 T/s).
+MAD_PEAK_T_PER_S = 256 * 4 * 16 * 2.4e9 / 1e12
 
 
 def cpu_model() -> str:
@@ -155,7 +159,7 @@ def main() -> int:
     votes_total = db.n * world * args.steps
     value = votes_total / elapsed
     rec_avg_s = rec_ms / max(rec_n, 1) / 1e3
-    achieved = W_INT32_OPS_PER_VOTE * db.n / rec_avg_s / 1e12
+    achieved = W_LIMB_PRODUCTS_PER_VOTE * db.n / rec_avg_s / 1e12
     out = {
         "metric": METRIC,
         "value": value,
@@ -180,11 +184,14 @@ def main() -> int:
             "bound": "valu",
             "kernel": "k_recover",
             "achieved": achieved,
-            "peak": VALU_INT32_PEAK_TOPS,
-            "unit": "Tops/s (int32 lane-ops)",
-            "frac": achieved / VALU_INT32_PEAK_TOPS,
+            "peak": MAD_PEAK_T_PER_S,
+            "unit": "T limb-products/s (32x32->64, v_mad_u64_u32)",
+            "frac": achieved / MAD_PEAK_T_PER_S,
             "traffic": None,
-            "work_per_vote_int32_ops": W_INT32_OPS_PER_VOTE,
+            "work_per_vote": W_LIMB_PRODUCTS_PER_VOTE,
+            "work_source": "SURVEY.md 8(d): 2,480 modmul x 136 limb products (canonical algorithm)",
+            "impl_work_per_vote": W_IMPL_LIMB_PRODUCTS_PER_VOTE,
+            "impl_mad_pipe_frac": W_IMPL_LIMB_PRODUCTS_PER_VOTE * db.n / rec_avg_s / 1e12 / MAD_PEAK_T_PER_S,
             "kernel_ms_avg": rec_avg_s * 1e3,
             "kernel_launches": rec_n,
             "call_ms_avg": call_ms / max(calls, 1),

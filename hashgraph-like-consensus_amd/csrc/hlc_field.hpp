@@ -241,86 +241,31 @@ HLC_DEV bool fe_eq_modp(const fe& a, const fe& b) {
   return fe_is_zero_modp(d);
 }
 
-// Reduce a 512-bit integer T = L + H*2^256 (t[0..15]) into [0, 2^256):
-//   x = L + H*977 + H*2^32 (9 limbs, top e < 2^33), then y = x[0..7] + e*K.
-HLC_DEV void fe_reduce512(fe& r, const uint32_t t[16]) {
-  uint32_t ml[8], mh[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint64_t m = (uint64_t)t[8 + i] * 977u;
-    ml[i] = (uint32_t)m;
-    mh[i] = (uint32_t)(m >> 32);
-  }
-  uint32_t cA = 0, cB = 0, cC = 0, x[8];
-  x[0] = adc(t[0], ml[0], cA);
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    x[i] = adc(t[i], ml[i], cA);
-    x[i] = adc(x[i], mh[i - 1], cB);
-    x[i] = adc(x[i], t[7 + i], cC);
-  }
-  uint32_t e_lo = adc(mh[7], 0u, cA);
-  e_lo = adc(e_lo, 0u, cB);
-  e_lo = adc(e_lo, t[15], cC);
-  const uint32_t e_hi = cC;  // e = e_lo + e_hi*2^32
-  // e*K = e_lo*977 + (e_hi*977 + e_lo)*2^32 + e_hi*2^64
-  const uint64_t f = (uint64_t)e_lo * 977u;
-  const uint32_t g = (uint32_t)(f >> 32) + e_hi * 977u;  // < 2^11
-  uint32_t c1 = 0, c2 = 0, y[8];
-  y[0] = adc(x[0], (uint32_t)f, c1);
-  y[1] = adc(x[1], g, c1);
-  y[1] = adc(y[1], e_lo, c2);
-  y[2] = adc(x[2], e_hi, c1);
-  y[2] = adc(y[2], 0u, c2);
-#pragma unroll
-  for (int i = 3; i < 8; ++i) y[i] = x[i];
-  uint32_t c3 = c1 + c2;
-  if (c3) {  // rare: carries past limb 2
+// c3 (<= 2) is the carry out of limb 2 of the fused reduction in hlc_field_asm.hpp: almost always
+// 0, so its propagation sits behind a branch the whole wave skips.
+HLC_DEV void fe_fix_top(uint32_t r[8], uint32_t c3) {
+  if (c3) {
     uint32_t c = 0;
-    y[3] = adc(y[3], c3, c);
+    r[3] = adc(r[3], c3, c);
 #pragma unroll
-    for (int i = 4; i < 8; ++i) y[i] = adc(y[i], 0u, c);
-    if (c) fe_add_k(y);
+    for (int i = 4; i < 8; ++i) r[i] = adc(r[i], 0u, c);
+    if (c) fe_add_k(r);  // the value was within 2^67 of 2^256: one more fold, no further carry
   }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = y[i];
 }
 
 HLC_DEV void mul512(uint32_t t[16], const fe& a, const fe& b) { mul512_asm(t, a.v, b.v); }
 
-// a^2: off-diagonal scan (28 products, asm), doubling, then the 8 diagonal squares.
-HLC_DEV void sqr512(uint32_t t[16], const fe& a) {
-  uint32_t x[16];
-  sqr_offdiag_asm(x, a.v);
-  uint32_t y[16];
-  y[15] = x[14] >> 31;
-#pragma unroll
-  for (int k = 14; k > 1; --k) y[k] = __builtin_amdgcn_alignbit(x[k], x[k - 1], 31);
-  y[1] = x[1] << 1;
-  uint32_t c = 0;
-  {
-    const uint64_t d = (uint64_t)a.v[0] * a.v[0];
-    t[0] = (uint32_t)d;
-    t[1] = adc(y[1], (uint32_t)(d >> 32), c);
-  }
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    const uint64_t d = (uint64_t)a.v[i] * a.v[i];
-    t[2 * i] = adc(y[2 * i], (uint32_t)d, c);
-    t[2 * i + 1] = adc(y[2 * i + 1], (uint32_t)(d >> 32), c);
-  }
-}
-
+// r = a * b, r = a^2: product scan with the pseudo-Mersenne reduction interleaved (asm)
 HLC_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
-  uint32_t t[16];
-  mul512(t, a, b);
-  fe_reduce512(r, t);
+  uint32_t c3;
+  fe_mul_asm(r.v, c3, a.v, b.v);
+  fe_fix_top(r.v, c3);
 }
 
 HLC_DEV void fe_sqr(fe& r, const fe& a) {
-  uint32_t t[16];
-  sqr512(t, a);
-  fe_reduce512(r, t);
+  uint32_t c3;
+  fe_sqr_asm(r.v, c3, a.v);
+  fe_fix_top(r.v, c3);
 }
 
 // r = a^(2^n) -- one call site per loop keeps code size bounded
