@@ -187,7 +187,10 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     HIPCHK(hipEventRecord(call0, s));
   }
   CHK(c->vote_prop.ensure(n * 4 + 4));
-  hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, s);
+  CHK(c->flag.ensure(16));
+  HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(uint32_t), s));
+  hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s);
+  uint32_t flags = hlc::FLAG_LARGE_PROPOSAL;  // without votes nothing was read back: be general
   uint8_t* status = dstatus;
   uint8_t* reason = dreason;
   if (!status) {
@@ -203,14 +206,11 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     CHK(c->pre_reason.ensure(n));
     CHK(c->verify.ensure(n));
     CHK(c->kec_dig.ensure(n * 32));
-    CHK(c->flag.ensure(16));
-    HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(uint32_t), s));
     hlc::launch_prehash_fused(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->kec_dig.as<uint32_t>(),
                               c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
-    uint32_t general = 0;
-    HIPCHK(hipMemcpyAsync(&general, c->flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&flags, c->flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (general) {  // some votes exceed the LDS window: general global-memory pipeline for those
+    if (flags & hlc::FLAG_GENERAL_PATH) {  // some votes exceed the LDS window: general global-memory pipeline for those
       CHK(run_prehash(c, dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
       hlc::launch_pre_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->sha_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
@@ -234,17 +234,20 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     hlc::launch_vote_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, now, c->pre.as<uint8_t>(),
                             c->pre_reason.as<uint8_t>(), c->verify.as<uint8_t>(), status, reason, s);
   }
-  uint64_t cap = 64;
-  while (cap < 2 * n) cap <<= 1;
-  CHK(c->chain_tab.ensure(cap * 4));
-  CHK(c->dup_tab.ensure(cap * 4));
   CHK(c->chain_code.ensure(n + 1));
   CHK(c->red.ensure(np * 16 + 16));
-  hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
-                     c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), s);
-  hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
-                          c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
-                          c->red.as<uint32_t>(), np, s);
+  if (flags & hlc::FLAG_LARGE_PROPOSAL) {  // proposals > 512 votes: global chain / duplicate tables
+    uint64_t cap = 64;
+    while (cap < 2 * n) cap <<= 1;
+    CHK(c->chain_tab.ensure(cap * 4));
+    CHK(c->dup_tab.ensure(cap * 4));
+    hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
+                       c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), s);
+    hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
+                            c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
+                            c->red.as<uint32_t>(), np, s);
+  }
+  hlc::launch_chain_small(dv, dprops, np, status, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), s);
   hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
   HIPCHK(hipGetLastError());
   if (c->timing) {

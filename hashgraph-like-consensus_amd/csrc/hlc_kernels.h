@@ -21,7 +21,10 @@ enum MsgMode { MSG_VOTE = 0, MSG_PAYLOAD = 1 };
 struct Workspace;  // defined in hlc_api.cpp
 
 // ---- prehash stage ----
-void launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv,
+// call flags (one device word, cleared by the caller): set by the kernels, read once per call
+constexpr uint32_t FLAG_GENERAL_PATH = 1u;     // some vote exceeds the fused prehash LDS window
+constexpr uint32_t FLAG_LARGE_PROPOSAL = 2u;   // some proposal has > 512 votes (global chain tables)
+void launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv, uint32_t* flags,
                          hipStream_t s);
 void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
                       int mode, uint64_t* sha_sz, uint64_t* kec_sz, hipStream_t s);
@@ -68,6 +71,11 @@ void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, co
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
                         uint32_t mask, uint8_t* chain_code, uint32_t* red, uint64_t np, hipStream_t s);
+// proposals with <= 512 votes: chain / duplicate / YES count in LDS, one wave per proposal
+// (writes chain_code and red for those; the global-table kernels skip them).  Run after
+// launch_chain_check (which clears red).
+void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, const uint8_t* status,
+                        uint8_t* chain_code, uint32_t* red, hipStream_t s);
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
                      const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red,
                      hlc_result* out, hipStream_t s);

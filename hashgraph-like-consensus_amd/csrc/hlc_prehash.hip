@@ -17,6 +17,8 @@ namespace hlc {
 namespace {
 
 constexpr int TPB = 256;
+constexpr uint32_t SMALL_CAP = 512;  // proposals up to this many votes: k_chain_small
+constexpr int SMALL_TPB = 64;        // one wave per proposal
 
 __device__ __forceinline__ uint32_t flen(const hlc_votes& v, uint64_t i, int f) {
   return v.field_len[i * HLC_NFIELDS + f];
@@ -60,9 +62,10 @@ __device__ uint64_t vote_enc_len(const hlc_votes& v, uint64_t i) {
   return n;
 }
 
-__global__ void k_assign_props(const hlc_proposal* props, uint32_t* vote_prop) {
+__global__ void k_assign_props(const hlc_proposal* props, uint32_t* vote_prop, uint32_t* flags) {
   const uint32_t p = blockIdx.x;
   const hlc_proposal d = props[p];
+  if (threadIdx.x == 0 && d.vote_count > SMALL_CAP) atomicOr(flags, FLAG_LARGE_PROPOSAL);
   for (uint64_t j = threadIdx.x; j < d.vote_count; j += blockDim.x) vote_prop[d.vote_begin + j] = p;
 }
 
@@ -318,7 +321,7 @@ __global__ void k_tables(hlc_votes v, uint64_t n, const uint32_t* vote_prop, con
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t p = vote_prop[i];
-  if (p == NO_PROP) return;
+  if (p == NO_PROP || props[p].vote_count <= SMALL_CAP) return;  // small: k_chain_small
   // HashMap<vote_hash, (owner, ts, idx)>: last index wins (utils.rs:180-183)
   if (props[p].vote_count > 1) table_insert<true>(chain_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_VOTE_HASH);
   // seen_owners HashSet: the first occurrence is the one later duplicates collide with
@@ -343,6 +346,7 @@ __global__ void k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop
                               uint32_t mask, uint8_t* chain_code, uint32_t* red) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t p = i < n ? vote_prop[i] : NO_PROP;
+  if (p != NO_PROP && props[p].vote_count <= SMALL_CAP) p = NO_PROP;  // small: k_chain_small
   bool yes = false;
   if (p != NO_PROP) {
     const hlc_proposal d = props[p];
@@ -383,6 +387,99 @@ __global__ void k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop
     if (p0 != NO_PROP && (threadIdx.x & 63) == 0 && y) atomicAdd(&red[4 * p0 + 3], (uint32_t)__popcll(y));
   } else if (yes) {
     atomicAdd(&red[4 * p + 3], 1u);
+  }
+}
+
+// ---------------- small proposals: one wave per proposal, no global tables ----------------
+// validate_vote_chain (utils.rs:175-215), seen_owners (session.rs:270-275) and the YES count of a
+// proposal with at most SMALL_CAP votes.  32-bit FNV keys of every owner and vote_hash sit in
+// LDS; every key hit is confirmed byte for byte, so collisions cannot change an outcome.  The
+// parent lookup scans from the last vote down (the reference's HashMap keeps the LAST index of a
+// vote_hash), the duplicate scan from the first vote up (the first repeat is the error).
+__device__ __forceinline__ uint32_t key32(const uint8_t* b, uint32_t len) {
+  uint32_t h = 2166136261u ^ (len * 0x9E3779B1u);
+  for (uint32_t k = 0; k < len; ++k) h = (h ^ b[k]) * 16777619u;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, off));
+  return x;
+}
+
+__global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hlc_proposal* props,
+                                                           const uint8_t* status, uint8_t* chain_code,
+                                                           uint32_t* red) {
+  __shared__ uint32_t h_own[SMALL_CAP], h_vh[SMALL_CAP];
+  const uint32_t p = blockIdx.x;
+  const hlc_proposal d = props[p];
+  const uint32_t nv = d.vote_count;
+  if (nv > SMALL_CAP) return;  // large proposals: global tables (k_tables / k_chain_check)
+  const uint64_t b0 = d.vote_begin;
+  for (uint32_t j = threadIdx.x; j < nv; j += SMALL_TPB) {
+    const uint64_t i = b0 + j;
+    h_own[j] = key32(fptr(v, i, HLC_F_OWNER), flen(v, i, HLC_F_OWNER));
+    h_vh[j] = key32(fptr(v, i, HLC_F_VOTE_HASH), flen(v, i, HLC_F_VOTE_HASH));
+  }
+  __syncthreads();
+  const uint32_t none = 0xFFFFFFFFu;
+  uint32_t bad = none, chain = none, dup = none, yes = 0;
+  for (uint32_t j = threadIdx.x; j < nv; j += SMALL_TPB) {
+    const uint64_t i = b0 + j;
+    uint8_t cc = HLC_OK;
+    if (nv > 1) {
+      // received link (utils.rs:188-198)
+      if (j > 0 && flen(v, i, HLC_F_RECEIVED) != 0) {
+        if (!bytes_eq(fptr(v, i, HLC_F_RECEIVED), flen(v, i, HLC_F_RECEIVED), fptr(v, i - 1, HLC_F_VOTE_HASH),
+                      flen(v, i - 1, HLC_F_VOTE_HASH)) ||
+            v.timestamp[i - 1] > v.timestamp[i])
+          cc = HLC_RECEIVED_HASH_MISMATCH;
+      }
+      // parent link (utils.rs:202-211): the last vote whose vote_hash equals parent_hash
+      const uint32_t lp = flen(v, i, HLC_F_PARENT);
+      if (cc == HLC_OK && lp != 0) {
+        const uint8_t* pb = fptr(v, i, HLC_F_PARENT);
+        const uint32_t hp = key32(pb, lp);
+        uint32_t hit = none;
+        for (uint32_t k = nv; k-- > 0;) {
+          if (h_vh[k] == hp &&
+              bytes_eq(fptr(v, b0 + k, HLC_F_VOTE_HASH), flen(v, b0 + k, HLC_F_VOTE_HASH), pb, lp)) {
+            hit = k;
+            break;
+          }
+        }
+        if (hit == none ||
+            !(bytes_eq(fptr(v, b0 + hit, HLC_F_OWNER), flen(v, b0 + hit, HLC_F_OWNER), fptr(v, i, HLC_F_OWNER),
+                       flen(v, i, HLC_F_OWNER)) &&
+              v.timestamp[b0 + hit] <= v.timestamp[i] && hit < j))
+          cc = HLC_PARENT_HASH_MISMATCH;
+      }
+    }
+    chain_code[i] = cc;
+    if (status[i] != HLC_OK) bad = min(bad, j);
+    if (cc != HLC_OK) chain = min(chain, j);
+    // seen_owners: an earlier vote with the same owner makes this one the duplicate
+    const uint32_t ho = h_own[j];
+    for (uint32_t k = 0; k < j; ++k) {
+      if (h_own[k] == ho && bytes_eq(fptr(v, b0 + k, HLC_F_OWNER), flen(v, b0 + k, HLC_F_OWNER),
+                                     fptr(v, i, HLC_F_OWNER), flen(v, i, HLC_F_OWNER))) {
+        dup = min(dup, j);
+        break;
+      }
+    }
+    yes += v.vote[i] != 0;
+  }
+  bad = wave_min(bad);
+  chain = wave_min(chain);
+  dup = wave_min(dup);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) yes += (uint32_t)__shfl_xor((int)yes, off);
+  if (threadIdx.x == 0) {
+    red[4 * p + 0] = bad;
+    red[4 * p + 1] = chain;
+    red[4 * p + 2] = dup;
+    red[4 * p + 3] = yes;
   }
 }
 
@@ -523,7 +620,7 @@ __global__ void __launch_bounds__(FUSED_TPB) k_prehash_fused(hlc_votes v, uint64
     if (sha_sz > FBUF || kec_sz > FBUF) {
       pre[i] = PRE_GENERAL;
       pre_reason[i] = 0;
-      atomicOr(general, 1u);
+      atomicOr(general, FLAG_GENERAL_PATH);
       return;
     }
     // SHA-256 input (utils.rs:39-45) + padding, then compress from LDS
@@ -655,9 +752,9 @@ void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_l
 }
 
 void launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv,
-                         hipStream_t s) {
+                         uint32_t* flags, hipStream_t s) {
   if (nv) hipMemsetAsync(vote_prop, 0xFF, nv * sizeof(uint32_t), s);
-  if (np) hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np), dim3(TPB), 0, s, props, vote_prop);
+  if (np) hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np), dim3(TPB), 0, s, props, vote_prop, flags);
 }
 
 void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
@@ -722,6 +819,12 @@ void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
   if (n)
     hipLaunchKernelGGL(k_chain_check, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, status,
                        chain_tab, dup_tab, mask, chain_code, red);
+}
+
+void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, const uint8_t* status,
+                        uint8_t* chain_code, uint32_t* red, hipStream_t s) {
+  if (np)
+    hipLaunchKernelGGL(k_chain_small, dim3((unsigned)np), dim3(SMALL_TPB), 0, s, *v, props, status, chain_code, red);
 }
 
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
