@@ -396,10 +396,35 @@ __global__ void k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop
 // LDS; every key hit is confirmed byte for byte, so collisions cannot change an outcome.  The
 // parent lookup scans from the last vote down (the reference's HashMap keeps the LAST index of a
 // vote_hash), the duplicate scan from the first vote up (the first repeat is the error).
+// cheap key of a byte field: length + first and last 4 bytes (all loads independent); a key
+// match is always confirmed with bytes_eq_fast, so any key function is correct
 __device__ __forceinline__ uint32_t key32(const uint8_t* b, uint32_t len) {
-  uint32_t h = 2166136261u ^ (len * 0x9E3779B1u);
-  for (uint32_t k = 0; k < len; ++k) h = (h ^ b[k]) * 16777619u;
+  uint32_t h = len * 0x9E3779B1u;
+  if (len >= 4) {
+    const uint32_t f = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+    const uint8_t* e = b + len - 4;
+    const uint32_t l = (uint32_t)e[0] | ((uint32_t)e[1] << 8) | ((uint32_t)e[2] << 16) | ((uint32_t)e[3] << 24);
+    h ^= f ^ __builtin_amdgcn_alignbit(l, l, 13);
+  } else {
+    for (uint32_t k = 0; k < len; ++k) h ^= (uint32_t)b[k] << (8 * k);
+  }
   return h;
+}
+
+template <int N>
+__device__ __forceinline__ bool eq_n(const uint8_t* a, const uint8_t* b) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) d |= (uint32_t)(a[k] ^ b[k]);  // every load issued before any test
+  return d == 0;
+}
+
+// bytes_eq with unrolled fast paths for the canonical field lengths (address 20, hash 32)
+__device__ __forceinline__ bool bytes_eq_fast(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+  if (al != bl) return false;
+  if (al == 32) return eq_n<32>(a, b);
+  if (al == 20) return eq_n<20>(a, b);
+  return bytes_eq(a, al, b, bl);
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
@@ -431,7 +456,7 @@ __global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hl
     if (nv > 1) {
       // received link (utils.rs:188-198)
       if (j > 0 && flen(v, i, HLC_F_RECEIVED) != 0) {
-        if (!bytes_eq(fptr(v, i, HLC_F_RECEIVED), flen(v, i, HLC_F_RECEIVED), fptr(v, i - 1, HLC_F_VOTE_HASH),
+        if (!bytes_eq_fast(fptr(v, i, HLC_F_RECEIVED), flen(v, i, HLC_F_RECEIVED), fptr(v, i - 1, HLC_F_VOTE_HASH),
                       flen(v, i - 1, HLC_F_VOTE_HASH)) ||
             v.timestamp[i - 1] > v.timestamp[i])
           cc = HLC_RECEIVED_HASH_MISMATCH;
@@ -444,13 +469,13 @@ __global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hl
         uint32_t hit = none;
         for (uint32_t k = nv; k-- > 0;) {
           if (h_vh[k] == hp &&
-              bytes_eq(fptr(v, b0 + k, HLC_F_VOTE_HASH), flen(v, b0 + k, HLC_F_VOTE_HASH), pb, lp)) {
+              bytes_eq_fast(fptr(v, b0 + k, HLC_F_VOTE_HASH), flen(v, b0 + k, HLC_F_VOTE_HASH), pb, lp)) {
             hit = k;
             break;
           }
         }
         if (hit == none ||
-            !(bytes_eq(fptr(v, b0 + hit, HLC_F_OWNER), flen(v, b0 + hit, HLC_F_OWNER), fptr(v, i, HLC_F_OWNER),
+            !(bytes_eq_fast(fptr(v, b0 + hit, HLC_F_OWNER), flen(v, b0 + hit, HLC_F_OWNER), fptr(v, i, HLC_F_OWNER),
                        flen(v, i, HLC_F_OWNER)) &&
               v.timestamp[b0 + hit] <= v.timestamp[i] && hit < j))
           cc = HLC_PARENT_HASH_MISMATCH;
@@ -462,7 +487,7 @@ __global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hl
     // seen_owners: an earlier vote with the same owner makes this one the duplicate
     const uint32_t ho = h_own[j];
     for (uint32_t k = 0; k < j; ++k) {
-      if (h_own[k] == ho && bytes_eq(fptr(v, b0 + k, HLC_F_OWNER), flen(v, b0 + k, HLC_F_OWNER),
+      if (h_own[k] == ho && bytes_eq_fast(fptr(v, b0 + k, HLC_F_OWNER), flen(v, b0 + k, HLC_F_OWNER),
                                      fptr(v, i, HLC_F_OWNER), flen(v, i, HLC_F_OWNER))) {
         dup = min(dup, j);
         break;
