@@ -503,6 +503,25 @@ int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_
   return 0;
 }
 
+int hlc_consensus_timeout_batch(hlc_ctx* ctx, uint64_t n, const hlc_session_tally* sessions, uint8_t* out_state,
+                                uint8_t* out_status) {
+  if (!ctx || (n && (!sessions || !out_state || !out_status))) return set_err(HLC_EINVAL, "NULL argument");
+  if (!n) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  CHK(upload(ctx->in_props, sessions, n, s));
+  CHK(ctx->out_misc.ensure(2 * n + 16));
+  uint8_t* d_state = ctx->out_misc.as<uint8_t>();
+  uint8_t* d_status = d_state + n;
+  hlc::launch_timeout(n, ctx->in_props.as<hlc_session_tally>(), d_state, d_status, s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out_state, d_state, n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(out_status, d_status, n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
 int hlc_eth_address_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, uint8_t* out_addr20) {
   if (!ctx || (n && (!priv32 || !out_addr20))) return set_err(HLC_EINVAL, "NULL argument");
   if (!n) return 0;

@@ -71,6 +71,8 @@ void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, co
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
                         uint32_t mask, uint8_t* chain_code, uint32_t* red, uint64_t np, hipStream_t s);
+// batched handle_consensus_timeout: new state + status per session
+void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status, hipStream_t s);
 // proposals with <= 512 votes: chain / duplicate / YES count in LDS, one wave per proposal
 // (writes chain_code and red for those; the global-table kernels skip them).  Run after
 // launch_chain_check (which clears red).

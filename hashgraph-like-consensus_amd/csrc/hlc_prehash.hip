@@ -520,8 +520,10 @@ __device__ uint32_t threshold_value(uint32_t n, double t) {
   return (uint32_t)x;
 }
 
-// utils.rs:227-286 (is_timeout = false) -> -1 None / 0 / 1
-__device__ int consensus_result(uint32_t total, uint32_t yes, uint32_t n, double t, bool liveness) {
+// utils.rs:227-286 -> -1 None / 0 / 1.  At a timeout silent peers count toward the quorum
+// (effective total = n, utils.rs:249-256).
+__device__ int consensus_result(uint32_t total, uint32_t yes, uint32_t n, double t, bool liveness,
+                                bool is_timeout = false) {
   uint32_t no = total > yes ? total - yes : 0;
   uint32_t silent = n > total ? n - total : 0;
   if (n <= 2) {
@@ -529,7 +531,7 @@ __device__ int consensus_result(uint32_t total, uint32_t yes, uint32_t n, double
     return yes == n;
   }
   uint32_t req = threshold_value(n, t);
-  if (total < req) return -1;
+  if ((is_timeout ? n : total) < req) return -1;
   uint32_t yw = yes + (liveness ? silent : 0), nw = no + (liveness ? 0 : silent);
   if (yw >= req && yw > nw) return 1;
   if (nw >= req && nw > yw) return 0;
@@ -585,6 +587,28 @@ __global__ void k_finalize(const hlc_proposal* props, uint64_t np, uint64_t now,
     }
   }
   out[p] = r;
+}
+
+// handle_consensus_timeout (service.rs:323-373) per session
+__global__ void k_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const hlc_session_tally t = ss[i];
+  uint8_t st = HLC_OK, state;
+  if (t.state == HLC_SESSION_REACHED_NO || t.state == HLC_SESSION_REACHED_YES) {
+    state = t.state;  // service.rs:331-333: an earlier result stands
+  } else {
+    const int r = consensus_result(t.total, t.yes, t.expected_voters_count, t.consensus_threshold,
+                                   t.liveness_criteria_yes != 0, true);
+    if (r < 0) {
+      state = HLC_SESSION_FAILED;  // service.rs:344-346, 362-371
+      st = HLC_INSUFFICIENT_VOTES_AT_TIMEOUT;
+    } else {
+      state = r ? HLC_SESSION_REACHED_YES : HLC_SESSION_REACHED_NO;
+    }
+  }
+  out_state[i] = state;
+  out_status[i] = st;
 }
 
 // ---------------- fused fast path: one kernel for the whole byte stage ----------------
@@ -844,6 +868,11 @@ void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
   if (n)
     hipLaunchKernelGGL(k_chain_check, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, status,
                        chain_tab, dup_tab, mask, chain_code, red);
+}
+
+void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status,
+                    hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_timeout, dim3(blocks_for(n)), dim3(TPB), 0, s, n, ss, out_state, out_status);
 }
 
 void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, const uint8_t* status,

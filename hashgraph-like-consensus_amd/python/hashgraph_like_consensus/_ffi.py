@@ -67,6 +67,19 @@ class hlc_result(ctypes.Structure):
     ]
 
 
+class hlc_session_tally(ctypes.Structure):
+    _fields_ = [
+        ("total", c_uint32),
+        ("yes", c_uint32),
+        ("expected_voters_count", c_uint32),
+        ("state", c_uint8),
+        ("liveness_criteria_yes", c_uint8),
+        ("_pad", c_uint8 * 2),
+        ("consensus_threshold", c_double),
+    ]
+
+
+assert ctypes.sizeof(hlc_session_tally) == 24
 assert ctypes.sizeof(hlc_proposal) == 56
 assert ctypes.sizeof(hlc_result) == 16
 
@@ -81,6 +94,11 @@ try:
         ("consensus_threshold", "<f8"), ("use_gossipsub_rounds", "u1"),
         ("liveness_criteria_yes", "u1"), ("_pad", "u1", (6,)),
     ])
+    SESSION_TALLY_DTYPE = np.dtype([
+        ("total", "<u4"), ("yes", "<u4"), ("expected_voters_count", "<u4"), ("state", "u1"),
+        ("liveness_criteria_yes", "u1"), ("_pad", "u1", (2,)), ("consensus_threshold", "<f8"),
+    ])
+    assert SESSION_TALLY_DTYPE.itemsize == 24
     RESULT_DTYPE = np.dtype([
         ("status", "u1"), ("transition", "u1"), ("scheme_reason", "u1"), ("_pad", "u1"),
         ("bad_index", "<u4"), ("yes", "<u4"), ("total", "<u4"),
@@ -93,7 +111,7 @@ EXPORTED_SYMBOLS = (
     "hlc_ctx_create", "hlc_ctx_destroy", "hlc_ctx_reserve", "hlc_last_error", "hlc_abi_version",
     "hlc_compute_vote_hashes", "hlc_eth_verify_batch", "hlc_validate_proposals",
     "hlc_validate_proposals_device", "hlc_eth_address_batch", "hlc_eth_sign_batch",
-    "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time",
+    "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_consensus_timeout_batch",
 )
 
 _lib = None
@@ -139,6 +157,8 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_eth_address_batch.restype = c_int
     lib.hlc_eth_sign_batch.argtypes = [vp, c_uint64, u8p, u8p, c_uint64, u64p, u32p, u8p]
     lib.hlc_eth_sign_batch.restype = c_int
+    lib.hlc_consensus_timeout_batch.argtypes = [vp, c_uint64, vp, u8p, u8p]
+    lib.hlc_consensus_timeout_batch.restype = c_int
     lib.hlc_ctx_set_kernel_timing.argtypes = [vp, c_int]
     lib.hlc_ctx_set_kernel_timing.restype = c_int
     lib.hlc_ctx_take_kernel_time.argtypes = [vp, POINTER(ctypes.c_double), u64p, POINTER(ctypes.c_double), u64p]

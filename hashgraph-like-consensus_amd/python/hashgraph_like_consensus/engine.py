@@ -103,6 +103,17 @@ class Engine:
             _ffi.ptr(st, c_uint8), _ffi.ptr(addr, c_uint8)))
         return st[:n], addr[:n]
 
+    def consensus_timeout_batch(self, sessions: np.ndarray):
+        """hlc_consensus_timeout_batch over a SESSION_TALLY_DTYPE array -> (new state u8[n],
+        status u8[n]) -- handle_consensus_timeout (service.rs:323-373) per session."""
+        sessions = np.ascontiguousarray(sessions, dtype=_ffi.SESSION_TALLY_DTYPE)
+        n = sessions.shape[0]
+        state = np.zeros(max(n, 1), np.uint8)
+        status = np.zeros(max(n, 1), np.uint8)
+        _ffi.check(self.lib.hlc_consensus_timeout_batch(self.ctx, n, c_void_p(sessions.ctypes.data) if n else None,
+                                                        _ffi.ptr(state, c_uint8), _ffi.ptr(status, c_uint8)))
+        return state[:n], status[:n]
+
     # ---- signing side -------------------------------------------------------------------
     def address_batch(self, priv: np.ndarray) -> np.ndarray:
         priv = np.ascontiguousarray(priv, dtype=np.uint8).reshape(-1, 32)

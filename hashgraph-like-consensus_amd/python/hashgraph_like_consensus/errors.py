@@ -36,6 +36,7 @@ ParentHashMismatch = _variant("ParentHashMismatch", 12, "error.rs:45")
 DuplicateVote = _variant("DuplicateVote", 13, "error.rs:27")
 MaxRoundsExceeded = _variant("MaxRoundsExceeded", 14, "error.rs:65")
 ProposalAlreadyExist = _variant("ProposalAlreadyExist", 15, "error.rs:57")
+InsufficientVotesAtTimeout = _variant("InsufficientVotesAtTimeout", 16, "error.rs:64")
 InvalidConsensusThreshold = _variant("InvalidConsensusThreshold", 100, "error.rs:13-14")
 InvalidTimeout = _variant("InvalidTimeout", 101, "error.rs:15-16")
 SessionNotActive = _variant("SessionNotActive", 102, "error.rs:53")
@@ -64,7 +65,7 @@ SCHEME_REASONS = {
 _BY_CODE = {cls.code: cls for cls in (
     ProposalExpired, VoteProposalIdMismatch, EmptyVoteOwner, EmptyVoteHash, EmptySignature, InvalidVoteHash,
     InvalidVoteSignature, TimestampOlderThanCreationTime, VoteExpired, ReceivedHashMismatch, ParentHashMismatch,
-    DuplicateVote, MaxRoundsExceeded, ProposalAlreadyExist)}
+    DuplicateVote, MaxRoundsExceeded, ProposalAlreadyExist, InsufficientVotesAtTimeout)}
 
 
 def from_status(status: int, reason: int = 0) -> ConsensusError:

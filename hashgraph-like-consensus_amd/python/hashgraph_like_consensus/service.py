@@ -5,6 +5,7 @@
 * `compute_vote_hash(es)`   utils.rs:37-52
 * `build_vote`              utils.rs:55-104
 * `ConsensusService.process_incoming_proposal(s)`  service.rs:263-279 -> session.rs:198-300
+* `ConsensusService.handle_consensus_timeout(s)`   service.rs:323-373 (batched tally)
 
 Only the slice of `ConsensusService` that sits on the validation path is mirrored: the
 duplicate-session check (`ProposalAlreadyExist`), config resolution (service.rs:444-484) and
@@ -186,6 +187,14 @@ class SessionRecord:
     yes: int
     total: int
     created_at: int
+    failed: bool = False       # ConsensusState::Failed after a timeout without a result
+
+    @property
+    def state(self) -> int:
+        """HLC_SESSION_*: 0 Active, 1 ConsensusReached(false), 2 ConsensusReached(true), 3 Failed."""
+        if self.consensus is not None:
+            return 2 if self.consensus else 1
+        return 3 if self.failed else 0
 
 
 class ConsensusService:
@@ -251,6 +260,47 @@ class ConsensusService:
                 for i, o in zip(retry, rest):
                     outcomes[i] = o
         return outcomes  # type: ignore[return-value]
+
+    def handle_consensus_timeout(self, scope: Union[str, bytes], proposal_id: int, now: int) -> bool:
+        """service.rs:323-373: the consensus result, or raises InsufficientVotesAtTimeout (the
+        session is then Failed) / SessionNotFound."""
+        res = self.handle_consensus_timeouts(scope, [proposal_id], now)[0]
+        if isinstance(res, errors.ConsensusError):
+            raise res
+        return res
+
+    def handle_consensus_timeouts(self, scope: Union[str, bytes], proposal_ids: Sequence[int],
+                                  now: int) -> List[Union[bool, errors.ConsensusError]]:
+        """Batched timeout tally: one GPU call (hlc_consensus_timeout_batch) for every session;
+        per id the result bool or the ConsensusError the reference returns."""
+        from . import _ffi
+        key = _scope_key(scope)
+        recs = [self.sessions.get((key, pid)) for pid in proposal_ids]
+        live = [r for r in recs if r is not None]
+        arr = np.zeros(len(live), dtype=_ffi.SESSION_TALLY_DTYPE)
+        for k, r in enumerate(live):
+            arr[k]["total"], arr[k]["yes"] = r.total, r.yes
+            arr[k]["expected_voters_count"] = r.proposal.expected_voters_count
+            arr[k]["state"] = r.state
+            arr[k]["liveness_criteria_yes"] = 1 if r.proposal.liveness_criteria_yes else 0
+            arr[k]["consensus_threshold"] = r.config.consensus_threshold
+        state, status = self.engine.consensus_timeout_batch(arr) if len(live) else (np.zeros(0), np.zeros(0))
+        out: List[Union[bool, errors.ConsensusError]] = []
+        k = 0
+        for r in recs:
+            if r is None:
+                out.append(errors.SessionNotFound())
+                continue
+            st, code = int(state[k]), int(status[k])
+            k += 1
+            if code:
+                r.failed = True
+                out.append(errors.from_status(code))
+            else:
+                r.consensus = st == 2
+                r.transition = TRANSITION_CONSENSUS_REACHED
+                out.append(r.consensus)
+        return out
 
     def _store(self, key: bytes, p: Proposal, cfg: ConsensusConfig, o: ProposalOutcome, now: int) -> None:
         self.sessions[(key, p.proposal_id)] = SessionRecord(p, cfg, o.transition, o.consensus, o.yes, o.total, now)

@@ -51,6 +51,7 @@ extern "C" {
 #define HLC_DUPLICATE_VOTE 13                  /* error.rs:27 */
 #define HLC_MAX_ROUNDS_EXCEEDED 14             /* error.rs:65 */
 #define HLC_PROPOSAL_ALREADY_EXIST 15          /* error.rs:57 (host-side, storage) */
+#define HLC_INSUFFICIENT_VOTES_AT_TIMEOUT 16   /* error.rs:64 (handle_consensus_timeout) */
 
 /* Sub-reason of HLC_SIGNATURE_SCHEME (the reference's Verify(String) message class). */
 #define HLC_SCHEME_NONE 0
@@ -118,6 +119,24 @@ typedef struct hlc_result {
   uint32_t total;        /* votes in the owner->vote map (status == OK) */
 } hlc_result; /* 16 bytes */
 
+/* Session state (session.rs:157-164) for the timeout tally. */
+#define HLC_SESSION_ACTIVE 0
+#define HLC_SESSION_REACHED_NO 1
+#define HLC_SESSION_REACHED_YES 2
+#define HLC_SESSION_FAILED 3
+
+/* One session as `handle_consensus_timeout` (service.rs:323-373) sees it: the counts of its
+ * owner->vote map (session.rs:167-178), its state, and the scalars of its config / proposal. */
+typedef struct hlc_session_tally {
+  uint32_t total;                 /* votes in the session (distinct owners) */
+  uint32_t yes;                   /* YES votes among them */
+  uint32_t expected_voters_count; /* Proposal.expected_voters_count */
+  uint8_t state;                  /* HLC_SESSION_* */
+  uint8_t liveness_criteria_yes;  /* Proposal.liveness_criteria_yes */
+  uint8_t _pad[2];
+  double consensus_threshold;     /* ConsensusConfig.consensus_threshold */
+} hlc_session_tally; /* 24 bytes */
+
 typedef struct hlc_ctx hlc_ctx;
 
 /* ---- Context -------------------------------------------------------------------- */
@@ -179,6 +198,14 @@ int hlc_validate_proposals_device(hlc_ctx* ctx, const hlc_votes* votes,
                                   uint64_t now, hlc_result* out_results,
                                   uint8_t* out_vote_status, uint8_t* out_vote_reason,
                                   uint8_t* out_recovered, void* stream);
+
+/* Batched `ConsensusService::handle_consensus_timeout` (service.rs:323-373)
+ * over n sessions: a session already in ConsensusReached(r) keeps it; otherwise
+ * calculate_consensus_result(..., is_timeout = true) (utils.rs:227-286) decides
+ * ConsensusReached(r) or Failed.  out_state[i] = the new HLC_SESSION_* state;
+ * out_status[i] = HLC_OK (Ok(result)) or HLC_INSUFFICIENT_VOTES_AT_TIMEOUT (Err). */
+int hlc_consensus_timeout_batch(hlc_ctx* ctx, uint64_t n, const hlc_session_tally* sessions,
+                                uint8_t* out_state, uint8_t* out_status);
 
 /* ---- Signing side (generator / embedders simulating many peers) -- */
 

@@ -518,6 +518,23 @@ def calculate_consensus_result(total: int, yes: int, n: int, t: float, liveness:
     return None
 
 
+# Session states (session.rs:157-164) as the ABI numbers them (HLC_SESSION_*)
+SESSION_ACTIVE, SESSION_REACHED_NO, SESSION_REACHED_YES, SESSION_FAILED = 0, 1, 2, 3
+INSUFFICIENT_VOTES_AT_TIMEOUT = 16  # error.rs:64
+
+
+def handle_consensus_timeout(state: int, total: int, yes: int, n: int, t: float,
+                             liveness: bool) -> Tuple[int, int]:
+    """service.rs:323-373 on one session -> (new state, status): an earlier ConsensusReached
+    stands; otherwise the timeout tally decides ConsensusReached(r) or Failed + error."""
+    if state in (SESSION_REACHED_NO, SESSION_REACHED_YES):
+        return state, OK
+    r = calculate_consensus_result(total, yes, n, t, liveness, True)
+    if r is None:
+        return SESSION_FAILED, INSUFFICIENT_VOTES_AT_TIMEOUT
+    return (SESSION_REACHED_YES if r else SESSION_REACHED_NO), OK
+
+
 @dataclass
 class ConsensusConfig:
     """session.rs:27-44 (timeout omitted: not on the validation path)."""
