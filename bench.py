@@ -34,11 +34,39 @@ METRIC = "verified votes/sec (ecrecover+chain check) at 1/2/4/8 MI355X vs host C
 # §8(d) before tuning: 2,480 modmul x 136 limb products (canonical 8x32 Montgomery CIOS).
 W_LIMB_PRODUCTS_PER_VOTE = 2480 * 136
 # The implemented algorithm needs fewer (GLV + regular windows, 16-bit G comb, pseudo-Mersenne
-# fold): tools/work_model.py counts its field operations -> reported beside, never as `achieved`.
+# fold): DESIGN.md §5 counts its field operations -> reported beside, never as `achieved`.
 W_IMPL_LIMB_PRODUCTS_PER_VOTE = 129_328
 # Peak: v_mad_u64_u32 is quarter rate -- 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz
 # (profiles/r01_ubench_int.txt measures 35.6 T/s).
 MAD_PEAK_T_PER_S = 256 * 4 * 16 * 2.4e9 / 1e12
+# rocprofv3 PMC passes of this same bench command (tools/profile.sh), committed under profiles/:
+# `traffic` = memory-side bytes per k_recover launch from FETCH_SIZE / WRITE_SIZE (KiB), with the
+# gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes).
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r01_rocprof_v10_s5")
+
+
+def pmc_traffic(kernel: str = "k_recover"):
+    """Per-launch (fetch, write, total) bytes of `kernel` from the committed PMC passes, or None."""
+    import csv
+
+    def per_launch(name: str, counter: str):
+        path = os.path.join(PMC_PROFILE, name)
+        if not os.path.exists(path):
+            return None
+        vals = []
+        with open(path, newline="") as f:
+            for row in csv.DictReader(f):
+                if f"::{kernel}(" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                    vals.append(float(row["Counter_Value"]))
+        return sum(vals) / len(vals) * 1024.0 if vals else None
+
+    fetch = per_launch("pmc_fetch.csv", "FETCH_SIZE")
+    write = per_launch("pmc_write.csv", "WRITE_SIZE")
+    if fetch is None or write is None:
+        return None
+    fetch *= 2.0  # gfx950: FETCH_SIZE reports half the bytes of 128-B requests
+    return {"fetch_bytes": fetch, "write_bytes": write, "bytes": fetch + write,
+            "source": os.path.relpath(PMC_PROFILE, ROOT)}
 
 
 def cpu_model() -> str:
@@ -160,6 +188,7 @@ def main() -> int:
     value = votes_total / elapsed
     rec_avg_s = rec_ms / max(rec_n, 1) / 1e3
     achieved = W_LIMB_PRODUCTS_PER_VOTE * db.n / rec_avg_s / 1e12
+    traffic = pmc_traffic("k_recover")
     out = {
         "metric": METRIC,
         "value": value,
@@ -187,7 +216,8 @@ def main() -> int:
             "peak": MAD_PEAK_T_PER_S,
             "unit": "T limb-products/s (32x32->64, v_mad_u64_u32)",
             "frac": achieved / MAD_PEAK_T_PER_S,
-            "traffic": None,
+            "traffic": traffic["bytes"] if traffic else None,
+            "traffic_detail": traffic,
             "work_per_vote": W_LIMB_PRODUCTS_PER_VOTE,
             "work_source": "SURVEY.md 8(d): 2,480 modmul x 136 limb products (canonical algorithm)",
             "impl_work_per_vote": W_IMPL_LIMB_PRODUCTS_PER_VOTE,
