@@ -97,6 +97,10 @@ struct hlc_ctx {
   }
   DBuf vote_prop, sha_sz, sha_off, kec_sz, kec_off, sha_buf, kec_buf, sha_dig, kec_dig, pre, pre_reason,
       verify, status, reason, chain_code, chain_tab, dup_tab, red, scan_tmp, totals, flag;
+  // wire decode: staged inputs, walk / record workspace, decoded votes (hlc_votes SoA over the wire bytes)
+  DBuf w_wire, w_moff, w_mlen, w_scope, w_vcount, w_vbegin, w_vrec_off, w_vrec_len, w_vrec_msg, w_first_bad,
+      w_vote_err, w_props, w_wout, w_res;
+  DBuf w_vid, w_pid, w_ts, w_vote, w_foff, w_flen;
 };
 
 namespace {
@@ -254,6 +258,80 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     HIPCHK(hipEventRecord(call1, s));
     c->call_ev.emplace_back(call0, call1);
   }
+  return 0;
+}
+
+// Device decode of n_msgs Proposal messages (all pointers device memory).  Fills the context's
+// decoded-vote SoA (*dv, viewing `wire` as its byte arena), dprops / dwout (caller-provided
+// device arrays of n_msgs), and *n_votes.  One host synchronisation (the vote total).
+int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* moff, const uint32_t* mlen,
+                  uint64_t nm, const hlc_scope_config* scope, uint64_t n_scope, hlc_proposal* dprops,
+                  hlc_wire_proposal* dwout, hlc_votes* dv, uint64_t* n_votes, hipStream_t s) {
+  CHK(c->w_vcount.ensure(nm * 8 + 8));
+  CHK(c->w_vbegin.ensure(nm * 8 + 8));
+  uint64_t* vcount = c->w_vcount.as<uint64_t>();
+  uint64_t* vbegin = c->w_vbegin.as<uint64_t>();
+  uint64_t nv = 0;
+  if (nm) {
+    hlc::launch_wire_walk(0, wire, moff, mlen, nm, vcount, nullptr, nullptr, nullptr, scope, n_scope, nullptr,
+                          nullptr, nullptr, s);
+    CHK(scan_sizes(c, nm, vcount, vbegin, &nv, s));
+  }
+  if (nv > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
+  CHK(c->w_vrec_off.ensure(nv * 8 + 8));
+  CHK(c->w_vrec_len.ensure(nv * 4 + 4));
+  CHK(c->w_vrec_msg.ensure(nv * 4 + 4));
+  CHK(c->w_first_bad.ensure(nm * 4 + 4));
+  CHK(c->w_vote_err.ensure(nv + 1));
+  CHK(c->w_vid.ensure(nv * 4 + 4));
+  CHK(c->w_pid.ensure(nv * 4 + 4));
+  CHK(c->w_ts.ensure(nv * 8 + 8));
+  CHK(c->w_vote.ensure(nv + 1));
+  CHK(c->w_foff.ensure(nv * 8 * HLC_NFIELDS + 8));
+  CHK(c->w_flen.ensure(nv * 4 * HLC_NFIELDS + 4));
+  dv->n = nv;
+  dv->vote_id = c->w_vid.as<uint32_t>();
+  dv->proposal_id = c->w_pid.as<uint32_t>();
+  dv->timestamp = c->w_ts.as<uint64_t>();
+  dv->vote = c->w_vote.as<uint8_t>();
+  dv->bytes = wire;
+  dv->bytes_len = wire_len;
+  dv->field_off = c->w_foff.as<uint64_t>();
+  dv->field_len = c->w_flen.as<uint32_t>();
+  if (nm) {
+    hlc::launch_wire_walk(1, wire, moff, mlen, nm, vcount, vbegin, dwout, dprops, scope, n_scope,
+                          c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(), c->w_vrec_msg.as<uint32_t>(), s);
+    HIPCHK(hipMemsetAsync(c->w_first_bad.p, 0xFF, nm * 4, s));
+    hlc::launch_wire_votes(wire, moff, mlen, nv, c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(),
+                           c->w_vrec_msg.as<uint32_t>(), vbegin, dv, c->w_vote_err.as<uint8_t>(),
+                           c->w_first_bad.as<uint32_t>(), s);
+    hlc::launch_wire_final(nm, vbegin, c->w_vote_err.as<uint8_t>(), c->w_first_bad.as<uint32_t>(), dwout, dprops, s);
+  }
+  HIPCHK(hipGetLastError());
+  *n_votes = nv;
+  return 0;
+}
+
+int check_wire_host(const uint8_t* wire, uint64_t wire_len, const uint64_t* moff, const uint32_t* mlen, uint64_t nm,
+                    const hlc_scope_config* scope, uint64_t n_scope) {
+  if (nm && (!moff || !mlen || !scope)) return set_err(HLC_EINVAL, "NULL message / scope array");
+  if (nm && n_scope != 1 && n_scope != nm) return set_err(HLC_EINVAL, "n_scope must be 1 or n_msgs");
+  for (uint64_t i = 0; i < nm; ++i) {
+    if (mlen[i] && (!wire || moff[i] + mlen[i] > wire_len || moff[i] + mlen[i] < moff[i]))
+      return set_err(HLC_EINVAL, "message (offset, length) outside the wire buffer");
+  }
+  return 0;
+}
+
+// Stages the wire inputs on the device.
+int stage_wire(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* moff, const uint32_t* mlen,
+               uint64_t nm, const hlc_scope_config* scope, uint64_t n_scope, hipStream_t s) {
+  CHK(upload(c->w_wire, wire, wire ? wire_len : 0, s));
+  CHK(upload(c->w_moff, moff, nm, s));
+  CHK(upload(c->w_mlen, mlen, nm, s));
+  CHK(upload(c->w_scope, scope, nm ? n_scope : 0, s));
+  CHK(c->w_props.ensure(nm * sizeof(hlc_proposal) + 16));
+  CHK(c->w_wout.ensure(nm * sizeof(hlc_wire_proposal) + 16));
   return 0;
 }
 
@@ -440,6 +518,104 @@ int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_propo
   if (out_vote_reason && n) HIPCHK(hipMemcpyAsync(out_vote_reason, ctx->out_reason.p, n, hipMemcpyDeviceToHost, s));
   if (out_recovered && n) HIPCHK(hipMemcpyAsync(out_recovered, ctx->out_rec.p, n * 20, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hlc_decode_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire_len, const uint64_t* msg_off,
+                         const uint32_t* msg_len, uint64_t n_msgs, const hlc_scope_config* scope, uint64_t n_scope,
+                         hlc_proposal* out_props, hlc_wire_proposal* out_wire, uint64_t* inout_n_votes,
+                         uint32_t* vote_id, uint32_t* proposal_id, uint64_t* timestamp, uint8_t* vote,
+                         uint64_t* field_off, uint32_t* field_len) {
+  if (!ctx || !inout_n_votes || (n_msgs && !out_props)) return set_err(HLC_EINVAL, "NULL argument");
+  CHK(check_wire_host(wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope));
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  CHK(stage_wire(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, s));
+  hlc_votes dv;
+  uint64_t nv = 0;
+  CHK(decode_device(ctx, ctx->w_wire.as<uint8_t>(), wire_len, ctx->w_moff.as<uint64_t>(), ctx->w_mlen.as<uint32_t>(),
+                    n_msgs, ctx->w_scope.as<hlc_scope_config>(), n_scope, ctx->w_props.as<hlc_proposal>(),
+                    ctx->w_wout.as<hlc_wire_proposal>(), &dv, &nv, s));
+  if (n_msgs) {
+    HIPCHK(hipMemcpyAsync(out_props, ctx->w_props.p, n_msgs * sizeof(hlc_proposal), hipMemcpyDeviceToHost, s));
+    if (out_wire)
+      HIPCHK(hipMemcpyAsync(out_wire, ctx->w_wout.p, n_msgs * sizeof(hlc_wire_proposal), hipMemcpyDeviceToHost, s));
+  }
+  const uint64_t cap = *inout_n_votes;
+  *inout_n_votes = nv;
+  const bool want = vote_id || proposal_id || timestamp || vote || field_off || field_len;
+  int rc = 0;
+  if (want && nv > cap) {
+    rc = set_err(HLC_ERANGE, "vote capacity too small: " + std::to_string(nv) + " votes decoded");
+  } else if (want && nv) {
+    if (!vote_id || !proposal_id || !timestamp || !vote || !field_off || !field_len)
+      return set_err(HLC_EINVAL, "vote output arrays must be all set or all NULL");
+    HIPCHK(hipMemcpyAsync(vote_id, dv.vote_id, nv * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(proposal_id, dv.proposal_id, nv * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(timestamp, dv.timestamp, nv * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(vote, dv.vote, nv, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(field_off, dv.field_off, nv * 8 * HLC_NFIELDS, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(field_len, dv.field_len, nv * 4 * HLC_NFIELDS, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  return rc;
+}
+
+int hlc_validate_wire_proposals_device(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire_len, const uint64_t* msg_off,
+                                       const uint32_t* msg_len, uint64_t n_msgs, const hlc_scope_config* scope,
+                                       uint64_t n_scope, uint64_t now, hlc_result* out_results,
+                                       hlc_wire_proposal* out_wire, void* stream) {
+  if (!ctx || (n_msgs && (!msg_off || !msg_len || !scope || !out_results)))
+    return set_err(HLC_EINVAL, "NULL argument");
+  if (n_msgs && n_scope != 1 && n_scope != n_msgs) return set_err(HLC_EINVAL, "n_scope must be 1 or n_msgs");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  CHK(ctx->w_props.ensure(n_msgs * sizeof(hlc_proposal) + 16));
+  hlc_wire_proposal* wout = out_wire;
+  if (!wout) {
+    CHK(ctx->w_wout.ensure(n_msgs * sizeof(hlc_wire_proposal) + 16));
+    wout = ctx->w_wout.as<hlc_wire_proposal>();
+  }
+  hlc_votes dv;
+  uint64_t nv = 0;
+  CHK(decode_device(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, ctx->w_props.as<hlc_proposal>(),
+                    wout, &dv, &nv, s));
+  CHK(validate_device(ctx, &dv, ctx->w_props.as<hlc_proposal>(), n_msgs, now, out_results, nullptr, nullptr, nullptr,
+                      s));
+  hlc::launch_wire_results(n_msgs, wout, out_results, s);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int hlc_validate_wire_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire_len, const uint64_t* msg_off,
+                                const uint32_t* msg_len, uint64_t n_msgs, const hlc_scope_config* scope,
+                                uint64_t n_scope, uint64_t now, hlc_result* out_results, hlc_wire_proposal* out_wire,
+                                uint64_t* out_n_votes) {
+  if (!ctx || (n_msgs && !out_results)) return set_err(HLC_EINVAL, "NULL argument");
+  CHK(check_wire_host(wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope));
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  CHK(stage_wire(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, s));
+  CHK(ctx->w_res.ensure(n_msgs * sizeof(hlc_result) + 16));
+  hlc_votes dv;
+  uint64_t nv = 0;
+  CHK(decode_device(ctx, ctx->w_wire.as<uint8_t>(), wire_len, ctx->w_moff.as<uint64_t>(), ctx->w_mlen.as<uint32_t>(),
+                    n_msgs, ctx->w_scope.as<hlc_scope_config>(), n_scope, ctx->w_props.as<hlc_proposal>(),
+                    ctx->w_wout.as<hlc_wire_proposal>(), &dv, &nv, s));
+  CHK(validate_device(ctx, &dv, ctx->w_props.as<hlc_proposal>(), n_msgs, now, ctx->w_res.as<hlc_result>(), nullptr,
+                      nullptr, nullptr, s));
+  hlc::launch_wire_results(n_msgs, ctx->w_wout.as<hlc_wire_proposal>(), ctx->w_res.as<hlc_result>(), s);
+  HIPCHK(hipGetLastError());
+  if (n_msgs) {
+    HIPCHK(hipMemcpyAsync(out_results, ctx->w_res.p, n_msgs * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
+    if (out_wire)
+      HIPCHK(hipMemcpyAsync(out_wire, ctx->w_wout.p, n_msgs * sizeof(hlc_wire_proposal), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  if (out_n_votes) *out_n_votes = nv;
   return 0;
 }
 

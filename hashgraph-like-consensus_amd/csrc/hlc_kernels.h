@@ -82,6 +82,21 @@ void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const
                      const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red,
                      hlc_result* out, hipStream_t s);
 
+// ---- wire decode (hlc_wire.hip) ----
+// pass 0: vote_count[m]; pass 1: vote records at vote_begin[m] + k, wout[m], pout[m]
+void launch_wire_walk(int pass, const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
+                      uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout,
+                      hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope, uint64_t* vrec_off,
+                      uint32_t* vrec_len, uint32_t* vrec_msg, hipStream_t s);
+// decodes vote records into `out` (device SoA); first_bad[m] (pre-set to ~0) = first failing record
+void launch_wire_votes(const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nv,
+                       const uint64_t* vrec_off, const uint32_t* vrec_len, const uint32_t* vrec_msg,
+                       const uint64_t* vote_begin, const hlc_votes* out, uint8_t* vote_err, uint32_t* first_bad,
+                       hipStream_t s);
+void launch_wire_final(uint64_t nm, const uint64_t* vote_begin, const uint8_t* vote_err, const uint32_t* first_bad,
+                       hlc_wire_proposal* wout, hlc_proposal* pout, hipStream_t s);
+void launch_wire_results(uint64_t nm, const hlc_wire_proposal* wout, hlc_result* res, hipStream_t s);
+
 // ---- signing ----
 void launch_build_fbtab(uint32_t* fbtab, hipStream_t s);
 void launch_address(uint64_t n, const uint8_t* priv, const uint32_t* fbtab, uint8_t* addr, hipStream_t s);

@@ -104,6 +104,17 @@ try:
         ("bad_index", "<u4"), ("yes", "<u4"), ("total", "<u4"),
     ])
     assert PROPOSAL_DTYPE.itemsize == 56 and RESULT_DTYPE.itemsize == 16
+    # hlc_scope_config / hlc_wire_proposal (include/hlc.h, wire decode)
+    SCOPE_CONFIG_DTYPE = np.dtype([
+        ("consensus_threshold", "<f8"), ("max_rounds", "<u4"), ("use_gossipsub_rounds", "u1"),
+        ("_pad", "u1", (3,)),
+    ])
+    WIRE_PROPOSAL_DTYPE = np.dtype([
+        ("name_off", "<u8"), ("payload_off", "<u8"), ("owner_off", "<u8"),
+        ("name_len", "<u4"), ("payload_len", "<u4"), ("owner_len", "<u4"), ("round", "<u4"),
+        ("bad_vote", "<u4"), ("decode_status", "u1"), ("_pad", "u1", (3,)),
+    ])
+    assert SCOPE_CONFIG_DTYPE.itemsize == 16 and WIRE_PROPOSAL_DTYPE.itemsize == 48
 except ImportError:  # pragma: no cover
     np = None
 
@@ -112,6 +123,7 @@ EXPORTED_SYMBOLS = (
     "hlc_compute_vote_hashes", "hlc_eth_verify_batch", "hlc_validate_proposals",
     "hlc_validate_proposals_device", "hlc_eth_address_batch", "hlc_eth_sign_batch",
     "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_consensus_timeout_batch",
+    "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
 )
 
 _lib = None
@@ -159,6 +171,15 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_eth_sign_batch.restype = c_int
     lib.hlc_consensus_timeout_batch.argtypes = [vp, c_uint64, vp, u8p, u8p]
     lib.hlc_consensus_timeout_batch.restype = c_int
+    lib.hlc_decode_proposals.argtypes = [vp, u8p, c_uint64, u64p, u32p, c_uint64, vp, c_uint64, vp, vp,
+                                         u64p, u32p, u32p, u64p, u8p, u64p, u32p]
+    lib.hlc_decode_proposals.restype = c_int
+    lib.hlc_validate_wire_proposals.argtypes = [vp, u8p, c_uint64, u64p, u32p, c_uint64, vp, c_uint64,
+                                                c_uint64, vp, vp, u64p]
+    lib.hlc_validate_wire_proposals.restype = c_int
+    lib.hlc_validate_wire_proposals_device.argtypes = [vp, vp, c_uint64, vp, vp, c_uint64, vp, c_uint64,
+                                                       c_uint64, vp, vp, vp]
+    lib.hlc_validate_wire_proposals_device.restype = c_int
     lib.hlc_ctx_set_kernel_timing.argtypes = [vp, c_int]
     lib.hlc_ctx_set_kernel_timing.restype = c_int
     lib.hlc_ctx_take_kernel_time.argtypes = [vp, POINTER(ctypes.c_double), u64p, POINTER(ctypes.c_double), u64p]

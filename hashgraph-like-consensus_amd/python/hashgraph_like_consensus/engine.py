@@ -114,6 +114,58 @@ class Engine:
                                                         _ffi.ptr(state, c_uint8), _ffi.ptr(status, c_uint8)))
         return state[:n], status[:n]
 
+    # ---- wire format (gossip bytes of consensus.proto Proposal messages) -----------------
+    @staticmethod
+    def _wire_args(wire, msg_off, msg_len, scope):
+        wire = np.ascontiguousarray(np.frombuffer(wire, np.uint8) if isinstance(wire, (bytes, bytearray)) else wire,
+                                    dtype=np.uint8)
+        msg_off = np.ascontiguousarray(msg_off, dtype=np.uint64)
+        msg_len = np.ascontiguousarray(msg_len, dtype=np.uint32)
+        scope = np.ascontiguousarray(scope, dtype=_ffi.SCOPE_CONFIG_DTYPE).reshape(-1)
+        buf = wire if wire.size else np.zeros(1, np.uint8)
+        return buf, int(wire.size), msg_off, msg_len, scope
+
+    def decode_proposals(self, wire, msg_off, msg_len, scope):
+        """hlc_decode_proposals -> (props PROPOSAL_DTYPE[m], wire_info WIRE_PROPOSAL_DTYPE[m],
+        VoteBatch of the decoded votes whose arena is `wire`)."""
+        buf, wlen, msg_off, msg_len, scope = self._wire_args(wire, msg_off, msg_len, scope)
+        m = msg_off.shape[0]
+        props = np.zeros(max(m, 1), _ffi.PROPOSAL_DTYPE)
+        winfo = np.zeros(max(m, 1), _ffi.WIRE_PROPOSAL_DTYPE)
+        nv = c_uint64(0)
+        args = (self.ctx, _ffi.ptr(buf, c_uint8), wlen, _ffi.ptr(msg_off, c_uint64), _ffi.ptr(msg_len, c_uint32), m,
+                c_void_p(scope.ctypes.data), scope.shape[0], c_void_p(props.ctypes.data),
+                c_void_p(winfo.ctypes.data), ctypes.byref(nv))
+        _ffi.check(self.lib.hlc_decode_proposals(*args, None, None, None, None, None, None))  # count only
+        n = nv.value
+        vid = np.zeros(max(n, 1), np.uint32)
+        pid = np.zeros(max(n, 1), np.uint32)
+        ts = np.zeros(max(n, 1), np.uint64)
+        vt = np.zeros(max(n, 1), np.uint8)
+        foff = np.zeros((max(n, 1), 5), np.uint64)
+        flen = np.zeros((max(n, 1), 5), np.uint32)
+        nv.value = max(n, 1)
+        _ffi.check(self.lib.hlc_decode_proposals(*args, _ffi.ptr(vid, c_uint32), _ffi.ptr(pid, c_uint32),
+                                                 _ffi.ptr(ts, c_uint64), _ffi.ptr(vt, c_uint8),
+                                                 _ffi.ptr(foff, c_uint64), _ffi.ptr(flen, c_uint32)))
+        batch = VoteBatch(vote_id=vid[:n], proposal_id=pid[:n], timestamp=ts[:n], vote=vt[:n],
+                          arena=buf[:wlen], field_off=foff[:n], field_len=flen[:n])
+        return props[:m], winfo[:m], batch
+
+    def validate_wire_proposals(self, wire, msg_off, msg_len, scope, now: int):
+        """hlc_validate_wire_proposals (process_incoming_proposal from wire bytes) ->
+        (results RESULT_DTYPE[m], wire_info WIRE_PROPOSAL_DTYPE[m], decoded vote count)."""
+        buf, wlen, msg_off, msg_len, scope = self._wire_args(wire, msg_off, msg_len, scope)
+        m = msg_off.shape[0]
+        res = np.zeros(max(m, 1), _ffi.RESULT_DTYPE)
+        winfo = np.zeros(max(m, 1), _ffi.WIRE_PROPOSAL_DTYPE)
+        nv = c_uint64(0)
+        _ffi.check(self.lib.hlc_validate_wire_proposals(
+            self.ctx, _ffi.ptr(buf, c_uint8), wlen, _ffi.ptr(msg_off, c_uint64), _ffi.ptr(msg_len, c_uint32), m,
+            c_void_p(scope.ctypes.data), scope.shape[0], now, c_void_p(res.ctypes.data),
+            c_void_p(winfo.ctypes.data), ctypes.byref(nv)))
+        return res[:m], winfo[:m], nv.value
+
     # ---- signing side -------------------------------------------------------------------
     def address_batch(self, priv: np.ndarray) -> np.ndarray:
         priv = np.ascontiguousarray(priv, dtype=np.uint8).reshape(-1, 32)

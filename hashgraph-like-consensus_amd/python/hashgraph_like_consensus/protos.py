@@ -64,3 +64,33 @@ def encode_vote(v: Vote) -> bytes:
         if val:
             out += key + _varint(len(val)) + val
     return bytes(out)
+
+
+def encode_proposal(p: Proposal) -> bytes:
+    """prost `encode_to_vec` of a Proposal (consensus.proto:5-16): fields in tag order, proto3
+    defaults omitted, each vote a length-delimited tag-14 record (signature included).  The
+    wire form the embedder's network layer hands to the device decoder (hlc_decode_proposals)."""
+    out = bytearray()
+    name = p.name.encode("utf-8") if isinstance(p.name, str) else bytes(p.name)
+    if name:
+        out += b"\x52" + _varint(len(name)) + name
+    if p.payload:
+        out += b"\x5a" + _varint(len(p.payload)) + p.payload
+    if p.proposal_id:
+        out += b"\x60" + _varint(p.proposal_id)
+    if p.proposal_owner:
+        out += b"\x6a" + _varint(len(p.proposal_owner)) + p.proposal_owner
+    for v in p.votes:
+        ev = encode_vote(v)
+        out += b"\x72" + _varint(len(ev)) + ev
+    if p.expected_voters_count:
+        out += b"\x78" + _varint(p.expected_voters_count)
+    if p.round:
+        out += b"\x80\x01" + _varint(p.round)
+    if p.timestamp:
+        out += b"\x88\x01" + _varint(p.timestamp)
+    if p.expiration_timestamp:
+        out += b"\x90\x01" + _varint(p.expiration_timestamp)
+    if p.liveness_criteria_yes:
+        out += b"\x98\x01\x01"
+    return bytes(out)

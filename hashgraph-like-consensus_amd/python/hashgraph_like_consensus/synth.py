@@ -185,3 +185,63 @@ def engine_signers(engine) -> Tuple[AddrFn, SignFn]:
         return engine.sign_batch_arena(priv, arena, off, lens, total)
 
     return addr_fn, sign_fn
+
+
+def to_wire(batch: VoteBatch, desc: np.ndarray, names=None):
+    """Encode the proposals of a (batch, desc) workload as gossip bytes: one prost `Proposal`
+    message (consensus.proto:5-16, votes included with their signatures) per proposal,
+    concatenated.  Returns (wire u8[bytes], msg_off u64[P], msg_len u32[P], scope
+    SCOPE_CONFIG_DTYPE[P]) -- the inputs of hlc_validate_wire_proposals."""
+    def vbytes(i: int) -> bytes:
+        out = bytearray()
+        vid, pid, ts = int(batch.vote_id[i]), int(batch.proposal_id[i]), int(batch.timestamp[i])
+        if vid:
+            out += b"\xa0\x01" + _varint(vid)
+        fo, fl = batch.field_off[i], batch.field_len[i]
+        arena = batch.arena
+
+        def fld(k):
+            return arena[int(fo[k]):int(fo[k]) + int(fl[k])].tobytes()
+        if fl[0]:
+            out += b"\xaa\x01" + _varint(int(fl[0])) + fld(0)
+        if pid:
+            out += b"\xb0\x01" + _varint(pid)
+        if ts:
+            out += b"\xb8\x01" + _varint(ts)
+        if batch.vote[i]:
+            out += b"\xc0\x01\x01"
+        for k, key in ((1, b"\xca\x01"), (2, b"\xd2\x01"), (3, b"\xda\x01"), (4, b"\xe2\x01")):
+            if fl[k]:
+                out += key + _varint(int(fl[k])) + fld(k)
+        return bytes(out)
+
+    msgs = []
+    for p in range(desc.shape[0]):
+        d = desc[p]
+        out = bytearray()
+        name = (names[p] if names is not None else f"proposal-{p}").encode()
+        if name:
+            out += b"\x52" + _varint(len(name)) + name
+        if int(d["proposal_id"]):
+            out += b"\x60" + _varint(int(d["proposal_id"]))
+        b0, cnt = int(d["vote_begin"]), int(d["vote_count"])
+        for i in range(b0, b0 + cnt):
+            ev = vbytes(i)
+            out += b"\x72" + _varint(len(ev)) + ev
+        for key, val in ((b"\x78", int(d["expected_voters_count"])), (b"\x80\x01", 1),
+                         (b"\x88\x01", int(d["timestamp"])), (b"\x90\x01", int(d["expiration_timestamp"]))):
+            if val:
+                out += key + _varint(val)
+        if d["liveness_criteria_yes"]:
+            out += b"\x98\x01\x01"
+        msgs.append(bytes(out))
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.uint32, count=len(msgs))
+    off = np.zeros(len(msgs), np.uint64)
+    if msgs:
+        off[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+    wire = np.frombuffer(b"".join(msgs), np.uint8).copy()
+    scope = np.zeros(desc.shape[0], _ffi.SCOPE_CONFIG_DTYPE)
+    scope["consensus_threshold"] = desc["consensus_threshold"]
+    scope["max_rounds"] = desc["max_rounds"]
+    scope["use_gossipsub_rounds"] = desc["use_gossipsub_rounds"]
+    return wire, off, lens, scope

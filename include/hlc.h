@@ -32,6 +32,7 @@ extern "C" {
 #define HLC_EDEVICE (-2)  /* HIP runtime / kernel failure */
 #define HLC_ENOMEM (-3)   /* device allocation failed */
 #define HLC_ENODEV (-4)   /* no usable gfx950 device */
+#define HLC_ERANGE (-5)   /* an output capacity is too small (the required size is reported) */
 
 /* ---- Item status codes: the hot-path subset of `ConsensusError`
  *      (/root/reference/src/error.rs:11-74).  Values are ABI. ------------------- */
@@ -52,6 +53,8 @@ extern "C" {
 #define HLC_MAX_ROUNDS_EXCEEDED 14             /* error.rs:65 */
 #define HLC_PROPOSAL_ALREADY_EXIST 15          /* error.rs:57 (host-side, storage) */
 #define HLC_INSUFFICIENT_VOTES_AT_TIMEOUT 16   /* error.rs:64 (handle_consensus_timeout) */
+#define HLC_PROPOSAL_DECODE_ERROR 17           /* wire bytes are not a Proposal (prost DecodeError,
+                                                  raised by the embedder before service.rs:263) */
 
 /* Sub-reason of HLC_SIGNATURE_SCHEME (the reference's Verify(String) message class). */
 #define HLC_SCHEME_NONE 0
@@ -137,6 +140,40 @@ typedef struct hlc_session_tally {
   double consensus_threshold;     /* ConsensusConfig.consensus_threshold */
 } hlc_session_tally; /* 24 bytes */
 
+/* ---- Wire format (consensus.proto:5-29) ------------------------
+ * prost 0.14 `DecodeError` classes, reported per message by the device decoder. */
+#define HLC_WIRE_OK 0
+#define HLC_WIRE_INVALID_VARINT 1       /* > 10 bytes, 10th byte >= 2, or out of bytes */
+#define HLC_WIRE_INVALID_KEY 2          /* key > u32::MAX */
+#define HLC_WIRE_INVALID_WIRE_TYPE 3    /* wire type 6 or 7 */
+#define HLC_WIRE_INVALID_TAG 4          /* field number 0 */
+#define HLC_WIRE_WIRE_TYPE_MISMATCH 5   /* known field with the wrong wire type */
+#define HLC_WIRE_BUFFER_UNDERFLOW 6     /* length / fixed-width value past the end */
+#define HLC_WIRE_DELIMITED_EXCEEDED 7   /* a Vote's fields run past the Vote's length */
+#define HLC_WIRE_INVALID_UTF8 8         /* Proposal.name is not UTF-8 */
+#define HLC_WIRE_UNEXPECTED_END_GROUP 9 /* end-group key without its start group */
+#define HLC_WIRE_RECURSION_LIMIT 10     /* groups nested past prost's recursion limit (100) */
+
+/* The `resolve_config` inputs (service.rs:444-484) that come from the scope, not the message:
+ * the scope's ConsensusConfig (or ConsensusConfig::gossipsub() when it has none). */
+typedef struct hlc_scope_config {
+  double consensus_threshold;     /* ConsensusConfig.consensus_threshold */
+  uint32_t max_rounds;            /* ConsensusConfig.max_rounds */
+  uint8_t use_gossipsub_rounds;   /* ConsensusConfig.use_gossipsub_rounds */
+  uint8_t _pad[3];
+} hlc_scope_config; /* 16 bytes */
+
+/* Decoded Proposal fields that validation does not consume, plus the decode outcome.
+ * Offsets are relative to the start of the message. */
+typedef struct hlc_wire_proposal {
+  uint64_t name_off, payload_off, owner_off; /* Proposal.name / payload / proposal_owner */
+  uint32_t name_len, payload_len, owner_len;
+  uint32_t round;          /* Proposal.round (tag 16) as sent; from_proposal resets it to 1 */
+  uint32_t bad_vote;       /* index of the failing `votes` record, or 0xFFFFFFFF */
+  uint8_t decode_status;   /* HLC_WIRE_*: the first error prost meets in stream order */
+  uint8_t _pad[3];
+} hlc_wire_proposal; /* 48 bytes */
+
 typedef struct hlc_ctx hlc_ctx;
 
 /* ---- Context -------------------------------------------------------------------- */
@@ -217,6 +254,44 @@ int hlc_eth_address_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, uint8
 int hlc_eth_sign_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, const uint8_t* bytes,
                        uint64_t bytes_len, const uint64_t* payload_off,
                        const uint32_t* payload_len, uint8_t* out_sig65);
+
+/* ---- Wire decode -------------------------------------------------- */
+
+/* prost `Proposal::decode` (consensus.proto:5-29) on the device for n_msgs messages, message i =
+ * wire[msg_off[i] .. + msg_len[i]] (messages may share or overlap bytes).  scope has n_scope
+ * entries: 1 (shared by every message) or n_msgs.
+ * out_props[i]: the message's hlc_proposal (vote_begin / vote_count into the decoded votes,
+ * scalars from the message and scope[i]); vote_count = 0 when decoding failed.
+ * out_wire[i] (optional): decode status and the remaining fields.
+ * Decoded votes: *inout_n_votes is the capacity of the vote arrays on entry and the number of
+ * decoded vote records on return; field_off values index `wire` itself.  When the capacity is
+ * too small nothing is written to the vote arrays and HLC_ERANGE is returned (out_props and
+ * out_wire are still written).  Vote arrays may all be NULL to query the count. */
+int hlc_decode_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire_len, const uint64_t* msg_off,
+                         const uint32_t* msg_len, uint64_t n_msgs, const hlc_scope_config* scope,
+                         uint64_t n_scope, hlc_proposal* out_props, hlc_wire_proposal* out_wire,
+                         uint64_t* inout_n_votes, uint32_t* vote_id, uint32_t* proposal_id,
+                         uint64_t* timestamp, uint8_t* vote, uint64_t* field_off, uint32_t* field_len);
+
+/* `process_incoming_proposal` (service.rs:263-279) from wire bytes: device decode, then the
+ * validate-many pipeline of hlc_validate_proposals on the decoded proposals, with no host
+ * round trip of the votes.  out_results[i].status = HLC_PROPOSAL_DECODE_ERROR (scheme_reason =
+ * HLC_WIRE_* reason, bad_index = failing vote record or 0xFFFFFFFF) when message i does not
+ * decode, else the from_proposal outcome.  out_wire (optional) as in hlc_decode_proposals;
+ * out_n_votes (optional) receives the number of decoded vote records. */
+int hlc_validate_wire_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire_len,
+                                const uint64_t* msg_off, const uint32_t* msg_len, uint64_t n_msgs,
+                                const hlc_scope_config* scope, uint64_t n_scope, uint64_t now,
+                                hlc_result* out_results, hlc_wire_proposal* out_wire,
+                                uint64_t* out_n_votes);
+
+/* Same with every pointer in DEVICE memory, enqueued on `stream` (NULL: the context's stream).
+ * One host synchronisation reads the decoded vote count (to size the workspace). */
+int hlc_validate_wire_proposals_device(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire_len,
+                                       const uint64_t* msg_off, const uint32_t* msg_len,
+                                       uint64_t n_msgs, const hlc_scope_config* scope,
+                                       uint64_t n_scope, uint64_t now, hlc_result* out_results,
+                                       hlc_wire_proposal* out_wire, void* stream);
 
 #ifdef __cplusplus
 }

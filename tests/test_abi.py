@@ -119,3 +119,44 @@ def test_ctx_create_without_gpu_reports_error():
         pytest.skip("a gfx950 device is present")
     assert rc == header_defines()["HLC_ENODEV"]
     assert lib.hlc_last_error()
+
+
+WIRE_PROBE = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "hlc.h"
+int main(void) {
+  printf("%zu %zu\n", sizeof(hlc_scope_config), sizeof(hlc_wire_proposal));
+  printf("%zu %zu %zu\n", offsetof(hlc_scope_config, consensus_threshold), offsetof(hlc_scope_config, max_rounds),
+         offsetof(hlc_scope_config, use_gossipsub_rounds));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", offsetof(hlc_wire_proposal, name_off),
+         offsetof(hlc_wire_proposal, payload_off), offsetof(hlc_wire_proposal, owner_off),
+         offsetof(hlc_wire_proposal, name_len), offsetof(hlc_wire_proposal, payload_len),
+         offsetof(hlc_wire_proposal, owner_len), offsetof(hlc_wire_proposal, round),
+         offsetof(hlc_wire_proposal, bad_vote), offsetof(hlc_wire_proposal, decode_status));
+  return 0;
+}
+"""
+
+
+def test_wire_struct_layout_and_codes(tmp_path):
+    """hlc_scope_config / hlc_wire_proposal layouts and HLC_WIRE_* codes match the Python side
+    (numpy dtypes, oracle/wire_oracle.py reason codes)."""
+    import wire_oracle as wo
+    src = tmp_path / "wprobe.c"
+    src.write_text(WIRE_PROBE)
+    exe = tmp_path / "wprobe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    lines = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    assert list(map(int, lines[0].split())) == [_ffi.SCOPE_CONFIG_DTYPE.itemsize, _ffi.WIRE_PROPOSAL_DTYPE.itemsize]
+    assert list(map(int, lines[1].split())) == [_ffi.SCOPE_CONFIG_DTYPE.fields[n][1] for n in
+                                                ("consensus_threshold", "max_rounds", "use_gossipsub_rounds")]
+    assert list(map(int, lines[2].split())) == [_ffi.WIRE_PROPOSAL_DTYPE.fields[n][1] for n in
+                                                ("name_off", "payload_off", "owner_off", "name_len", "payload_len",
+                                                 "owner_len", "round", "bad_vote", "decode_status")]
+    d = header_defines()
+    for name in ("OK", "INVALID_VARINT", "INVALID_KEY", "INVALID_WIRE_TYPE", "INVALID_TAG", "WIRE_TYPE_MISMATCH",
+                 "BUFFER_UNDERFLOW", "DELIMITED_EXCEEDED", "INVALID_UTF8", "UNEXPECTED_END_GROUP",
+                 "RECURSION_LIMIT"):
+        assert d["HLC_WIRE_" + name] == getattr(wo, name), name
+    assert d["HLC_PROPOSAL_DECODE_ERROR"] == 17 and d["HLC_ERANGE"] == -5

@@ -1,0 +1,163 @@
+"""GPU parity of the wire path (hlc_wire.hip through the C ABI) against the oracles.
+
+  * decode: fuzzed Proposal messages (valid, and mutated into every prost DecodeError class)
+    decoded on the device == oracle/wire_oracle.py (prost 0.14 restated): status, failing
+    record, every scalar and every (offset, length) of every vote;
+  * validate from wire: hlc_validate_wire_proposals on encoded workloads (clean, Byzantine, and
+    with undecodable messages mixed in) == the C oracle's from_proposal outcomes on the same
+    proposals, and == the SoA path (hlc_validate_proposals) -- bit for bit.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import coracle
+import wire_oracle as wo
+from adversarial import byzantine
+from hashgraph_like_consensus import _ffi, synth
+from hashgraph_like_consensus.protos import encode_proposal
+from helpers import oracle_workload
+from wire_fuzz import mutate, random_proposal
+
+pytestmark = pytest.mark.gpu
+THREADS = max(1, min(16, os.cpu_count() or 1))
+VOTE_FIELDS = ("vote_owner", "parent_hash", "received_hash", "vote_hash", "signature")
+
+
+def _pack(msgs):
+    lens = np.array([len(m) for m in msgs], np.uint32)
+    off = np.zeros(len(msgs), np.uint64)
+    if msgs:
+        off[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+    return np.frombuffer(b"".join(msgs) or b"\0", np.uint8)[:int(lens.sum())].copy(), off, lens
+
+
+def _scope(n, gossipsub=True):
+    sc = np.zeros(n, _ffi.SCOPE_CONFIG_DTYPE)
+    sc["consensus_threshold"] = 2.0 / 3.0
+    sc["max_rounds"] = 2 if gossipsub else 0
+    sc["use_gossipsub_rounds"] = 1 if gossipsub else 0
+    return sc
+
+
+def _check_decode(engine, msgs, scope):
+    wire, off, lens = _pack(msgs)
+    props, winfo, batch = engine.decode_proposals(wire, off, lens, scope)
+    codes = set()
+    for m, msg in enumerate(msgs):
+        code, p, bad = wo.decode_proposal_ex(msg)
+        codes.add(code)
+        w = winfo[m]
+        assert int(w["decode_status"]) == code, f"message {m}: status {int(w['decode_status'])} != {code}"
+        assert int(w["bad_vote"]) == bad, f"message {m}: bad vote"
+        d = props[m]
+        sc = scope[0] if scope.shape[0] == 1 else scope[m]
+        assert d["max_rounds"] == sc["max_rounds"] and d["use_gossipsub_rounds"] == sc["use_gossipsub_rounds"]
+        assert d["consensus_threshold"] == sc["consensus_threshold"]
+        if code != wo.OK:
+            assert int(d["vote_count"]) == 0
+            continue
+        assert (int(d["proposal_id"]), int(d["timestamp"]), int(d["expiration_timestamp"]),
+                int(d["expected_voters_count"]), bool(d["liveness_criteria_yes"])) == (
+            p.proposal_id, p.timestamp, p.expiration_timestamp, p.expected_voters_count, p.liveness_criteria_yes)
+        assert int(w["round"]) == p.round
+        for k, f in (("name", "name"), ("payload", "payload"), ("owner", "proposal_owner")):
+            assert (int(w[f"{k}_off"]), int(w[f"{k}_len"])) == getattr(p, f), f"message {m}: {f}"
+        assert int(d["vote_count"]) == len(p.votes)
+        base = int(off[m])
+        for j, v in enumerate(p.votes):
+            i = int(d["vote_begin"]) + j
+            assert (int(batch.vote_id[i]), int(batch.proposal_id[i]), int(batch.timestamp[i]),
+                    bool(batch.vote[i])) == (v.vote_id, v.proposal_id, v.timestamp, v.vote), f"msg {m} vote {j}"
+            for k, f in enumerate(VOTE_FIELDS):
+                o, ln = getattr(v, f)
+                assert int(batch.field_len[i, k]) == ln, f"msg {m} vote {j} {f} length"
+                if ln:
+                    assert int(batch.field_off[i, k]) == base + o, f"msg {m} vote {j} {f} offset"
+    return codes
+
+
+def test_gpu_decode_fuzzed_messages(engine):
+    rnd = random.Random(21)
+    msgs = []
+    for t in range(1500):
+        msg = encode_proposal(random_proposal(rnd, max_votes=5))
+        msgs.append(msg if t % 3 == 0 else mutate(rnd, msg))
+    # hand-made edge cases: empty message, groups, deep group nesting, UTF-8, delimited overrun
+    msgs += [b"", b"\xfb\x01\x08\x01\xfc\x01", b"\xfb\x01" * 120 + b"\xfc\x01" * 120,
+             b"\xfb\x01" * 99 + b"\xfc\x01" * 99, b"\x72\x08\xfb\x01" * 1 + b"\xfb\x01\xfc\x01\xfc\x01\x00\x00",
+             b"\x52\x03\xed\xa0\x80", b"\x52\x04\xf0\x9f\x98\x80", b"\x72\x02\xa0\x01\x05",
+             b"\x60" + b"\xff" * 9 + b"\x01", b"\x60" + b"\xff" * 9 + b"\x02"]
+    codes = _check_decode(engine, msgs, _scope(1))
+    assert {wo.OK, wo.INVALID_VARINT, wo.BUFFER_UNDERFLOW, wo.WIRE_TYPE_MISMATCH, wo.INVALID_UTF8,
+            wo.DELIMITED_EXCEEDED, wo.RECURSION_LIMIT} <= codes
+
+
+def test_gpu_decode_per_message_scope_and_overlap(engine):
+    rnd = random.Random(22)
+    msgs = [encode_proposal(random_proposal(rnd, max_votes=3)) for _ in range(40)]
+    sc = _scope(40)
+    sc["max_rounds"] = np.arange(40)
+    sc["use_gossipsub_rounds"] = np.arange(40) % 2
+    _check_decode(engine, msgs, sc)
+    # the same bytes referenced by two messages
+    wire, off, lens = _pack(msgs[:1])
+    props, winfo, batch = engine.decode_proposals(wire, np.array([0, 0], np.uint64), np.array([lens[0]] * 2, np.uint32),
+                                                  _scope(1))
+    assert props[0]["vote_count"] == props[1]["vote_count"] and batch.n == 2 * int(props[0]["vote_count"])
+
+
+def test_gpu_decode_empty_and_capacity(engine):
+    props, winfo, batch = engine.decode_proposals(b"", np.zeros(0, np.uint64), np.zeros(0, np.uint32), _scope(1))
+    assert props.shape[0] == 0 and batch.n == 0
+
+
+def _wire_vs_oracle(engine, w_batch, desc, now, extra_msgs=()):
+    wire, off, lens, scope = synth.to_wire(w_batch, desc)
+    if extra_msgs:  # undecodable messages appended (decode errors must not disturb the rest)
+        ew, eo, el = _pack(list(extra_msgs))
+        off = np.concatenate([off, eo + np.uint64(wire.size)])
+        lens = np.concatenate([lens, el])
+        wire = np.concatenate([wire, ew])
+        scope = np.concatenate([scope, _scope(len(extra_msgs))])
+    res, winfo, nv = engine.validate_wire_proposals(wire, off, lens, scope, now)
+    P = desc.shape[0]
+    # vote records walked (those of messages that fail later included), as hlc_decode_proposals counts them
+    props, _, dbatch = engine.decode_proposals(wire, off, lens, scope)
+    assert nv == dbatch.n and (props["vote_count"][:P] == desc["vote_count"]).all()
+    assert (winfo["decode_status"][:P] == 0).all()
+    cres, _, _, _ = coracle.validate_proposals(w_batch, desc, now, threads=THREADS)
+    bad = np.nonzero(res[:P] != cres)[0]
+    assert bad.size == 0, f"{bad.size} proposals differ from the oracle, first {bad[:5]}: {res[bad[:3]]} vs {cres[bad[:3]]}"
+    sres, _, _, _ = engine.validate_proposals(w_batch, desc, now, want_votes=False)
+    assert np.array_equal(res[:P], sres)
+    for k, m in enumerate(extra_msgs):
+        code, p, badv = wo.decode_proposal_ex(m)
+        r = res[P + k]
+        if code == wo.OK:
+            continue
+        assert (int(r["status"]), int(r["scheme_reason"]), int(r["bad_index"])) == (
+            17, code, badv)  # HLC_PROPOSAL_DECODE_ERROR
+    return res
+
+
+def test_gpu_validate_wire_clean_and_decode_errors(engine):
+    w = oracle_workload(24, 16, 16, True, 0x484C4311, name="wire-clean")
+    rnd = random.Random(23)
+    extra = [mutate(rnd, encode_proposal(random_proposal(rnd, max_votes=3))) for _ in range(60)]
+    res = _wire_vs_oracle(engine, w.batch, w.desc, w.now, extra)
+    assert (res["status"][:24] == 0).all()
+
+
+def test_gpu_validate_wire_byzantine(engine):
+    w = oracle_workload(48, 16, 16, True, 0x484C4312, name="wire-byz")
+    batch, desc, kinds = byzantine(w, fraction=1 / 3, seed=7)
+    res = _wire_vs_oracle(engine, batch, desc, w.now)
+    assert (res["status"] != 0).sum() > 0
+
+
+def test_gpu_validate_wire_p2p(engine):
+    w = oracle_workload(6, 40, 60, False, 0x484C4313, name="wire-p2p")
+    _wire_vs_oracle(engine, w.batch, w.desc, w.now)
