@@ -105,6 +105,53 @@ def cpu_baseline(workload, sample_proposals: int) -> dict:
     }
 
 
+def wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire, soa_step_s):
+    """Secondary line: the same proposals as gossip bytes -- one prost
+    `Proposal` message each, votes embedded -- resident in HBM, decoded on the device and fed to
+    the same validation pipeline (hlc_validate_wire_proposals_device).  Also the full-size
+    property check: wire-path outcomes == SoA-path outcomes for every proposal."""
+    t0 = time.perf_counter()
+    wire, off, lens, scope = synth.to_wire(w.batch, w.desc)
+    t_enc = time.perf_counter() - t0
+    dw = DeviceWire(wire, off, lens, scope, w.now, device=dev)
+
+    def step():
+        eng.validate_wire_proposals_device(dw, handle)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    res_w, res_s = dw.results_numpy(), db.results_numpy()
+    assert np.array_equal(res_w, res_s), "wire-path outcomes differ from the SoA path"
+    assert (dw.winfo_numpy()["decode_status"] == 0).all()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    step_s = el / args.steps
+    return {
+        "metric": "verified votes/s from wire bytes (device protobuf decode + validation)",
+        "value": db.n * world * args.steps / el,
+        "unit": "votes/s",
+        "ms_per_step": step_s * 1e3,
+        "wire_bytes_per_step_per_gpu": int(wire.size),
+        "decode_overhead_ms": (step_s - soa_step_s) * 1e3,
+        "decode_overhead_GBps": wire.size / max(step_s - soa_step_s, 1e-9) / 1e9,
+        "outcomes_equal_soa_path": True,
+        "host_encode_seconds": t_enc,
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,13 +161,14 @@ def main() -> int:
     ap.add_argument("--votes-per-proposal", type=int, default=64)
     ap.add_argument("--cpu-sample-proposals", type=int, default=10_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wire", action="store_true", help="skip the wire-bytes leg (device protobuf decode)")
     args = ap.parse_args()
 
     import numpy as np
     import torch
 
     from hashgraph_like_consensus import synth
-    from hashgraph_like_consensus.device import DeviceBatch
+    from hashgraph_like_consensus.device import DeviceBatch, DeviceWire
     from hashgraph_like_consensus.engine import Engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -229,6 +277,9 @@ def main() -> int:
         },
         "gen_seconds": t_gen,
     }
+    if not args.no_wire:
+        out["wire"] = wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire,
+                               elapsed / args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, min(args.cpu_sample_proposals, P))
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

@@ -57,3 +57,39 @@ class DeviceBatch:
 
     def status_numpy(self) -> np.ndarray:
         return self.status[: self.n].cpu().numpy()
+
+
+class DeviceWire:
+    """Gossip bytes of n Proposal messages resident in HBM (synth.to_wire layout) for
+    hlc_validate_wire_proposals_device."""
+
+    def __init__(self, wire: np.ndarray, msg_off: np.ndarray, msg_len: np.ndarray, scope: np.ndarray, now: int,
+                 device: str = "cuda:0"):
+        import torch
+        from ctypes import c_void_p
+
+        def up(a):
+            a = np.ascontiguousarray(a)
+            return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(device)
+
+        self.n_msgs = int(msg_off.shape[0])
+        self.n_scope = int(scope.shape[0])
+        self.wire_len = int(wire.size)
+        self.now = int(now)
+        self._t = {"wire": up(wire if wire.size else np.zeros(1, np.uint8)), "off": up(msg_off.astype(np.uint64)),
+                   "len": up(msg_len.astype(np.uint32)), "scope": up(scope)}
+        self.results = torch.zeros(self.n_msgs * 16 + 16, dtype=torch.uint8, device=device)
+        self.winfo = torch.zeros(self.n_msgs * 48 + 48, dtype=torch.uint8, device=device)
+        t = self._t
+        self.wire_ptr = c_void_p(t["wire"].data_ptr())
+        self.off_ptr = c_void_p(t["off"].data_ptr())
+        self.len_ptr = c_void_p(t["len"].data_ptr())
+        self.scope_ptr = c_void_p(t["scope"].data_ptr())
+        self.results_ptr = c_void_p(self.results.data_ptr())
+        self.winfo_ptr = c_void_p(self.winfo.data_ptr())
+
+    def results_numpy(self) -> np.ndarray:
+        return self.results[: self.n_msgs * 16].cpu().numpy().view(_ffi.RESULT_DTYPE)
+
+    def winfo_numpy(self) -> np.ndarray:
+        return self.winfo[: self.n_msgs * 48].cpu().numpy().view(_ffi.WIRE_PROPOSAL_DTYPE)

@@ -200,6 +200,14 @@ class Engine:
             dbatch.results_ptr, dbatch.status_ptr, dbatch.reason_ptr, None,
             c_void_p(stream_handle) if stream_handle else None))
 
+    def validate_wire_proposals_device(self, dwire, stream_handle: int = 0) -> None:
+        """hlc_validate_wire_proposals_device over a `device.DeviceWire` (wire bytes, message
+        extents and scope configs in HBM); results land in dwire.results."""
+        _ffi.check(self.lib.hlc_validate_wire_proposals_device(
+            self.ctx, dwire.wire_ptr, dwire.wire_len, dwire.off_ptr, dwire.len_ptr, dwire.n_msgs, dwire.scope_ptr,
+            dwire.n_scope, dwire.now, dwire.results_ptr, dwire.winfo_ptr,
+            c_void_p(stream_handle) if stream_handle else None))
+
     def set_kernel_timing(self, enable: bool) -> None:
         _ffi.check(self.lib.hlc_ctx_set_kernel_timing(self.ctx, 1 if enable else 0))
 
