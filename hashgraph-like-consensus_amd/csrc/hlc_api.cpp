@@ -101,6 +101,9 @@ struct hlc_ctx {
   DBuf w_wire, w_moff, w_mlen, w_scope, w_vcount, w_vbegin, w_vrec_off, w_vrec_len, w_vrec_msg, w_first_bad,
       w_vote_err, w_props, w_wout, w_res;
   DBuf w_vid, w_pid, w_ts, w_vote, w_foff, w_flen;
+  // streaming votes
+  DBuf s_vsess, s_sessions, s_owners, s_osess, s_props, s_keys, s_iota, s_order, s_segb, s_sege, s_tab, s_sort_tmp,
+      s_st, s_tr, s_ins;
 };
 
 namespace {
@@ -179,6 +182,47 @@ int ensure_fbtab(hlc_ctx* c) {
   return 0;
 }
 
+// Per-vote validate_vote stage (utils.rs:127-171; plus the proposal_id match of utils.rs:113-115)
+// for votes already mapped to proposals (vote_prop, NO_PROP = skip): fused LDS prehash, the
+// general path for oversize votes, signature recovery, status assembly.  c->flag must hold the
+// flags of the mapping step (cleared or set by launch_assign_props); *flags receives them.
+int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t now,
+               uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* flags, hipStream_t s) {
+  const uint64_t n = dv->n;
+  CHK(c->pre.ensure(n));
+  CHK(c->pre_reason.ensure(n));
+  CHK(c->verify.ensure(n));
+  CHK(c->kec_dig.ensure(n * 32));
+  hlc::launch_prehash_fused(dv, n, vote_prop, dprops, c->kec_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
+                            c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
+  HIPCHK(hipMemcpyAsync(flags, c->flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (*flags & hlc::FLAG_GENERAL_PATH) {  // some votes exceed the LDS window: general global-memory pipeline for those
+    CHK(run_prehash(c, dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
+    hlc::launch_pre_status(dv, n, vote_prop, dprops, c->sha_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
+                           c->pre_reason.as<uint8_t>(), s);
+  }
+  CHK(ensure_recover_scratch(c));
+  if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
+  hipEvent_t r0 = nullptr, r1 = nullptr;
+  if (c->timing) {
+    r0 = c->take_event();
+    r1 = c->take_event();
+    HIPCHK(hipEventRecord(r0, s));
+  }
+  hlc::launch_recover(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_SIGNATURE,
+                      dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(),
+                      c->rec_lanes, c->verify.as<uint8_t>(), drec, s);
+  if (c->timing) {
+    HIPCHK(hipEventRecord(r1, s));
+    c->rec_ev.emplace_back(r0, r1);
+  }
+  hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
+                          c->verify.as<uint8_t>(), status, reason, s);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 // Device-resident validate-many (every pointer is device memory).
 int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops, uint64_t np, uint64_t now,
                     hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s) {
@@ -205,39 +249,7 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     CHK(c->reason.ensure(n + 1));
     reason = c->reason.as<uint8_t>();
   }
-  if (n) {
-    CHK(c->pre.ensure(n));
-    CHK(c->pre_reason.ensure(n));
-    CHK(c->verify.ensure(n));
-    CHK(c->kec_dig.ensure(n * 32));
-    hlc::launch_prehash_fused(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->kec_dig.as<uint32_t>(),
-                              c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
-    HIPCHK(hipMemcpyAsync(&flags, c->flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (flags & hlc::FLAG_GENERAL_PATH) {  // some votes exceed the LDS window: general global-memory pipeline for those
-      CHK(run_prehash(c, dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
-      hlc::launch_pre_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->sha_dig.as<uint32_t>(),
-                             c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
-    }
-    CHK(ensure_recover_scratch(c));
-    if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
-    hipEvent_t r0 = nullptr, r1 = nullptr;
-    if (c->timing) {
-      r0 = c->take_event();
-      r1 = c->take_event();
-      HIPCHK(hipEventRecord(r0, s));
-    }
-    hlc::launch_recover(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
-                        dv->field_off + HLC_F_SIGNATURE, dv->field_off + HLC_F_OWNER, HLC_NFIELDS,
-                        c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(), c->rec_lanes,
-                        c->verify.as<uint8_t>(), drec, s);
-    if (c->timing) {
-      HIPCHK(hipEventRecord(r1, s));
-      c->rec_ev.emplace_back(r0, r1);
-    }
-    hlc::launch_vote_status(dv, n, c->vote_prop.as<uint32_t>(), dprops, now, c->pre.as<uint8_t>(),
-                            c->pre_reason.as<uint8_t>(), c->verify.as<uint8_t>(), status, reason, s);
-  }
+  if (n) CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, now, status, reason, drec, &flags, s));
   CHK(c->chain_code.ensure(n + 1));
   CHK(c->red.ensure(np * 16 + 16));
   if (flags & hlc::FLAG_LARGE_PROPOSAL) {  // proposals > 512 votes: global chain / duplicate tables
@@ -616,6 +628,89 @@ int hlc_validate_wire_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire
   }
   HIPCHK(hipStreamSynchronize(s));
   if (out_n_votes) *out_n_votes = nv;
+  return 0;
+}
+
+int hlc_process_votes(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote_session, hlc_session* sessions,
+                      uint64_t n_sessions, const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
+                      uint64_t now, uint8_t* out_status, uint8_t* out_transition, uint8_t* out_inserted,
+                      uint8_t* out_reason) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  CHK(check_votes_host(votes));
+  const uint64_t n = votes->n;
+  if (n && (!vote_session || !out_status || !out_transition || !out_inserted))
+    return set_err(HLC_EINVAL, "NULL vote_session / output array");
+  if (n_sessions && !sessions) return set_err(HLC_EINVAL, "sessions is NULL");
+  if (n_owners && (!owners || !owner_session)) return set_err(HLC_EINVAL, "NULL owner arrays");
+  if (n_sessions >= hlc::NO_PROP || n + n_owners > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "batch too large");
+  for (uint64_t i = 0; i < n; ++i)
+    if (vote_session[i] != hlc::NO_PROP && vote_session[i] >= n_sessions)
+      return set_err(HLC_EINVAL, "vote_session index out of range");
+  for (uint64_t k = 0; k < n_owners; ++k)
+    if (owner_session[k] >= n_sessions) return set_err(HLC_EINVAL, "owner_session index out of range");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  hlc_votes dv;
+  CHK(stage_votes(ctx, votes, &dv, s));
+  CHK(upload(ctx->s_vsess, vote_session, n, s));
+  CHK(upload(ctx->s_sessions, sessions, n_sessions, s));
+  CHK(upload(ctx->s_owners, owners, n_owners * 20, s));
+  CHK(upload(ctx->s_osess, owner_session, n_owners, s));
+  CHK(ctx->s_props.ensure(n_sessions * sizeof(hlc_proposal) + 16));
+  const uint32_t* vsess = ctx->s_vsess.as<uint32_t>();
+  hlc_session* dss = ctx->s_sessions.as<hlc_session>();
+  hlc_proposal* dprops = ctx->s_props.as<hlc_proposal>();
+  hlc::launch_sessions_to_props(dss, n_sessions, dprops, s);
+  // 1. validate_vote for every vote against its session's proposal (same kernels as validate-many)
+  CHK(ctx->status.ensure(n + 1));
+  CHK(ctx->reason.ensure(n + 1));
+  CHK(ctx->flag.ensure(16));
+  HIPCHK(hipMemsetAsync(ctx->flag.p, 0, sizeof(uint32_t), s));
+  uint32_t flags = 0;
+  if (n) CHK(vote_stage(ctx, &dv, vsess, dprops, now, ctx->status.as<uint8_t>(), ctx->reason.as<uint8_t>(), nullptr,
+                        &flags, s));
+  // 2. each session's votes in delivery order
+  CHK(ctx->s_keys.ensure(n * 4 + 4));
+  CHK(ctx->s_iota.ensure(n * 4 + 4));
+  CHK(ctx->s_order.ensure(n * 4 + 4));
+  size_t tb = 0;
+  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
+                              ctx->s_order.as<uint32_t>(), nullptr, tb, s);
+  CHK(ctx->s_sort_tmp.ensure(tb + 16));
+  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
+                              ctx->s_order.as<uint32_t>(), ctx->s_sort_tmp.p, tb, s);
+  CHK(ctx->s_segb.ensure(n_sessions * 4 + 4));
+  CHK(ctx->s_sege.ensure(n_sessions * 4 + 4));
+  HIPCHK(hipMemsetAsync(ctx->s_segb.p, 0, n_sessions * 4 + 4, s));
+  HIPCHK(hipMemsetAsync(ctx->s_sege.p, 0, n_sessions * 4 + 4, s));
+  hlc::launch_segments(ctx->s_keys.as<uint32_t>(), n, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(), s);
+  // 3. (session, owner) table: existing owner maps, then add_vote in order per session
+  uint64_t cap = 64;
+  while (cap < 2 * (n + n_owners)) cap <<= 1;
+  CHK(ctx->s_tab.ensure(cap * 4));
+  HIPCHK(hipMemsetAsync(ctx->s_tab.p, 0xFF, cap * 4, s));
+  hlc::launch_owner_insert(ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1), ctx->s_owners.as<uint8_t>(),
+                           ctx->s_osess.as<uint32_t>(), n_owners, &dv, vsess, s);
+  CHK(ctx->s_st.ensure(n + 1));
+  CHK(ctx->s_tr.ensure(n + 1));
+  CHK(ctx->s_ins.ensure(n + 1));
+  hlc::launch_stream_init(n, vsess, ctx->status.as<uint8_t>(), ctx->s_st.as<uint8_t>(), ctx->s_tr.as<uint8_t>(),
+                          ctx->s_ins.as<uint8_t>(), s);
+  hlc::launch_apply_votes(dss, n_sessions, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(),
+                          ctx->s_order.as<uint32_t>(), &dv, now, ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1),
+                          ctx->s_owners.as<uint8_t>(), ctx->s_osess.as<uint32_t>(), n_owners, vsess,
+                          ctx->s_st.as<uint8_t>(), ctx->s_tr.as<uint8_t>(), ctx->s_ins.as<uint8_t>(), s);
+  HIPCHK(hipGetLastError());
+  if (n) {
+    HIPCHK(hipMemcpyAsync(out_status, ctx->s_st.p, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_transition, ctx->s_tr.p, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_inserted, ctx->s_ins.p, n, hipMemcpyDeviceToHost, s));
+    if (out_reason) HIPCHK(hipMemcpyAsync(out_reason, ctx->reason.p, n, hipMemcpyDeviceToHost, s));
+  }
+  if (n_sessions)
+    HIPCHK(hipMemcpyAsync(sessions, dss, n_sessions * sizeof(hlc_session), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
 

@@ -1,0 +1,266 @@
+// hlc_stream.hip -- the streaming vote path: many independent
+// `ConsensusService::process_incoming_vote` calls (service.rs:286-305) micro-batched across
+// sessions.  Per-vote validation (validate_vote, utils.rs:127-171) runs through the same
+// prehash / recovery / status kernels as validate-many; this file holds the session side:
+//   k_sessions_to_props  session -> hlc_proposal (the scalars validate_vote reads)
+//   radix sort of (session, vote index), stable -> each session's votes in delivery order
+//   k_owner_insert       existing owner maps -> one global (session, owner) hash table
+//   k_apply_votes        one lane per session walks its votes in order: add_vote
+//                        (session.rs:225-249) with check_round_limit / update_round /
+//                        check_consensus (session.rs:306-387) and the duplicate-owner test
+//                        against the table (insert on accept)
+// Integer work on a few bytes per vote; the sequential part is per session only.
+#include <hipcub/hipcub.hpp>
+
+#include "hlc_kernels.h"
+#include "hlc_tally.hpp"
+
+namespace hlc {
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+
+inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB); }
+
+__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ uint32_t owner_hash(uint32_t session, const uint8_t* owner) {
+  uint32_t h = 0x9E3779B9u ^ session * 0x85EBCA6Bu;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    h ^= ld_le32(owner + 4 * k) * 0xCC9E2D51u;
+    h = (h << 13) | (h >> 19);
+    h = h * 5u + 0xE6546B64u;
+  }
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  return h;
+}
+
+struct OwnerKeys {
+  const uint8_t* owners;          // existing owners, 20 B each
+  const uint32_t* owner_session;  // their sessions
+  uint64_t n_owners;
+  const uint8_t* bytes;           // vote arena
+  const uint64_t* field_off;      // [n][HLC_NFIELDS]
+  const uint32_t* vote_session;   // [n]
+};
+
+__device__ __forceinline__ void key_of(const OwnerKeys& k, uint32_t ref, uint32_t& session, const uint8_t*& owner) {
+  if (ref < k.n_owners) {
+    session = k.owner_session[ref];
+    owner = k.owners + 20ull * ref;
+  } else {
+    const uint64_t v = ref - k.n_owners;
+    session = k.vote_session[v];
+    owner = k.bytes + k.field_off[v * HLC_NFIELDS + HLC_F_OWNER];
+  }
+}
+
+__device__ __forceinline__ bool same_owner(const uint8_t* a, const uint8_t* b) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) d |= (uint32_t)(a[k] ^ b[k]);
+  return d == 0;
+}
+
+// Find (session, owner) or insert ref.  Returns true when the key was already present.
+// Slots are never deleted, so a lane always re-finds the keys it inserted itself.
+__device__ bool find_or_insert(uint32_t* tab, uint32_t mask, const OwnerKeys& k, uint32_t session,
+                               const uint8_t* owner, uint32_t ref) {
+  uint32_t slot = owner_hash(session, owner) & mask;
+  for (;;) {
+    uint32_t cur = __hip_atomic_load(tab + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == EMPTY) {
+      cur = atomicCAS(tab + slot, EMPTY, ref);
+      if (cur == EMPTY) return false;
+    }
+    uint32_t s2;
+    const uint8_t* o2;
+    key_of(k, cur, s2, o2);
+    if (s2 == session && same_owner(o2, owner)) return true;
+    slot = (slot + 1) & mask;
+  }
+}
+
+__global__ void __launch_bounds__(TPB) k_sessions_to_props(const hlc_session* __restrict__ ss, uint64_t m,
+                                                           hlc_proposal* __restrict__ props) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= m) return;
+  const hlc_session x = ss[s];
+  hlc_proposal p;
+  p.vote_begin = 0;
+  p.vote_count = 0;
+  p.proposal_id = x.proposal_id;
+  p.timestamp = x.timestamp;
+  p.expiration_timestamp = x.expiration_timestamp;
+  p.expected_voters_count = x.expected_voters_count;
+  p.max_rounds = x.max_rounds;
+  p.consensus_threshold = x.consensus_threshold;
+  p.use_gossipsub_rounds = x.use_gossipsub_rounds;
+  p.liveness_criteria_yes = x.liveness_criteria_yes;
+  for (int k = 0; k < 6; ++k) p._pad[k] = 0;
+  props[s] = p;
+}
+
+__global__ void __launch_bounds__(TPB) k_iota(uint32_t* __restrict__ v, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+// segment [seg_begin[s], seg_end[s]) of each session in the sorted order (pre-zeroed)
+__global__ void __launch_bounds__(TPB) k_segments(const uint32_t* __restrict__ key, uint64_t n,
+                                                  uint32_t* __restrict__ seg_begin, uint32_t* __restrict__ seg_end) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t s = key[j];
+  if (s == NO_PROP) return;
+  if (j == 0 || key[j - 1] != s) seg_begin[s] = (uint32_t)j;
+  if (j + 1 == n || key[j + 1] != s) seg_end[s] = (uint32_t)(j + 1);
+}
+
+__global__ void __launch_bounds__(TPB) k_owner_insert(uint32_t* tab, uint32_t mask, OwnerKeys k) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= k.n_owners) return;
+  find_or_insert(tab, mask, k, k.owner_session[r], k.owners + 20ull * r, (uint32_t)r);
+}
+
+// per vote: SessionNotFound or the validate_vote status (the session side may override OK)
+__global__ void __launch_bounds__(TPB) k_stream_init(uint64_t n, const uint32_t* __restrict__ vote_session,
+                                                     const uint8_t* __restrict__ vstatus, uint8_t* __restrict__ st,
+                                                     uint8_t* __restrict__ tr, uint8_t* __restrict__ ins) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st[i] = vote_session[i] == NO_PROP ? (uint8_t)HLC_SESSION_NOT_FOUND : vstatus[i];
+  tr[i] = HLC_STILL_ACTIVE;
+  ins[i] = 0;
+}
+
+// ConsensusSession::add_vote for every validated vote of session s, in delivery order.
+__global__ void __launch_bounds__(TPB) k_apply_votes(hlc_session* __restrict__ ss, uint64_t m,
+                                                     const uint32_t* __restrict__ seg_begin,
+                                                     const uint32_t* __restrict__ seg_end,
+                                                     const uint32_t* __restrict__ order, const uint8_t* vote,
+                                                     uint64_t now, uint32_t* tab, uint32_t mask, OwnerKeys k,
+                                                     uint8_t* __restrict__ st, uint8_t* __restrict__ tr,
+                                                     uint8_t* __restrict__ ins) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= m) return;
+  const uint32_t b = seg_begin[s], e = seg_end[s];
+  if (b >= e) return;
+  hlc_session x = ss[s];
+  for (uint32_t j = b; j < e; ++j) {
+    const uint32_t i = order[j];
+    if (st[i] != HLC_OK) continue;  // validate_vote failed: the session is not touched
+    uint8_t code = HLC_OK, trans = HLC_STILL_ACTIVE;
+    if (x.state == HLC_SESSION_REACHED_NO || x.state == HLC_SESSION_REACHED_YES) {
+      trans = x.state == HLC_SESSION_REACHED_YES ? HLC_REACHED_YES : HLC_REACHED_NO;  // session.rs:247
+    } else if (x.state != HLC_SESSION_ACTIVE) {
+      code = HLC_SESSION_NOT_ACTIVE;  // session.rs:248
+    } else if (now >= x.expiration_timestamp) {
+      code = HLC_PROPOSAL_EXPIRED;  // session.rs:232, utils.rs:320-328
+    } else {
+      // check_round_limit(1), session.rs:306-344
+      uint32_t projected;
+      if (x.use_gossipsub_rounds) {
+        projected = (x.round == 2 || x.round == 1) ? 2u : x.round;
+      } else {
+        const uint32_t cur = x.round ? x.round - 1 : 0;
+        projected = cur == 0xFFFFFFFFu ? cur : cur + 1;
+      }
+      const uint32_t limit =
+          x.use_gossipsub_rounds ? x.max_rounds
+                                 : (x.max_rounds ? x.max_rounds : threshold_value(x.expected_voters_count,
+                                                                                  x.consensus_threshold));
+      if (1u > x.expected_voters_count || projected > limit) {
+        x.state = HLC_SESSION_FAILED;
+        code = HLC_MAX_ROUNDS_EXCEEDED;
+      } else {
+        const uint8_t* owner = k.bytes + k.field_off[(uint64_t)i * HLC_NFIELDS + HLC_F_OWNER];
+        if (find_or_insert(tab, mask, k, (uint32_t)s, owner, (uint32_t)(k.n_owners + i))) {
+          code = HLC_DUPLICATE_VOTE;  // session.rs:236-238
+        } else {
+          ins[i] = 1;
+          x.total += 1;
+          x.yes += vote[i] ? 1u : 0u;
+          if (x.use_gossipsub_rounds) {  // update_round(1), session.rs:350-366
+            if (x.round == 1) x.round = 2;
+          } else if (x.round != 0xFFFFFFFFu) {
+            x.round += 1;
+          }
+          const int c = consensus_result(x.total, x.yes, x.expected_voters_count, x.consensus_threshold,
+                                         x.liveness_criteria_yes != 0);  // check_consensus, session.rs:372-387
+          x.state = c < 0 ? HLC_SESSION_ACTIVE : (c ? HLC_SESSION_REACHED_YES : HLC_SESSION_REACHED_NO);
+          trans = c < 0 ? HLC_STILL_ACTIVE : (c ? HLC_REACHED_YES : HLC_REACHED_NO);
+        }
+      }
+    }
+    st[i] = code;
+    tr[i] = trans;
+  }
+  ss[s] = x;
+}
+
+}  // namespace
+
+void launch_sessions_to_props(const hlc_session* ss, uint64_t m, hlc_proposal* props, hipStream_t s) {
+  if (!m) return;
+  hipLaunchKernelGGL(k_sessions_to_props, dim3(blocks_for(m)), dim3(TPB), 0, s, ss, m, props);
+}
+
+void launch_sort_by_session(const uint32_t* vote_session, uint64_t n, uint32_t* keys_out, uint32_t* iota,
+                            uint32_t* order, void* temp, size_t& temp_bytes, hipStream_t s) {
+  if (!temp) {
+    hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, vote_session, keys_out, iota, order, (int)n, 0, 32, s);
+    return;
+  }
+  if (!n) return;
+  hipLaunchKernelGGL(k_iota, dim3(blocks_for(n)), dim3(TPB), 0, s, iota, n);
+  hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, vote_session, keys_out, iota, order, (int)n, 0, 32, s);
+}
+
+void launch_segments(const uint32_t* keys, uint64_t n, uint32_t* seg_begin, uint32_t* seg_end, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_segments, dim3(blocks_for(n)), dim3(TPB), 0, s, keys, n, seg_begin, seg_end);
+}
+
+static OwnerKeys owner_keys(const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
+                            const hlc_votes* v, const uint32_t* vote_session) {
+  OwnerKeys k;
+  k.owners = owners;
+  k.owner_session = owner_session;
+  k.n_owners = n_owners;
+  k.bytes = v->bytes;
+  k.field_off = v->field_off;
+  k.vote_session = vote_session;
+  return k;
+}
+
+void launch_owner_insert(uint32_t* tab, uint32_t mask, const uint8_t* owners, const uint32_t* owner_session,
+                         uint64_t n_owners, const hlc_votes* v, const uint32_t* vote_session, hipStream_t s) {
+  if (!n_owners) return;
+  hipLaunchKernelGGL(k_owner_insert, dim3(blocks_for(n_owners)), dim3(TPB), 0, s, tab, mask,
+                     owner_keys(owners, owner_session, n_owners, v, vote_session));
+}
+
+void launch_stream_init(uint64_t n, const uint32_t* vote_session, const uint8_t* vstatus, uint8_t* st, uint8_t* tr,
+                        uint8_t* ins, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_stream_init, dim3(blocks_for(n)), dim3(TPB), 0, s, n, vote_session, vstatus, st, tr, ins);
+}
+
+void launch_apply_votes(hlc_session* ss, uint64_t m, const uint32_t* seg_begin, const uint32_t* seg_end,
+                        const uint32_t* order, const hlc_votes* v, uint64_t now, uint32_t* tab, uint32_t mask,
+                        const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
+                        const uint32_t* vote_session, uint8_t* st, uint8_t* tr, uint8_t* ins, hipStream_t s) {
+  if (!m) return;
+  hipLaunchKernelGGL(k_apply_votes, dim3(blocks_for(m)), dim3(TPB), 0, s, ss, m, seg_begin, seg_end, order, v->vote,
+                     now, tab, mask, owner_keys(owners, owner_session, n_owners, v, vote_session), st, tr, ins);
+}
+
+}  // namespace hlc

@@ -115,6 +115,14 @@ try:
         ("bad_vote", "<u4"), ("decode_status", "u1"), ("_pad", "u1", (3,)),
     ])
     assert SCOPE_CONFIG_DTYPE.itemsize == 16 and WIRE_PROPOSAL_DTYPE.itemsize == 48
+    # hlc_session (include/hlc.h, streaming votes)
+    SESSION_DTYPE = np.dtype([
+        ("timestamp", "<u8"), ("expiration_timestamp", "<u8"), ("proposal_id", "<u4"),
+        ("expected_voters_count", "<u4"), ("round", "<u4"), ("total", "<u4"), ("yes", "<u4"),
+        ("max_rounds", "<u4"), ("consensus_threshold", "<f8"), ("state", "u1"), ("use_gossipsub_rounds", "u1"),
+        ("liveness_criteria_yes", "u1"), ("_pad", "u1", (5,)),
+    ])
+    assert SESSION_DTYPE.itemsize == 56
 except ImportError:  # pragma: no cover
     np = None
 
@@ -124,6 +132,7 @@ EXPORTED_SYMBOLS = (
     "hlc_validate_proposals_device", "hlc_eth_address_batch", "hlc_eth_sign_batch",
     "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_consensus_timeout_batch",
     "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
+    "hlc_process_votes",
 )
 
 _lib = None
@@ -180,6 +189,9 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_validate_wire_proposals_device.argtypes = [vp, vp, c_uint64, vp, vp, c_uint64, vp, c_uint64,
                                                        c_uint64, vp, vp, vp]
     lib.hlc_validate_wire_proposals_device.restype = c_int
+    lib.hlc_process_votes.argtypes = [vp, POINTER(hlc_votes), u32p, vp, c_uint64, u8p, u32p, c_uint64, c_uint64,
+                                      u8p, u8p, u8p, u8p]
+    lib.hlc_process_votes.restype = c_int
     lib.hlc_ctx_set_kernel_timing.argtypes = [vp, c_int]
     lib.hlc_ctx_set_kernel_timing.restype = c_int
     lib.hlc_ctx_take_kernel_time.argtypes = [vp, POINTER(ctypes.c_double), u64p, POINTER(ctypes.c_double), u64p]

@@ -114,6 +114,28 @@ class Engine:
                                                         _ffi.ptr(state, c_uint8), _ffi.ptr(status, c_uint8)))
         return state[:n], status[:n]
 
+    # ---- streaming votes -----------------------------------------------------------------
+    def process_votes(self, batch: VoteBatch, vote_session: np.ndarray, sessions: np.ndarray,
+                      owners: Optional[np.ndarray] = None, owner_session: Optional[np.ndarray] = None, now: int = 0):
+        """hlc_process_votes: process_incoming_vote (service.rs:286-305) for every vote, in order.
+        `sessions` (SESSION_DTYPE) is updated in place.  -> (status, transition, inserted, reason)."""
+        n = batch.n
+        vote_session = np.ascontiguousarray(vote_session, dtype=np.uint32)
+        assert sessions.dtype == _ffi.SESSION_DTYPE and sessions.flags.c_contiguous
+        owners = np.zeros((0, 20), np.uint8) if owners is None else np.ascontiguousarray(owners, np.uint8).reshape(-1, 20)
+        owner_session = (np.zeros(0, np.uint32) if owner_session is None
+                         else np.ascontiguousarray(owner_session, dtype=np.uint32))
+        out = [np.zeros(max(n, 1), np.uint8) for _ in range(4)]
+        view = batch.view()
+        obuf = owners if owners.size else np.zeros((1, 20), np.uint8)
+        osb = owner_session if owner_session.size else np.zeros(1, np.uint32)
+        _ffi.check(self.lib.hlc_process_votes(
+            self.ctx, ctypes.byref(view), _ffi.ptr(vote_session if n else np.zeros(1, np.uint32), c_uint32),
+            c_void_p(sessions.ctypes.data) if sessions.shape[0] else None, sessions.shape[0],
+            _ffi.ptr(obuf, c_uint8), _ffi.ptr(osb, c_uint32), owners.shape[0], now,
+            *[_ffi.ptr(o, c_uint8) for o in out]))
+        return tuple(o[:n] for o in out)
+
     # ---- wire format (gossip bytes of consensus.proto Proposal messages) -----------------
     @staticmethod
     def _wire_args(wire, msg_off, msg_len, scope):

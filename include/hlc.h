@@ -55,6 +55,8 @@ extern "C" {
 #define HLC_INSUFFICIENT_VOTES_AT_TIMEOUT 16   /* error.rs:64 (handle_consensus_timeout) */
 #define HLC_PROPOSAL_DECODE_ERROR 17           /* wire bytes are not a Proposal (prost DecodeError,
                                                   raised by the embedder before service.rs:263) */
+#define HLC_SESSION_NOT_ACTIVE 18              /* error.rs:54 (add_vote on a Failed session) */
+#define HLC_SESSION_NOT_FOUND 19               /* error.rs:56 (no session for the vote's proposal) */
 
 /* Sub-reason of HLC_SIGNATURE_SCHEME (the reference's Verify(String) message class). */
 #define HLC_SCHEME_NONE 0
@@ -174,6 +176,24 @@ typedef struct hlc_wire_proposal {
   uint8_t _pad[3];
 } hlc_wire_proposal; /* 48 bytes */
 
+/* One live session as `process_incoming_vote` (service.rs:286-305) reads and mutates it
+ * (session.rs:167-190): proposal scalars, resolved config, state, round and tally.  In/out. */
+typedef struct hlc_session {
+  uint64_t timestamp;             /* Proposal.timestamp (creation time, validate_vote) */
+  uint64_t expiration_timestamp;  /* Proposal.expiration_timestamp */
+  uint32_t proposal_id;           /* Proposal.proposal_id (votes must carry it) */
+  uint32_t expected_voters_count; /* Proposal.expected_voters_count */
+  uint32_t round;                 /* Proposal.round of the session (in/out) */
+  uint32_t total;                 /* votes in the owner->vote map (in/out) */
+  uint32_t yes;                   /* YES votes among them (in/out) */
+  uint32_t max_rounds;            /* ConsensusConfig.max_rounds */
+  double consensus_threshold;     /* ConsensusConfig.consensus_threshold */
+  uint8_t state;                  /* HLC_SESSION_* (in/out) */
+  uint8_t use_gossipsub_rounds;   /* ConsensusConfig.use_gossipsub_rounds */
+  uint8_t liveness_criteria_yes;  /* Proposal.liveness_criteria_yes */
+  uint8_t _pad[5];
+} hlc_session; /* 56 bytes */
+
 typedef struct hlc_ctx hlc_ctx;
 
 /* ---- Context -------------------------------------------------------------------- */
@@ -254,6 +274,31 @@ int hlc_eth_address_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, uint8
 int hlc_eth_sign_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, const uint8_t* bytes,
                        uint64_t bytes_len, const uint64_t* payload_off,
                        const uint32_t* payload_len, uint8_t* out_sig65);
+
+/* ---- Streaming votes ---------------------------------------------- */
+
+/* `ConsensusService::process_incoming_vote` (service.rs:286-305) for n votes delivered in
+ * array order, micro-batched across sessions.  vote_session[i] = index into sessions[] of the
+ * session the embedder's storage returns for (scope, vote.proposal_id), or 0xFFFFFFFF when
+ * there is none (HLC_SESSION_NOT_FOUND); a session whose proposal_id differs from the vote's is
+ * a caller mapping error, reported as HLC_VOTE_PROPOSAL_ID_MISMATCH.
+ * Each vote gets exactly the outcome of the reference's
+ * sequential calls: validate_vote against the session's proposal (utils.rs:127-171, the same
+ * kernels as validate-many), then ConsensusSession::add_vote (session.rs:225-249): a session
+ * already in ConsensusReached(r) returns it without inserting, Failed -> SessionNotActive,
+ * expiry -> ProposalExpired, check_round_limit(1) -> MaxRoundsExceeded (and Failed),
+ * owner already in the map (existing owners or an earlier vote of this batch) -> DuplicateVote,
+ * else insert, update_round(1), check_consensus.  sessions[] is updated in place.
+ * Existing owner maps: owners[k*20 .. +20] belongs to sessions[owner_session[k]] (20-byte
+ * addresses, the only identities EthereumConsensusSigner admits).
+ * Per vote: out_status = HLC_OK or the error; out_transition = HLC_STILL_ACTIVE /
+ * HLC_REACHED_NO / HLC_REACHED_YES when OK; out_inserted = 1 when the vote entered the map
+ * (the caller appends it to the session's proposal.votes); out_reason (optional) = HLC_SCHEME_*. */
+int hlc_process_votes(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote_session,
+                      hlc_session* sessions, uint64_t n_sessions, const uint8_t* owners,
+                      const uint32_t* owner_session, uint64_t n_owners, uint64_t now,
+                      uint8_t* out_status, uint8_t* out_transition, uint8_t* out_inserted,
+                      uint8_t* out_reason);
 
 /* ---- Wire decode -------------------------------------------------- */
 
