@@ -39,8 +39,9 @@ ProposalAlreadyExist = _variant("ProposalAlreadyExist", 15, "error.rs:57")
 InsufficientVotesAtTimeout = _variant("InsufficientVotesAtTimeout", 16, "error.rs:64")
 InvalidConsensusThreshold = _variant("InvalidConsensusThreshold", 100, "error.rs:13-14")
 InvalidTimeout = _variant("InvalidTimeout", 101, "error.rs:15-16")
-SessionNotActive = _variant("SessionNotActive", 102, "error.rs:53")
-SessionNotFound = _variant("SessionNotFound", 103, "error.rs:55")
+SessionNotActive = _variant("SessionNotActive", 18, "error.rs:53-54 (HLC_SESSION_NOT_ACTIVE)")
+SessionNotFound = _variant("SessionNotFound", 19, "error.rs:55-56 (HLC_SESSION_NOT_FOUND)")
+ProposalDecodeError = _variant("ProposalDecodeError", 17, "prost DecodeError on the wire bytes (HLC_PROPOSAL_DECODE_ERROR)")
 
 
 class SignatureScheme(ConsensusError):
@@ -65,7 +66,8 @@ SCHEME_REASONS = {
 _BY_CODE = {cls.code: cls for cls in (
     ProposalExpired, VoteProposalIdMismatch, EmptyVoteOwner, EmptyVoteHash, EmptySignature, InvalidVoteHash,
     InvalidVoteSignature, TimestampOlderThanCreationTime, VoteExpired, ReceivedHashMismatch, ParentHashMismatch,
-    DuplicateVote, MaxRoundsExceeded, ProposalAlreadyExist, InsufficientVotesAtTimeout)}
+    DuplicateVote, MaxRoundsExceeded, ProposalAlreadyExist, InsufficientVotesAtTimeout, ProposalDecodeError,
+    SessionNotActive, SessionNotFound)}
 
 
 def from_status(status: int, reason: int = 0) -> ConsensusError:

@@ -6,6 +6,8 @@
 * `build_vote`              utils.rs:55-104
 * `ConsensusService.process_incoming_proposal(s)`  service.rs:263-279 -> session.rs:198-300
 * `ConsensusService.handle_consensus_timeout(s)`   service.rs:323-373 (batched tally)
+* `ConsensusService.process_incoming_vote(s)`       service.rs:286-305 (micro-batched)
+* `ConsensusService.process_incoming_proposal_bytes` wire bytes -> device decode -> service.rs:263-279
 
 Only the slice of `ConsensusService` that sits on the validation path is mirrored: the
 duplicate-session check (`ProposalAlreadyExist`), config resolution (service.rs:444-484) and
@@ -187,7 +189,9 @@ class SessionRecord:
     yes: int
     total: int
     created_at: int
-    failed: bool = False       # ConsensusState::Failed after a timeout without a result
+    failed: bool = False       # ConsensusState::Failed (timeout without a result, round limit)
+    round: int = 1             # Proposal.round of the session (session.rs:350-366)
+    owners: set = field(default_factory=set)  # keys of the owner -> vote map
 
     @property
     def state(self) -> int:
@@ -302,8 +306,119 @@ class ConsensusService:
                 out.append(r.consensus)
         return out
 
+    def process_incoming_vote(self, scope: Union[str, bytes], vote: Vote, now: int) -> None:
+        """service.rs:286-305: raises the reference's error, else the vote is applied."""
+        err = self.process_incoming_votes(scope, [vote], now)[0]
+        if err is not None:
+            raise err
+
+    def process_incoming_votes(self, scope: Union[str, bytes], votes: Sequence[Vote],
+                               now: int) -> List[Optional[errors.ConsensusError]]:
+        """Micro-batched `process_incoming_vote`: one GPU call (hlc_process_votes) gives every vote
+        exactly the outcome of the reference's calls in delivery order; None = Ok.  Accepted votes
+        are appended to their session's proposal, states / rounds / tallies updated."""
+        from . import _ffi
+        key = _scope_key(scope)
+        recs: List[SessionRecord] = []
+        index: Dict[int, int] = {}
+        vsess = np.full(len(votes), 0xFFFFFFFF, np.uint32)
+        for i, v in enumerate(votes):
+            r = self.sessions.get((key, v.proposal_id))
+            if r is None:
+                continue
+            if v.proposal_id not in index:
+                index[v.proposal_id] = len(recs)
+                recs.append(r)
+            vsess[i] = index[v.proposal_id]
+        sarr = np.zeros(len(recs), _ffi.SESSION_DTYPE)
+        orows, osess = [], []
+        for k, r in enumerate(recs):
+            p, c = r.proposal, r.config
+            sarr[k] = (p.timestamp, p.expiration_timestamp, p.proposal_id, p.expected_voters_count, r.round, r.total,
+                       r.yes, c.max_rounds, c.consensus_threshold, r.state, int(c.use_gossipsub_rounds),
+                       int(p.liveness_criteria_yes), (0,) * 5)
+            for o in r.owners:
+                if len(o) == 20:
+                    orows.append(np.frombuffer(o, np.uint8))
+                    osess.append(k)
+        owners = np.stack(orows) if orows else np.zeros((0, 20), np.uint8)
+        st, tr, ins, rs = self.engine.process_votes(pack_votes(votes), vsess, sarr, owners,
+                                                    np.array(osess, np.uint32), now)
+        for k, r in enumerate(recs):
+            s = sarr[k]
+            r.round, r.total, r.yes = int(s["round"]), int(s["total"]), int(s["yes"])
+            state = int(s["state"])
+            r.failed = state == 3
+            r.consensus = None if state in (0, 3) else state == 2
+            if r.consensus is not None:
+                r.transition = TRANSITION_CONSENSUS_REACHED
+        out: List[Optional[errors.ConsensusError]] = []
+        for i, v in enumerate(votes):
+            if ins[i]:
+                r = recs[int(vsess[i])]
+                r.owners.add(v.vote_owner)
+                r.proposal.votes.append(v)
+            code = int(st[i])
+            out.append(None if code == 0 else errors.from_status(code, int(rs[i])))
+        return out
+
+    def process_incoming_proposal_bytes(self, scope: Union[str, bytes], messages: Sequence[bytes],
+                                        now: int) -> List[ProposalOutcome]:
+        """Gossip bytes of Proposal messages -> outcomes, as if each were prost-decoded and passed
+        to `process_incoming_proposal` in order.  Decoding runs on the device
+        (hlc_decode_proposals); the decoded SoA batch goes straight to validate-many.  A message
+        that does not decode gets ProposalDecodeError (the embedder's prost decode fails before
+        service.rs:263); a stored id gets ProposalAlreadyExist (service.rs:269-271)."""
+        from . import _ffi
+        key = _scope_key(scope)
+        base = self.scope_configs.get(key, self.default_config)
+        lens = np.array([len(m) for m in messages], np.uint32)
+        off = np.zeros(len(messages), np.uint64)
+        if len(messages):
+            off[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+        wire = np.frombuffer(b"".join(messages), np.uint8)
+        scope_cfg = np.zeros(1, _ffi.SCOPE_CONFIG_DTYPE)
+        scope_cfg[0] = (base.consensus_threshold, base.max_rounds, int(base.use_gossipsub_rounds), (0, 0, 0))
+        props, winfo, batch = self.engine.decode_proposals(wire, off, lens, scope_cfg)
+        res, _, _, _ = self.engine.validate_proposals(batch, props, now, want_votes=False)
+        out: List[ProposalOutcome] = []
+        for m, msg in enumerate(messages):
+            if int(winfo[m]["decode_status"]) != 0:
+                out.append(ProposalOutcome(0, errors.ProposalDecodeError()))
+                continue
+            p = _proposal_from_decoded(msg, props[m], winfo[m], batch, int(off[m]))
+            if (key, p.proposal_id) in self.sessions:
+                out.append(ProposalOutcome(p.proposal_id, errors.ProposalAlreadyExist()))
+                continue
+            o = _outcomes([p], res[m:m + 1])[0]
+            out.append(o)
+            if o.ok:
+                self._store(key, p, resolve_config(base, p), o, now)
+        return out
+
     def _store(self, key: bytes, p: Proposal, cfg: ConsensusConfig, o: ProposalOutcome, now: int) -> None:
-        self.sessions[(key, p.proposal_id)] = SessionRecord(p, cfg, o.transition, o.consensus, o.yes, o.total, now)
+        n = len(p.votes)
+        rnd = (2 if n else 1) if cfg.use_gossipsub_rounds else min(1 + n, 0xFFFFFFFF)  # from_proposal: round 1 + update_round(n)
+        self.sessions[(key, p.proposal_id)] = SessionRecord(p, cfg, o.transition, o.consensus, o.yes, o.total, now,
+                                                            round=rnd, owners={v.vote_owner for v in p.votes})
+
+
+def _proposal_from_decoded(msg: bytes, d, w, batch, base: int) -> Proposal:
+    """Proposal object from the device decoder's outputs (hlc_proposal + hlc_wire_proposal +
+    decoded vote SoA whose offsets index the wire buffer) -- marshalling only, no parsing."""
+    def sl(o, n):
+        return msg[int(o):int(o) + int(n)]
+    votes = []
+    for i in range(int(d["vote_begin"]), int(d["vote_begin"]) + int(d["vote_count"])):
+        f = [batch.field(i, k) for k in range(5)]
+        votes.append(Vote(vote_id=int(batch.vote_id[i]), vote_owner=f[0], proposal_id=int(batch.proposal_id[i]),
+                          timestamp=int(batch.timestamp[i]), vote=bool(batch.vote[i]), parent_hash=f[1],
+                          received_hash=f[2], vote_hash=f[3], signature=f[4]))
+    return Proposal(name=sl(w["name_off"], w["name_len"]).decode("utf-8"), payload=sl(w["payload_off"], w["payload_len"]),
+                    proposal_id=int(d["proposal_id"]), proposal_owner=sl(w["owner_off"], w["owner_len"]), votes=votes,
+                    expected_voters_count=int(d["expected_voters_count"]), round=int(w["round"]),
+                    timestamp=int(d["timestamp"]), expiration_timestamp=int(d["expiration_timestamp"]),
+                    liveness_criteria_yes=bool(d["liveness_criteria_yes"]))
 
 
 def _scope_key(scope: Union[str, bytes]) -> bytes:

@@ -29,6 +29,24 @@ class OracleEngine:
     def compute_vote_hashes(self, batch):
         return coracle.compute_vote_hashes(batch)
 
+    def process_votes(self, batch, vote_session, sessions, owners=None, owner_session=None, now=0):
+        """hlc_process_votes semantics through oracle/stream_oracle.py (sessions updated in place)."""
+        import stream_oracle as so
+        from adversarial import batch_to_votes
+        ss = [so.Session(int(x["proposal_id"]), int(x["timestamp"]), int(x["expiration_timestamp"]),
+                         int(x["expected_voters_count"]), int(x["round"]), int(x["total"]), int(x["yes"]),
+                         int(x["max_rounds"]), float(x["consensus_threshold"]), int(x["state"]),
+                         bool(x["use_gossipsub_rounds"]), bool(x["liveness_criteria_yes"])) for x in sessions]
+        for o, k in zip(owners if owners is not None else [], owner_session if owner_session is not None else []):
+            ss[int(k)].owners.add(bytes(o))
+        out = so.process_incoming_votes(ss, batch_to_votes(batch), [int(v) if v != 0xFFFFFFFF else -1
+                                                                    for v in vote_session], now)
+        for k, x in enumerate(ss):
+            sessions[k]["round"], sessions[k]["total"], sessions[k]["yes"], sessions[k]["state"] = (
+                x.round, x.total, x.yes, x.state)
+        cols = list(zip(*out)) if out else [(), (), (), ()]
+        return tuple(np.array(c, np.uint8) for c in cols)
+
 
 class OracleSigner:
     """EthereumConsensusSigner's identity/sign over the oracle (test infrastructure)."""
@@ -210,3 +228,59 @@ def test_gpu_reference_batch_scenarios(engine):
     old = make_proposal(3, owner, 1, 3, engine, expiration=T0 + 1)
     with pytest.raises(errors.ProposalExpired):
         svc.process_incoming_proposal("batch_gossipsub", old, T0 + 20)
+
+
+# ------------------------------------------------ streaming votes (service.rs:286-305) ------------
+def _gossip_pair(eng_factory):
+    """network_gossip_tests.rs:20-77: peer B stores peer A's vote-less proposal, then receives both
+    YES votes of an n = 2 proposal one at a time."""
+    eng = eng_factory()
+    svc = ConsensusService(engine=eng)
+    a, b = OracleSigner(71), OracleSigner(72)
+    p = Proposal(name="n2", payload=b"x", proposal_id=4242, proposal_owner=a.identity(), expected_voters_count=2,
+                 timestamp=T0, expiration_timestamp=T0 + 3600, liveness_criteria_yes=True)
+    svc.process_incoming_proposal("scope", p, T0 + 5)
+    va = build_vote(p, True, a, T0 + 6, eng)
+    pa = Proposal(**{**p.__dict__, "votes": [va]})
+    vb = build_vote(pa, True, b, T0 + 7, eng)
+    return svc, va, vb
+
+
+def _check_gossip(svc, va, vb):
+    svc.process_incoming_vote("scope", va, T0 + 8)
+    rec = svc.get_session("scope", 4242)
+    assert rec.consensus is None and rec.total == 1 and rec.round == 2
+    with pytest.raises(errors.DuplicateVote):
+        svc.process_incoming_vote("scope", va, T0 + 8)
+    svc.process_incoming_vote("scope", vb, T0 + 8)
+    assert rec.consensus is True and rec.total == 2 and len(rec.proposal.votes) == 2
+    with pytest.raises(errors.SessionNotFound):
+        svc.process_incoming_vote("other-scope", va, T0 + 8)
+    # a decided session returns its result for further votes without inserting them
+    assert svc.process_incoming_votes("scope", [va], T0 + 8) == [None] and rec.total == 2
+
+
+def test_service_incoming_votes_oracle_double():
+    _check_gossip(*_gossip_pair(OracleEngine))
+
+
+@pytest.mark.gpu
+def test_gpu_service_incoming_votes(engine):
+    _check_gossip(*_gossip_pair(lambda: engine))
+
+
+@pytest.mark.gpu
+def test_gpu_service_incoming_proposal_bytes(engine):
+    """Gossip bytes -> device decode -> validate -> stored session; undecodable bytes and a second
+    delivery of the same id get the errors the embedder + reference would produce."""
+    from hashgraph_like_consensus.protos import encode_proposal
+    svc = ConsensusService(engine=engine)
+    owner = OracleSigner(80)
+    p = make_proposal(5151, owner, 3, 3, engine)
+    msg = encode_proposal(p)
+    outs = svc.process_incoming_proposal_bytes("scope", [msg, msg[:-2], msg], T0 + 20)
+    assert outs[0].ok and outs[0].total == 3
+    assert isinstance(outs[1].error, errors.ProposalDecodeError)
+    assert isinstance(outs[2].error, errors.ProposalAlreadyExist)
+    rec = svc.get_session("scope", 5151)
+    assert rec.proposal == p and rec.owners == {v.vote_owner for v in p.votes}
