@@ -99,7 +99,7 @@ struct hlc_ctx {
       verify, status, reason, chain_code, chain_tab, dup_tab, red, scan_tmp, totals, flag;
   // wire decode: staged inputs, walk / record workspace, decoded votes (hlc_votes SoA over the wire bytes)
   DBuf w_wire, w_moff, w_mlen, w_scope, w_vcount, w_vbegin, w_vrec_off, w_vrec_len, w_vrec_msg, w_first_bad,
-      w_vote_err, w_props, w_wout, w_res;
+      w_vote_err, w_props, w_wout, w_res, w_slab_off, w_slab_len, w_big;
   DBuf w_vid, w_pid, w_ts, w_vote, w_foff, w_flen;
   // streaming votes
   DBuf s_vsess, s_sessions, s_owners, s_osess, s_props, s_keys, s_iota, s_order, s_segb, s_sege, s_tab, s_sort_tmp,
@@ -281,13 +281,31 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
                   hlc_wire_proposal* dwout, hlc_votes* dv, uint64_t* n_votes, hipStream_t s) {
   CHK(c->w_vcount.ensure(nm * 8 + 8));
   CHK(c->w_vbegin.ensure(nm * 8 + 8));
+  const uint64_t slab = hlc::wire_slab();
+  CHK(c->w_slab_off.ensure(nm * slab * 8 + 8));
+  CHK(c->w_slab_len.ensure(nm * slab * 4 + 4));
+  CHK(c->w_big.ensure(16));
   uint64_t* vcount = c->w_vcount.as<uint64_t>();
   uint64_t* vbegin = c->w_vbegin.as<uint64_t>();
   uint64_t nv = 0;
+  uint32_t big = 0;
   if (nm) {
-    hlc::launch_wire_walk(0, wire, moff, mlen, nm, vcount, nullptr, nullptr, nullptr, scope, n_scope, nullptr,
+    HIPCHK(hipMemsetAsync(c->w_big.p, 0, 4, s));
+    hlc::launch_wire_touch(wire, wire_len, c->w_big.as<uint32_t>() + 1, s);
+    hlc::launch_wire_walk(0, wire, moff, mlen, nm, vcount, nullptr, dwout, dprops, scope, n_scope,
+                          c->w_slab_off.as<uint64_t>(), c->w_slab_len.as<uint32_t>(), c->w_big.as<uint32_t>(), nullptr,
                           nullptr, nullptr, s);
-    CHK(scan_sizes(c, nm, vcount, vbegin, &nv, s));
+    size_t tb = 0;
+    hlc::launch_exclusive_scan(vcount, vbegin, nm, nullptr, tb, s);
+    CHK(c->scan_tmp.ensure(tb + 16));
+    hlc::launch_exclusive_scan(vcount, vbegin, nm, c->scan_tmp.p, tb, s);
+    uint64_t h[3] = {0, 0, 0};  // last begin, last count, big flag: one synchronisation
+    HIPCHK(hipMemcpyAsync(h, vbegin + (nm - 1), 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h + 1, vcount + (nm - 1), 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h + 2, c->w_big.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    nv = h[0] + h[1];
+    big = (uint32_t)h[2];
   }
   if (nv > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
   CHK(c->w_vrec_off.ensure(nv * 8 + 8));
@@ -311,8 +329,12 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
   dv->field_off = c->w_foff.as<uint64_t>();
   dv->field_len = c->w_flen.as<uint32_t>();
   if (nm) {
-    hlc::launch_wire_walk(1, wire, moff, mlen, nm, vcount, vbegin, dwout, dprops, scope, n_scope,
-                          c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(), c->w_vrec_msg.as<uint32_t>(), s);
+    hlc::launch_wire_place(nm, vcount, vbegin, c->w_slab_off.as<uint64_t>(), c->w_slab_len.as<uint32_t>(), dprops,
+                           c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(), c->w_vrec_msg.as<uint32_t>(), s);
+    if (big)  // messages with more vote records than the walker's slab: walk them again, writing in place
+      hlc::launch_wire_walk(1, wire, moff, mlen, nm, vcount, vbegin, dwout, dprops, scope, n_scope, nullptr, nullptr,
+                            nullptr, c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(),
+                            c->w_vrec_msg.as<uint32_t>(), s);
     HIPCHK(hipMemsetAsync(c->w_first_bad.p, 0xFF, nm * 4, s));
     hlc::launch_wire_votes(wire, moff, mlen, nv, c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(),
                            c->w_vrec_msg.as<uint32_t>(), vbegin, dv, c->w_vote_err.as<uint8_t>(),

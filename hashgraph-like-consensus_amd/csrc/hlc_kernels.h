@@ -83,11 +83,17 @@ void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const
                      hlc_result* out, hipStream_t s);
 
 // ---- wire decode (hlc_wire.hip) ----
-// pass 0: vote_count[m]; pass 1: vote records at vote_begin[m] + k, wout[m], pout[m]
-void launch_wire_walk(int pass, const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
-                      uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout,
-                      hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope, uint64_t* vrec_off,
-                      uint32_t* vrec_len, uint32_t* vrec_msg, hipStream_t s);
+// mode 0: vote_count[m], wout[m], pout[m], first wire_slab() records per message in slab_*, *big |= 1 when
+// a message has more; mode 1 (after the scan, only when *big): every record of those messages in place
+void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
+                      uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout, hlc_proposal* pout,
+                      const hlc_scope_config* scope, uint64_t n_scope, uint64_t* slab_off, uint32_t* slab_len,
+                      uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, hipStream_t s);
+void launch_wire_place(uint64_t nm, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* slab_off,
+                       const uint32_t* slab_len, hlc_proposal* pout, uint64_t* vrec_off, uint32_t* vrec_len,
+                       uint32_t* vrec_msg, hipStream_t s);
+uint64_t wire_slab();
+void launch_wire_touch(const uint8_t* wire, uint64_t len, uint32_t* sink, hipStream_t s);
 // decodes vote records into `out` (device SoA); first_bad[m] (pre-set to ~0) = first failing record
 void launch_wire_votes(const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nv,
                        const uint64_t* vrec_off, const uint32_t* vrec_len, const uint32_t* vrec_msg,

@@ -161,3 +161,22 @@ def test_gpu_validate_wire_byzantine(engine):
 def test_gpu_validate_wire_p2p(engine):
     w = oracle_workload(6, 40, 60, False, 0x484C4313, name="wire-p2p")
     _wire_vs_oracle(engine, w.batch, w.desc, w.now)
+
+
+def test_gpu_decode_large_messages(engine):
+    """Messages with more vote records than the walker keeps per message (128) and spanning many
+    4 KiB walker windows, mixed with small ones and a corrupted large one."""
+    from wire_fuzz import random_vote
+    from hashgraph_like_consensus.protos import Proposal
+    rnd = random.Random(24)
+    msgs = []
+    for k in range(6):
+        p = random_proposal(rnd, max_votes=3)
+        if k % 2 == 0:
+            p = Proposal(name="big", proposal_id=1000 + k, votes=[random_vote(rnd) for _ in range(130 + 70 * k)],
+                         expected_voters_count=500, timestamp=5, expiration_timestamp=9)
+        msgs.append(encode_proposal(p))
+    big = bytearray(msgs[2])
+    big[len(big) // 2] ^= 0x80  # corrupt somewhere in the middle of the vote records
+    msgs.append(bytes(big))
+    _check_decode(engine, msgs, _scope(1))
