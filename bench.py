@@ -152,6 +152,74 @@ def wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synt
     }
 
 
+def stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch):
+    """Secondary line: the same 640k signed votes delivered one by one to 10k
+    live sessions (fresh: no votes yet), in a shuffled gossip order, as micro-batched
+    `process_incoming_vote` calls (hlc_process_votes_device, inputs in HBM).  Each step restores
+    the initial sessions (a 560 KB device copy, inside the timed region) and processes every vote:
+    validate_vote on the GPU, then add_vote per session in delivery order.  Consistency guard:
+    every vote validates, and the votes marked inserted add up to the sessions' final totals."""
+    from hashgraph_like_consensus import _ffi
+    from hashgraph_like_consensus.batch import VoteBatch
+
+    b, d = w.batch, w.desc
+    P = d.shape[0]
+    perm = np.random.default_rng(0x484C4302).permutation(b.n)
+    pb = VoteBatch(vote_id=b.vote_id[perm], proposal_id=b.proposal_id[perm], timestamp=b.timestamp[perm],
+                   vote=b.vote[perm], arena=b.arena, field_off=b.field_off[perm], field_len=b.field_len[perm])
+    vsess = np.repeat(np.arange(P, dtype=np.uint32), d["vote_count"].astype(np.int64))[perm]
+    sess = np.zeros(P, _ffi.SESSION_DTYPE)
+    for f in ("timestamp", "expiration_timestamp", "proposal_id", "expected_voters_count", "max_rounds",
+              "consensus_threshold", "use_gossipsub_rounds", "liveness_criteria_yes"):
+        sess[f] = d[f]
+    sess["round"] = 1
+    dpb = DeviceBatch(pb, d, w.now, device=dev)
+    t_vs = torch.from_numpy(vsess.view(np.uint8).copy()).to(dev)
+    t_init = torch.from_numpy(sess.view(np.uint8).reshape(-1).copy()).to(dev)
+    t_sess = t_init.clone()
+    n = pb.n
+    outs = [torch.zeros(n + 1, dtype=torch.uint8, device=dev) for _ in range(3)]
+
+    def step():
+        with torch.cuda.stream(stream):
+            t_sess.copy_(t_init)
+        eng.process_votes_device(dpb, t_vs.data_ptr(), t_sess.data_ptr(), P, w.now, outs[0].data_ptr(),
+                                 outs[1].data_ptr(), outs[2].data_ptr(), handle)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    st = outs[0][:n].cpu().numpy()
+    ins = outs[2][:n].cpu().numpy()
+    fin = t_sess.cpu().numpy().view(_ffi.SESSION_DTYPE)
+    assert (st == 0).all(), f"{int((st != 0).sum())} streamed votes rejected"
+    assert int(ins.sum()) == int(fin["total"].sum()) and (fin["state"] != 3).all()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return {
+        "metric": "incoming votes/s, micro-batched process_incoming_vote (validate_vote + add_vote per session)",
+        "value": n * world * args.steps / el,
+        "unit": "votes/s",
+        "ms_per_step": el / args.steps * 1e3,
+        "votes_per_step_per_gpu": n,
+        "sessions": P,
+        "inserted_per_step": int(ins.sum()),
+        "decided_sessions": int((fin["state"] != 0).sum()),
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,6 +230,7 @@ def main() -> int:
     ap.add_argument("--cpu-sample-proposals", type=int, default=10_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-bytes leg (device protobuf decode)")
+    ap.add_argument("--no-stream", action="store_true", help="skip the streaming process_incoming_vote leg")
     args = ap.parse_args()
 
     import numpy as np
@@ -280,6 +349,8 @@ def main() -> int:
     if not args.no_wire:
         out["wire"] = wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire,
                                elapsed / args.steps)
+    if not args.no_stream:
+        out["stream"] = stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, min(args.cpu_sample_proposals, P))
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

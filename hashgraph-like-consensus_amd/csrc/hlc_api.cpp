@@ -653,6 +653,78 @@ int hlc_validate_wire_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire
   return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+// process_incoming_vote over device-resident inputs (see hlc_process_votes); outputs on device.
+int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vsess, hlc_session* dss,
+                         uint64_t n_sessions, const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
+                         uint64_t now, uint8_t* st, uint8_t* tr, uint8_t* ins, uint8_t* reason, hipStream_t s) {
+  const uint64_t n = dv->n;
+  CHK(ctx->s_props.ensure(n_sessions * sizeof(hlc_proposal) + 16));
+  hlc_proposal* dprops = ctx->s_props.as<hlc_proposal>();
+  hlc::launch_sessions_to_props(dss, n_sessions, dprops, s);
+  // 1. validate_vote for every vote against its session's proposal (same kernels as validate-many)
+  CHK(ctx->status.ensure(n + 1));
+  uint8_t* rs = reason;
+  if (!rs) {
+    CHK(ctx->reason.ensure(n + 1));
+    rs = ctx->reason.as<uint8_t>();
+  }
+  CHK(ctx->flag.ensure(16));
+  HIPCHK(hipMemsetAsync(ctx->flag.p, 0, sizeof(uint32_t), s));
+  uint32_t flags = 0;
+  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, now, ctx->status.as<uint8_t>(), rs, nullptr, &flags, s));
+  // 2. each session's votes in delivery order
+  CHK(ctx->s_keys.ensure(n * 4 + 4));
+  CHK(ctx->s_iota.ensure(n * 4 + 4));
+  CHK(ctx->s_order.ensure(n * 4 + 4));
+  size_t tb = 0;
+  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
+                              ctx->s_order.as<uint32_t>(), nullptr, tb, s);
+  CHK(ctx->s_sort_tmp.ensure(tb + 16));
+  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
+                              ctx->s_order.as<uint32_t>(), ctx->s_sort_tmp.p, tb, s);
+  CHK(ctx->s_segb.ensure(n_sessions * 4 + 4));
+  CHK(ctx->s_sege.ensure(n_sessions * 4 + 4));
+  HIPCHK(hipMemsetAsync(ctx->s_segb.p, 0, n_sessions * 4 + 4, s));
+  HIPCHK(hipMemsetAsync(ctx->s_sege.p, 0, n_sessions * 4 + 4, s));
+  hlc::launch_segments(ctx->s_keys.as<uint32_t>(), n, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(), s);
+  // 3. (session, owner) table: existing owner maps, then add_vote in order per session
+  uint64_t cap = 64;
+  while (cap < 2 * (n + n_owners)) cap <<= 1;
+  CHK(ctx->s_tab.ensure(cap * 4));
+  HIPCHK(hipMemsetAsync(ctx->s_tab.p, 0xFF, cap * 4, s));
+  hlc::launch_owner_insert(ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1), owners, owner_session, n_owners, dv, vsess,
+                           s);
+  hlc::launch_stream_init(n, vsess, ctx->status.as<uint8_t>(), st, tr, ins, s);
+  hlc::launch_apply_votes(dss, n_sessions, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(),
+                          ctx->s_order.as<uint32_t>(), dv, now, ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1), owners,
+                          owner_session, n_owners, vsess, st, tr, ins, s);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hlc_process_votes_device(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote_session,
+                             hlc_session* sessions, uint64_t n_sessions, const uint8_t* owners,
+                             const uint32_t* owner_session, uint64_t n_owners, uint64_t now, uint8_t* out_status,
+                             uint8_t* out_transition, uint8_t* out_inserted, uint8_t* out_reason, void* stream) {
+  if (!ctx || !votes) return set_err(HLC_EINVAL, "NULL argument");
+  if (votes->n && (!vote_session || !out_status || !out_transition || !out_inserted))
+    return set_err(HLC_EINVAL, "NULL vote_session / output array");
+  if (n_sessions >= hlc::NO_PROP || votes->n + n_owners > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "batch too large");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  return process_votes_device(ctx, votes, vote_session, sessions, n_sessions, owners, owner_session, n_owners, now,
+                              out_status, out_transition, out_inserted, out_reason, s);
+}
+
 int hlc_process_votes(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote_session, hlc_session* sessions,
                       uint64_t n_sessions, const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
                       uint64_t now, uint8_t* out_status, uint8_t* out_transition, uint8_t* out_inserted,
@@ -679,51 +751,14 @@ int hlc_process_votes(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote
   CHK(upload(ctx->s_sessions, sessions, n_sessions, s));
   CHK(upload(ctx->s_owners, owners, n_owners * 20, s));
   CHK(upload(ctx->s_osess, owner_session, n_owners, s));
-  CHK(ctx->s_props.ensure(n_sessions * sizeof(hlc_proposal) + 16));
-  const uint32_t* vsess = ctx->s_vsess.as<uint32_t>();
-  hlc_session* dss = ctx->s_sessions.as<hlc_session>();
-  hlc_proposal* dprops = ctx->s_props.as<hlc_proposal>();
-  hlc::launch_sessions_to_props(dss, n_sessions, dprops, s);
-  // 1. validate_vote for every vote against its session's proposal (same kernels as validate-many)
-  CHK(ctx->status.ensure(n + 1));
-  CHK(ctx->reason.ensure(n + 1));
-  CHK(ctx->flag.ensure(16));
-  HIPCHK(hipMemsetAsync(ctx->flag.p, 0, sizeof(uint32_t), s));
-  uint32_t flags = 0;
-  if (n) CHK(vote_stage(ctx, &dv, vsess, dprops, now, ctx->status.as<uint8_t>(), ctx->reason.as<uint8_t>(), nullptr,
-                        &flags, s));
-  // 2. each session's votes in delivery order
-  CHK(ctx->s_keys.ensure(n * 4 + 4));
-  CHK(ctx->s_iota.ensure(n * 4 + 4));
-  CHK(ctx->s_order.ensure(n * 4 + 4));
-  size_t tb = 0;
-  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
-                              ctx->s_order.as<uint32_t>(), nullptr, tb, s);
-  CHK(ctx->s_sort_tmp.ensure(tb + 16));
-  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
-                              ctx->s_order.as<uint32_t>(), ctx->s_sort_tmp.p, tb, s);
-  CHK(ctx->s_segb.ensure(n_sessions * 4 + 4));
-  CHK(ctx->s_sege.ensure(n_sessions * 4 + 4));
-  HIPCHK(hipMemsetAsync(ctx->s_segb.p, 0, n_sessions * 4 + 4, s));
-  HIPCHK(hipMemsetAsync(ctx->s_sege.p, 0, n_sessions * 4 + 4, s));
-  hlc::launch_segments(ctx->s_keys.as<uint32_t>(), n, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(), s);
-  // 3. (session, owner) table: existing owner maps, then add_vote in order per session
-  uint64_t cap = 64;
-  while (cap < 2 * (n + n_owners)) cap <<= 1;
-  CHK(ctx->s_tab.ensure(cap * 4));
-  HIPCHK(hipMemsetAsync(ctx->s_tab.p, 0xFF, cap * 4, s));
-  hlc::launch_owner_insert(ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1), ctx->s_owners.as<uint8_t>(),
-                           ctx->s_osess.as<uint32_t>(), n_owners, &dv, vsess, s);
   CHK(ctx->s_st.ensure(n + 1));
   CHK(ctx->s_tr.ensure(n + 1));
   CHK(ctx->s_ins.ensure(n + 1));
-  hlc::launch_stream_init(n, vsess, ctx->status.as<uint8_t>(), ctx->s_st.as<uint8_t>(), ctx->s_tr.as<uint8_t>(),
-                          ctx->s_ins.as<uint8_t>(), s);
-  hlc::launch_apply_votes(dss, n_sessions, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(),
-                          ctx->s_order.as<uint32_t>(), &dv, now, ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1),
-                          ctx->s_owners.as<uint8_t>(), ctx->s_osess.as<uint32_t>(), n_owners, vsess,
-                          ctx->s_st.as<uint8_t>(), ctx->s_tr.as<uint8_t>(), ctx->s_ins.as<uint8_t>(), s);
-  HIPCHK(hipGetLastError());
+  CHK(ctx->reason.ensure(n + 1));
+  hlc_session* dss = ctx->s_sessions.as<hlc_session>();
+  CHK(process_votes_device(ctx, &dv, ctx->s_vsess.as<uint32_t>(), dss, n_sessions, ctx->s_owners.as<uint8_t>(),
+                           ctx->s_osess.as<uint32_t>(), n_owners, now, ctx->s_st.as<uint8_t>(), ctx->s_tr.as<uint8_t>(),
+                           ctx->s_ins.as<uint8_t>(), ctx->reason.as<uint8_t>(), s));
   if (n) {
     HIPCHK(hipMemcpyAsync(out_status, ctx->s_st.p, n, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(out_transition, ctx->s_tr.p, n, hipMemcpyDeviceToHost, s));

@@ -136,6 +136,15 @@ class Engine:
             *[_ffi.ptr(o, c_uint8) for o in out]))
         return tuple(o[:n] for o in out)
 
+    def process_votes_device(self, dbatch, vote_session_ptr: int, sessions_ptr: int, n_sessions: int, now: int,
+                             st_ptr: int, tr_ptr: int, ins_ptr: int, stream_handle: int = 0) -> None:
+        """hlc_process_votes_device: votes of a device.DeviceBatch, session arrays and outputs in HBM
+        (raw device pointers as ints); no existing owner maps."""
+        _ffi.check(self.lib.hlc_process_votes_device(
+            self.ctx, ctypes.byref(dbatch.view), c_void_p(vote_session_ptr), c_void_p(sessions_ptr), n_sessions,
+            None, None, 0, now, c_void_p(st_ptr), c_void_p(tr_ptr), c_void_p(ins_ptr), None,
+            c_void_p(stream_handle) if stream_handle else None))
+
     # ---- wire format (gossip bytes of consensus.proto Proposal messages) -----------------
     @staticmethod
     def _wire_args(wire, msg_off, msg_len, scope):

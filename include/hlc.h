@@ -300,6 +300,16 @@ int hlc_process_votes(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote
                       uint8_t* out_status, uint8_t* out_transition, uint8_t* out_inserted,
                       uint8_t* out_reason);
 
+/* Same with every pointer (inside `votes`, vote_session, sessions, owners, owner_session and the
+ * outputs) in DEVICE memory, enqueued on `stream` (NULL: the context's stream); sessions are
+ * updated in place on the device.  vote_session entries must be < n_sessions or 0xFFFFFFFF
+ * (not re-checked on the host). */
+int hlc_process_votes_device(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote_session,
+                             hlc_session* sessions, uint64_t n_sessions, const uint8_t* owners,
+                             const uint32_t* owner_session, uint64_t n_owners, uint64_t now,
+                             uint8_t* out_status, uint8_t* out_transition, uint8_t* out_inserted,
+                             uint8_t* out_reason, void* stream);
+
 /* ---- Wire decode -------------------------------------------------- */
 
 /* prost `Proposal::decode` (consensus.proto:5-29) on the device for n_msgs messages, message i =
