@@ -9,6 +9,11 @@ gloo in the CPU tests.
 
 `shard_bounds` splits by cumulative vote count (the work unit), not by proposal count, so ranks
 stay balanced when proposal sizes differ.
+
+The two other entry paths shard the same way: `validate_wire_sharded` gives each
+rank a byte-balanced range of gossip messages (decode + validation on its GPU), and
+`process_votes_sharded` places session s on rank s % world, so every incoming vote is processed
+by the rank holding its session's state -- again with only the results gathered.
 """
 from __future__ import annotations
 
@@ -102,3 +107,100 @@ def validate_sharded(engine, batch: VoteBatch, desc: np.ndarray, now: int, group
                               for d in desc]) if desc.shape[0] else np.zeros(0, np.int64)
     status[all_idx] = vrows[:, 0]
     return full, status
+
+
+# ---- wire path: messages are independent proposals -------------------------------------------
+def wire_shard_bounds(msg_len: np.ndarray, world: int) -> np.ndarray:
+    """-> int64[world + 1] message-index boundaries holding ~1/world of the wire bytes each (the
+    bytes track the vote count, the work unit)."""
+    n = int(msg_len.shape[0])
+    if world <= 1 or n == 0:
+        return np.array([0] + [n] * max(world, 1), np.int64)
+    w = np.cumsum(msg_len.astype(np.int64) + 1)
+    cuts = np.searchsorted(w, w[-1] * np.arange(1, world, dtype=np.float64) / world, side="left") + 1
+    cuts = np.minimum(np.maximum.accumulate(cuts), n)
+    return np.concatenate([[0], cuts, [n]]).astype(np.int64)
+
+
+def validate_wire_sharded(engine, wire: np.ndarray, msg_off: np.ndarray, msg_len: np.ndarray, scope: np.ndarray,
+                          now: int, group=None, device: Optional[str] = None):
+    """Every rank passes the same gossip bytes; rank r decodes + validates its contiguous range of
+    messages (hlc_validate_wire_proposals on its own GPU) and all ranks receive every message's
+    (hlc_result, hlc_wire_proposal), identical to one call over the whole batch."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if device is None:
+        device = "cpu" if dist.get_backend(group) == "gloo" else f"cuda:{__import__('torch').cuda.current_device()}"
+    bounds = wire_shard_bounds(msg_len, world)
+    m0, m1 = int(bounds[rank]), int(bounds[rank + 1])
+    sc = scope if scope.shape[0] == 1 else scope[m0:m1]
+    if m1 > m0:
+        lo = int(msg_off[m0:m1].min())
+        hi = int((msg_off[m0:m1] + msg_len[m0:m1].astype(np.uint64)).max())
+        res, winfo, _ = engine.validate_wire_proposals(wire[lo:hi], msg_off[m0:m1] - np.uint64(lo), msg_len[m0:m1],
+                                                       sc, now)
+    else:
+        res = np.zeros(0, _ffi.RESULT_DTYPE)
+        winfo = np.zeros(0, _ffi.WIRE_PROPOSAL_DTYPE)
+    rrows = _gather_rows(np.ascontiguousarray(res).view(np.uint8).reshape(-1, _ffi.RESULT_DTYPE.itemsize), bounds,
+                         rank, world, group, device)
+    wrows = _gather_rows(np.ascontiguousarray(winfo).view(np.uint8).reshape(-1, _ffi.WIRE_PROPOSAL_DTYPE.itemsize),
+                         bounds, rank, world, group, device)
+    return (rrows.reshape(-1).view(_ffi.RESULT_DTYPE).copy(), wrows.reshape(-1).view(_ffi.WIRE_PROPOSAL_DTYPE).copy())
+
+
+# ---- streaming path: sessions are independent --------------------------------------------------
+def process_votes_sharded(engine, batch: VoteBatch, vote_session: np.ndarray, sessions: np.ndarray,
+                          owners: np.ndarray, owner_session: np.ndarray, now: int, group=None,
+                          device: Optional[str] = None):
+    """Micro-batched process_incoming_vote across ranks: session s lives on rank s % world (its
+    owner map with it), so each rank processes exactly the votes of its sessions, in delivery
+    order, on its own GPU (hlc_process_votes) -- no vote ever needs another rank's state.  Every
+    rank passes the same inputs and receives every vote's (status, transition, inserted, reason)
+    and every session's final state, identical to one call over the whole batch."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if device is None:
+        device = "cpu" if dist.get_backend(group) == "gloo" else f"cuda:{__import__('torch').cuda.current_device()}"
+    S = sessions.shape[0]
+    mine_s = np.arange(rank, S, world, dtype=np.int64)              # my sessions (global ids)
+    local_of = np.full(S, 0xFFFFFFFF, np.int64)
+    local_of[mine_s] = np.arange(mine_s.size)
+    vs = vote_session.astype(np.int64)
+    found = vs != 0xFFFFFFFF
+    vsafe = np.where(found, vs, 0)
+    # votes for missing sessions are answered by rank 0 (SessionNotFound needs no state)
+    mine_v = np.nonzero(np.where(found, (vsafe % world) == rank, rank == 0))[0]
+    sub = VoteBatch(batch.vote_id[mine_v], batch.proposal_id[mine_v], batch.timestamp[mine_v], batch.vote[mine_v],
+                    batch.arena, batch.field_off[mine_v], batch.field_len[mine_v])
+    lvs = np.where(found[mine_v], local_of[vsafe[mine_v]], 0xFFFFFFFF).astype(np.uint32)
+    lsess = np.ascontiguousarray(sessions[mine_s])
+    omask = (owner_session.astype(np.int64) % world) == rank
+    lown = np.ascontiguousarray(owners[omask]).reshape(-1, 20)
+    losess = local_of[owner_session[omask].astype(np.int64)].astype(np.uint32)
+    st, tr, ins, rs = engine.process_votes(sub, lvs, lsess, lown, losess, now)
+    # gather per-vote outputs (rows: global index u64 + 4 bytes) and session rows
+    vrow = np.zeros((mine_v.size, 12), np.uint8)
+    vrow[:, :8] = mine_v.astype(np.uint64).view(np.uint8).reshape(-1, 8)
+    vrow[:, 8], vrow[:, 9], vrow[:, 10], vrow[:, 11] = st, tr, ins, rs
+    import torch
+    counts = torch.tensor([mine_v.size, mine_s.size], dtype=torch.int64, device=device)
+    allc = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(allc, counts, group=group)
+    vb = np.concatenate([[0], np.cumsum([int(c[0]) for c in allc])])
+    sb = np.concatenate([[0], np.cumsum([int(c[1]) for c in allc])])
+    vrows = _gather_rows(vrow, vb, rank, world, group, device)
+    srow = np.zeros((mine_s.size, 8 + _ffi.SESSION_DTYPE.itemsize), np.uint8)
+    srow[:, :8] = mine_s.astype(np.uint64).view(np.uint8).reshape(-1, 8)
+    srow[:, 8:] = lsess.view(np.uint8).reshape(-1, _ffi.SESSION_DTYPE.itemsize)
+    srows = _gather_rows(srow, sb, rank, world, group, device)
+    n = batch.n
+    out = np.zeros((4, n), np.uint8)
+    gi = vrows[:, :8].copy().view(np.uint64).reshape(-1).astype(np.int64)
+    out[:, gi] = vrows[:, 8:12].T
+    final = sessions.copy()
+    si = srows[:, :8].copy().view(np.uint64).reshape(-1).astype(np.int64)
+    final[si] = srows[:, 8:].copy().reshape(-1).view(_ffi.SESSION_DTYPE)
+    return out[0], out[1], out[2], out[3], final

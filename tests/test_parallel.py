@@ -97,3 +97,80 @@ def test_gloo_world2_sharded_equals_single():
     for rank, res, st in got:
         assert res == ref.tobytes(), f"rank {rank} results differ"
         assert st == vst_ref.tobytes(), f"rank {rank} vote statuses differ"
+
+
+# ---- wire and streaming paths across ranks (gloo, world size 2) ----------------------------------
+def _worker2(rank, world, port, kind, payload, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "hashgraph-like-consensus_amd", "python"),
+              os.path.join(os.path.dirname(here), "oracle"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from oracle_engines import OracleEngine as OE
+    from hashgraph_like_consensus.batch import VoteBatch
+    from hashgraph_like_consensus.parallel import process_votes_sharded, validate_wire_sharded
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if kind == "wire":
+            res, winfo = validate_wire_sharded(OE(), *payload)
+            q.put((rank, res.tobytes() + winfo.tobytes()))
+        else:
+            batch = VoteBatch(*payload[0])
+            out = process_votes_sharded(OE(), batch, *payload[1:])
+            q.put((rank, b"".join(np.ascontiguousarray(o).tobytes() for o in out)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run2(kind, payload):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker2, args=(r, 2, port, kind, payload, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_gloo_world2_wire_sharded_equals_single():
+    import random
+    from oracle_engines import OracleEngine as OE
+    from hashgraph_like_consensus import _ffi, synth
+    from hashgraph_like_consensus.protos import encode_proposal
+    from wire_fuzz import mutate, random_proposal
+    w = oracle_workload(5, 6, 8, True, seed=43)
+    batch, desc, _ = byzantine(w, fraction=0.25, seed=11)
+    wire, off, lens, scope = synth.to_wire(batch, desc)
+    rnd = random.Random(3)
+    extra = [mutate(rnd, encode_proposal(random_proposal(rnd, max_votes=2))) for _ in range(6)]
+    ew = b"".join(extra)
+    eo = np.cumsum([0] + [len(e) for e in extra[:-1]]).astype(np.uint64) + np.uint64(wire.size)
+    wire = np.concatenate([wire, np.frombuffer(ew, np.uint8)])
+    off = np.concatenate([off, eo])
+    lens = np.concatenate([lens, np.array([len(e) for e in extra], np.uint32)])
+    scope = np.concatenate([scope, scope[:1].repeat(len(extra))])
+    ref_res, ref_w, _ = OE().validate_wire_proposals(wire, off, lens, scope, w.now)
+    ref = ref_res.tobytes() + ref_w.tobytes()
+    for rank, got in _run2("wire", (wire, off, lens, scope, w.now)):
+        assert got == ref, f"rank {rank}: sharded wire outcomes differ"
+
+
+def test_gloo_world2_stream_sharded_equals_single():
+    from oracle_engines import OracleEngine as OE
+    from stream_cases import device_inputs, streaming_workload
+    sessions, votes, vs, now = streaming_workload(0x484C4340, n_props=8, votes=6)
+    batch, vsess, sarr, owners, osess = device_inputs(sessions, votes, vs)
+    ref_s = sarr.copy()
+    st, tr, ins, rs = OE().process_votes(batch, vsess, ref_s, owners, osess, now)
+    ref = b"".join(np.ascontiguousarray(o).tobytes() for o in (st, tr, ins, rs, ref_s))
+    payload = ((batch.vote_id, batch.proposal_id, batch.timestamp, batch.vote, batch.arena, batch.field_off,
+                batch.field_len), vsess, sarr, owners, osess, now)
+    for rank, got in _run2("stream", payload):
+        assert got == ref, f"rank {rank}: sharded streaming outcomes differ"
