@@ -320,7 +320,10 @@ def main() -> int:
         "dtype": "u32",
         "data": "synthetic: deterministic signed votes (SURVEY §8d spec), generated + RFC6979-signed on the GPU",
         "config": {
-            "workload": "config2: 10k proposals x 64 voters (Gossipsub, n=64) per GPU, full from_proposal validation",
+            "workload": (f"config2: {P} proposals x {V} voters (Gossipsub, n={V}) per GPU, full from_proposal validation"
+                         if (P, V) == (10_000, 64) else
+                         f"config2-shaped: {P} proposals x {V} voters (Gossipsub, n={V}) per GPU, full from_proposal "
+                         f"validation" + (" (one rank's shard of config 4, 100M votes / 8 GPUs)" if P == 195_313 else "")),
             "proposals_per_gpu": P,
             "votes_per_proposal": V,
             "votes_per_step_per_gpu": db.n,
