@@ -180,3 +180,33 @@ def test_gpu_decode_large_messages(engine):
     big[len(big) // 2] ^= 0x80  # corrupt somewhere in the middle of the vote records
     msgs.append(bytes(big))
     _check_decode(engine, msgs, _scope(1))
+
+
+def test_gpu_decode_capacity_contract(engine):
+    """hlc_decode_proposals: too small a vote capacity -> HLC_ERANGE with the needed count reported
+    and the proposal records still written; NULL vote arrays query the count."""
+    import ctypes
+    from ctypes import c_uint8, c_uint32, c_uint64, c_void_p
+    rnd = random.Random(25)
+    msgs = [encode_proposal(random_proposal(rnd, max_votes=4)) for _ in range(8)]
+    wire, off, lens = _pack(msgs)
+    sc = _scope(1)
+    props = np.zeros(8, _ffi.PROPOSAL_DTYPE)
+    nv = c_uint64(0)
+    lib = engine.lib
+    args = (engine.ctx, _ffi.ptr(wire, c_uint8), wire.size, _ffi.ptr(off, c_uint64), _ffi.ptr(lens, c_uint32), 8,
+            c_void_p(sc.ctypes.data), 1, c_void_p(props.ctypes.data), None, ctypes.byref(nv))
+    assert lib.hlc_decode_proposals(*args, None, None, None, None, None, None) == 0
+    need = nv.value
+    assert need == sum(len(wo.decode_proposal(m)[1].votes) for m in msgs)
+    if need == 0:
+        return
+    small = [np.zeros(max(need, 1) * k, dt) for k, dt in ((1, np.uint32), (1, np.uint32), (1, np.uint64),
+                                                           (1, np.uint8), (5, np.uint64), (5, np.uint32))]
+    nv.value = need - 1
+    props[:] = 0
+    rc = lib.hlc_decode_proposals(*args, *[_ffi.ptr(a, t) for a, t in zip(small, (c_uint32, c_uint32, c_uint64, c_uint8,
+                                                                                 c_uint64, c_uint32))])
+    assert rc == -5 and nv.value == need          # HLC_ERANGE, count reported
+    assert int(props["vote_count"].sum()) == need  # proposal records written anyway
+    assert all(not a.any() for a in small)         # vote arrays untouched
