@@ -103,7 +103,7 @@ struct hlc_ctx {
   DBuf w_vid, w_pid, w_ts, w_vote, w_foff, w_flen;
   // streaming votes
   DBuf s_vsess, s_sessions, s_owners, s_osess, s_props, s_keys, s_iota, s_order, s_segb, s_sege, s_tab, s_sort_tmp,
-      s_st, s_tr, s_ins;
+      s_st, s_tr, s_ins, s_slot, s_dup;
 };
 
 namespace {
@@ -694,14 +694,16 @@ int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vses
   // 3. (session, owner) table: existing owner maps, then add_vote in order per session
   uint64_t cap = 64;
   while (cap < 2 * (n + n_owners)) cap <<= 1;
-  CHK(ctx->s_tab.ensure(cap * 4));
-  HIPCHK(hipMemsetAsync(ctx->s_tab.p, 0xFF, cap * 4, s));
-  hlc::launch_owner_insert(ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1), owners, owner_session, n_owners, dv, vsess,
-                           s);
+  CHK(ctx->s_tab.ensure(cap * 8));  // keys, then the minimum delivery position per key
+  HIPCHK(hipMemsetAsync(ctx->s_tab.p, 0xFF, cap * 8, s));
+  CHK(ctx->s_slot.ensure(n * 4 + 4));
+  CHK(ctx->s_dup.ensure(n + 1));
   hlc::launch_stream_init(n, vsess, ctx->status.as<uint8_t>(), st, tr, ins, s);
+  uint32_t* tab = ctx->s_tab.as<uint32_t>();
+  hlc::launch_dup_flags(tab, tab + cap, (uint32_t)(cap - 1), owners, owner_session, n_owners, dv, vsess, st,
+                        ctx->s_slot.as<uint32_t>(), ctx->s_dup.as<uint8_t>(), s);
   hlc::launch_apply_votes(dss, n_sessions, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(),
-                          ctx->s_order.as<uint32_t>(), dv, now, ctx->s_tab.as<uint32_t>(), (uint32_t)(cap - 1), owners,
-                          owner_session, n_owners, vsess, st, tr, ins, s);
+                          ctx->s_order.as<uint32_t>(), dv, now, ctx->s_dup.as<uint8_t>(), st, tr, ins, s);
   HIPCHK(hipGetLastError());
   return 0;
 }

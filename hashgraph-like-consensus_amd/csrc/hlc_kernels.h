@@ -109,14 +109,15 @@ void launch_sessions_to_props(const hlc_session* ss, uint64_t m, hlc_proposal* p
 void launch_sort_by_session(const uint32_t* vote_session, uint64_t n, uint32_t* keys_out, uint32_t* iota,
                             uint32_t* order, void* temp, size_t& temp_bytes, hipStream_t s);
 void launch_segments(const uint32_t* keys, uint64_t n, uint32_t* seg_begin, uint32_t* seg_end, hipStream_t s);
-void launch_owner_insert(uint32_t* tab, uint32_t mask, const uint8_t* owners, const uint32_t* owner_session,
-                         uint64_t n_owners, const hlc_votes* v, const uint32_t* vote_session, hipStream_t s);
+// duplicate flags: tab (pre-set to ~0), minv (pre-set to ~0) sized mask + 1; slot_of[n], dup[n]
+void launch_dup_flags(uint32_t* tab, uint32_t* minv, uint32_t mask, const uint8_t* owners,
+                      const uint32_t* owner_session, uint64_t n_owners, const hlc_votes* v, const uint32_t* vote_session,
+                      const uint8_t* st, uint32_t* slot_of, uint8_t* dup, hipStream_t s);
 void launch_stream_init(uint64_t n, const uint32_t* vote_session, const uint8_t* vstatus, uint8_t* st, uint8_t* tr,
                         uint8_t* ins, hipStream_t s);
 void launch_apply_votes(hlc_session* ss, uint64_t m, const uint32_t* seg_begin, const uint32_t* seg_end,
-                        const uint32_t* order, const hlc_votes* v, uint64_t now, uint32_t* tab, uint32_t mask,
-                        const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
-                        const uint32_t* vote_session, uint8_t* st, uint8_t* tr, uint8_t* ins, hipStream_t s);
+                        const uint32_t* order, const hlc_votes* v, uint64_t now, const uint8_t* dup, uint8_t* st,
+                        uint8_t* tr, uint8_t* ins, hipStream_t s);
 
 // ---- signing ----
 void launch_build_fbtab(uint32_t* fbtab, hipStream_t s);

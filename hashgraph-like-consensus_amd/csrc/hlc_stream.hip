@@ -4,11 +4,12 @@
 // prehash / recovery / status kernels as validate-many; this file holds the session side:
 //   k_sessions_to_props  session -> hlc_proposal (the scalars validate_vote reads)
 //   radix sort of (session, vote index), stable -> each session's votes in delivery order
-//   k_owner_insert       existing owner maps -> one global (session, owner) hash table
+//   k_owner_insert, k_vote_owner_insert, k_dup_flags
+//                        one global (session, owner) hash table with the minimum delivery
+//                        position per key -> every vote's duplicate flag, in parallel
 //   k_apply_votes        one lane per session walks its votes in order: add_vote
 //                        (session.rs:225-249) with check_round_limit / update_round /
-//                        check_consensus (session.rs:306-387) and the duplicate-owner test
-//                        against the table (insert on accept)
+//                        check_consensus (session.rs:306-387) -- register-only, no probes
 // Integer work on a few bytes per vote; the sequential part is per session only.
 #include <hipcub/hipcub.hpp>
 
@@ -69,21 +70,21 @@ __device__ __forceinline__ bool same_owner(const uint8_t* a, const uint8_t* b) {
   return d == 0;
 }
 
-// Find (session, owner) or insert ref.  Returns true when the key was already present.
-// Slots are never deleted, so a lane always re-finds the keys it inserted itself.
-__device__ bool find_or_insert(uint32_t* tab, uint32_t mask, const OwnerKeys& k, uint32_t session,
-                               const uint8_t* owner, uint32_t ref) {
+// Slot of key (session, owner), claiming an empty one with `ref` when the key is absent.
+// Slots are never deleted, so every lane re-finds a key another lane inserted.
+__device__ uint32_t key_slot(uint32_t* tab, uint32_t mask, const OwnerKeys& k, uint32_t session,
+                             const uint8_t* owner, uint32_t ref) {
   uint32_t slot = owner_hash(session, owner) & mask;
   for (;;) {
     uint32_t cur = __hip_atomic_load(tab + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == EMPTY) {
       cur = atomicCAS(tab + slot, EMPTY, ref);
-      if (cur == EMPTY) return false;
+      if (cur == EMPTY) return slot;
     }
     uint32_t s2;
     const uint8_t* o2;
     key_of(k, cur, s2, o2);
-    if (s2 == session && same_owner(o2, owner)) return true;
+    if (s2 == session && same_owner(o2, owner)) return slot;
     slot = (slot + 1) & mask;
   }
 }
@@ -124,10 +125,36 @@ __global__ void __launch_bounds__(TPB) k_segments(const uint32_t* __restrict__ k
   if (j + 1 == n || key[j + 1] != s) seg_end[s] = (uint32_t)(j + 1);
 }
 
-__global__ void __launch_bounds__(TPB) k_owner_insert(uint32_t* tab, uint32_t mask, OwnerKeys k) {
+// Duplicate test without the sequential replay (session.rs:236-238).  Within one session's
+// delivery order, once a validated vote is refused for any reason but DuplicateVote (decided,
+// Failed, expired, round limit), no later vote is inserted.  So a vote that reaches the
+// duplicate test is a duplicate iff its owner is in the existing map or an EARLIER validated
+// vote of the session has the same owner.  minv[slot] = min over (existing owner -> 0,
+// validated vote i -> i + 1); vote i is a duplicate iff minv < i + 1.
+__global__ void __launch_bounds__(TPB) k_owner_insert(uint32_t* tab, uint32_t* minv, uint32_t mask, OwnerKeys k) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= k.n_owners) return;
-  find_or_insert(tab, mask, k, k.owner_session[r], k.owners + 20ull * r, (uint32_t)r);
+  const uint32_t slot = key_slot(tab, mask, k, k.owner_session[r], k.owners + 20ull * r, (uint32_t)r);
+  atomicMin(minv + slot, 0u);
+}
+
+__global__ void __launch_bounds__(TPB) k_vote_owner_insert(uint64_t n, const uint8_t* __restrict__ st,
+                                                           uint32_t* tab, uint32_t* minv, uint32_t mask, OwnerKeys k,
+                                                           uint32_t* __restrict__ slot_of) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || st[i] != HLC_OK) return;  // only votes that passed validate_vote reach add_vote
+  const uint8_t* owner = k.bytes + k.field_off[i * HLC_NFIELDS + HLC_F_OWNER];
+  const uint32_t slot = key_slot(tab, mask, k, k.vote_session[i], owner, (uint32_t)(k.n_owners + i));
+  atomicMin(minv + slot, (uint32_t)(i + 1));
+  slot_of[i] = slot;
+}
+
+__global__ void __launch_bounds__(TPB) k_dup_flags(uint64_t n, const uint8_t* __restrict__ st,
+                                                   const uint32_t* __restrict__ minv,
+                                                   const uint32_t* __restrict__ slot_of, uint8_t* __restrict__ dup) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dup[i] = st[i] == HLC_OK && minv[slot_of[i]] < (uint32_t)(i + 1);
 }
 
 // per vote: SessionNotFound or the validate_vote status (the session side may override OK)
@@ -142,13 +169,15 @@ __global__ void __launch_bounds__(TPB) k_stream_init(uint64_t n, const uint32_t*
 }
 
 // ConsensusSession::add_vote for every validated vote of session s, in delivery order.
-__global__ void __launch_bounds__(TPB) k_apply_votes(hlc_session* __restrict__ ss, uint64_t m,
-                                                     const uint32_t* __restrict__ seg_begin,
-                                                     const uint32_t* __restrict__ seg_end,
-                                                     const uint32_t* __restrict__ order, const uint8_t* vote,
-                                                     uint64_t now, uint32_t* tab, uint32_t mask, OwnerKeys k,
-                                                     uint8_t* __restrict__ st, uint8_t* __restrict__ tr,
-                                                     uint8_t* __restrict__ ins) {
+constexpr int APPLY_TPB = 64;  // one wave per block: 10k sessions spread over 157 CUs
+
+__global__ void __launch_bounds__(APPLY_TPB) k_apply_votes(hlc_session* __restrict__ ss, uint64_t m,
+                                                           const uint32_t* __restrict__ seg_begin,
+                                                           const uint32_t* __restrict__ seg_end,
+                                                           const uint32_t* __restrict__ order, const uint8_t* vote,
+                                                           uint64_t now, const uint8_t* __restrict__ dup,
+                                                           uint8_t* __restrict__ st, uint8_t* __restrict__ tr,
+                                                           uint8_t* __restrict__ ins) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= m) return;
   const uint32_t b = seg_begin[s], e = seg_end[s];
@@ -181,8 +210,7 @@ __global__ void __launch_bounds__(TPB) k_apply_votes(hlc_session* __restrict__ s
         x.state = HLC_SESSION_FAILED;
         code = HLC_MAX_ROUNDS_EXCEEDED;
       } else {
-        const uint8_t* owner = k.bytes + k.field_off[(uint64_t)i * HLC_NFIELDS + HLC_F_OWNER];
-        if (find_or_insert(tab, mask, k, (uint32_t)s, owner, (uint32_t)(k.n_owners + i))) {
+        if (dup[i]) {
           code = HLC_DUPLICATE_VOTE;  // session.rs:236-238
         } else {
           ins[i] = 1;
@@ -241,11 +269,15 @@ static OwnerKeys owner_keys(const uint8_t* owners, const uint32_t* owner_session
   return k;
 }
 
-void launch_owner_insert(uint32_t* tab, uint32_t mask, const uint8_t* owners, const uint32_t* owner_session,
-                         uint64_t n_owners, const hlc_votes* v, const uint32_t* vote_session, hipStream_t s) {
-  if (!n_owners) return;
-  hipLaunchKernelGGL(k_owner_insert, dim3(blocks_for(n_owners)), dim3(TPB), 0, s, tab, mask,
-                     owner_keys(owners, owner_session, n_owners, v, vote_session));
+void launch_dup_flags(uint32_t* tab, uint32_t* minv, uint32_t mask, const uint8_t* owners,
+                      const uint32_t* owner_session, uint64_t n_owners, const hlc_votes* v, const uint32_t* vote_session,
+                      const uint8_t* st, uint32_t* slot_of, uint8_t* dup, hipStream_t s) {
+  const OwnerKeys k = owner_keys(owners, owner_session, n_owners, v, vote_session);
+  if (n_owners) hipLaunchKernelGGL(k_owner_insert, dim3(blocks_for(n_owners)), dim3(TPB), 0, s, tab, minv, mask, k);
+  const uint64_t n = v->n;
+  if (!n) return;
+  hipLaunchKernelGGL(k_vote_owner_insert, dim3(blocks_for(n)), dim3(TPB), 0, s, n, st, tab, minv, mask, k, slot_of);
+  hipLaunchKernelGGL(k_dup_flags, dim3(blocks_for(n)), dim3(TPB), 0, s, n, st, minv, slot_of, dup);
 }
 
 void launch_stream_init(uint64_t n, const uint32_t* vote_session, const uint8_t* vstatus, uint8_t* st, uint8_t* tr,
@@ -255,12 +287,11 @@ void launch_stream_init(uint64_t n, const uint32_t* vote_session, const uint8_t*
 }
 
 void launch_apply_votes(hlc_session* ss, uint64_t m, const uint32_t* seg_begin, const uint32_t* seg_end,
-                        const uint32_t* order, const hlc_votes* v, uint64_t now, uint32_t* tab, uint32_t mask,
-                        const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
-                        const uint32_t* vote_session, uint8_t* st, uint8_t* tr, uint8_t* ins, hipStream_t s) {
+                        const uint32_t* order, const hlc_votes* v, uint64_t now, const uint8_t* dup, uint8_t* st,
+                        uint8_t* tr, uint8_t* ins, hipStream_t s) {
   if (!m) return;
-  hipLaunchKernelGGL(k_apply_votes, dim3(blocks_for(m)), dim3(TPB), 0, s, ss, m, seg_begin, seg_end, order, v->vote,
-                     now, tab, mask, owner_keys(owners, owner_session, n_owners, v, vote_session), st, tr, ins);
+  hipLaunchKernelGGL(k_apply_votes, dim3((unsigned)((m + APPLY_TPB - 1) / APPLY_TPB)), dim3(APPLY_TPB), 0, s, ss, m,
+                     seg_begin, seg_end, order, v->vote, now, dup, st, tr, ins);
 }
 
 }  // namespace hlc
