@@ -210,3 +210,61 @@ def test_gpu_decode_capacity_contract(engine):
     assert rc == -5 and nv.value == need          # HLC_ERANGE, count reported
     assert int(props["vote_count"].sum()) == need  # proposal records written anyway
     assert all(not a.any() for a in small)         # vote arrays untouched
+
+
+def _hip():
+    """The HIP runtime libhlc.so itself uses (already loaded by the engine): device buffers for the
+    device-pointer entry points without a second runtime in the process."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+def test_gpu_wire_device_entry_misaligned(engine):
+    """hlc_validate_wire_proposals_device on a wire pointer that is not 16-byte aligned (the
+    walker's and vote kernel's byte-wise fallback paths) == the host-buffer entry."""
+    import ctypes
+    from ctypes import c_void_p
+    hip = _hip()
+    w = oracle_workload(6, 8, 8, True, 0x484C4314, name="wire-misaligned")
+    wire, off, lens, scope = synth.to_wire(w.batch, w.desc)
+    ref, rw, _ = engine.validate_wire_proposals(wire, off, lens, scope, w.now)
+    m = off.size
+
+    def dev(nbytes):
+        p = c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), max(nbytes, 16)) == 0
+        return p
+
+    def h2d(d, a):
+        assert hip.hipMemcpy(d, a.ctypes.data, a.nbytes, 1) == 0
+
+    def d2h(a, d):
+        assert hip.hipMemcpy(a.ctypes.data, d, a.nbytes, 2) == 0
+
+    bufs = {k: dev(n) for k, n in (("wire", wire.size + 16), ("off", off.nbytes), ("len", lens.nbytes),
+                                    ("scope", scope.nbytes), ("res", m * 16), ("wi", m * 48))}
+    try:
+        h2d(bufs["off"], off)
+        h2d(bufs["len"], lens)
+        h2d(bufs["scope"], scope)
+        for shift in (0, 3, 8):
+            padded = np.zeros(wire.size + 16, np.uint8)
+            padded[shift:shift + wire.size] = wire
+            h2d(bufs["wire"], padded)
+            _ffi.check(engine.lib.hlc_validate_wire_proposals_device(
+                engine.ctx, c_void_p(bufs["wire"].value + shift), wire.size, bufs["off"], bufs["len"], m,
+                bufs["scope"], scope.size, w.now, bufs["res"], bufs["wi"], None))
+            assert hip.hipDeviceSynchronize() == 0  # the entry is asynchronous on the context's stream
+            res = np.zeros(m, _ffi.RESULT_DTYPE)
+            wi = np.zeros(m, _ffi.WIRE_PROPOSAL_DTYPE)
+            d2h(res, bufs["res"])
+            d2h(wi, bufs["wi"])
+            assert np.array_equal(res, ref), f"shift {shift}: results differ"
+            assert np.array_equal(wi, rw), f"shift {shift}: wire info differs"
+    finally:
+        for p in bufs.values():
+            hip.hipFree(p)
