@@ -201,7 +201,9 @@ typedef struct hlc_ctx hlc_ctx;
  * state is what the static `Signer::verify` of signing.rs:69 needs). */
 int hlc_ctx_create(int device, hlc_ctx** out);
 void hlc_ctx_destroy(hlc_ctx* ctx);
-/* Pre-sizes the device workspace so later calls allocate nothing (graph-capture safe). */
+/* Pre-sizes the validate-many workspace (hlc_validate_proposals[_device] up to these sizes then
+ * allocates nothing).  The wire-decode and streaming paths grow their own workspace on first
+ * use and keep it for later calls of the same or smaller size. */
 int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, uint64_t max_bytes);
 const char* hlc_last_error(void);
 int hlc_abi_version(void);
