@@ -42,7 +42,7 @@ MAD_PEAK_T_PER_S = 256 * 4 * 16 * 2.4e9 / 1e12
 # rocprofv3 PMC passes of this same bench command (tools/profile.sh), committed under profiles/:
 # `traffic` = memory-side bytes per k_recover launch from FETCH_SIZE / WRITE_SIZE (KiB), with the
 # gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes).
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r01_rocprof_v12_s6")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r01_rocprof_v13_s7")
 
 
 def pmc_traffic(kernel: str = "k_recover"):
