@@ -268,3 +268,19 @@ def test_gpu_wire_device_entry_misaligned(engine):
     finally:
         for p in bufs.values():
             hip.hipFree(p)
+
+
+def test_gpu_wire_single_large_p2p_proposal(engine):
+    """One P2P proposal with 20,000 chained votes as a single gossip message: the walker's second
+    pass (> 128 records) and the global chain / duplicate tables (> 512 votes) behind the wire
+    path, against the SoA path and the C oracle; plus a re-linked vote and a replayed voter."""
+    w = synth.generate(1, 20_000, 30_000, False, synth.config_seed(3), *synth.engine_signers(engine))
+    res = _wire_vs_oracle(engine, w.batch, w.desc, w.now)
+    assert int(res[0]["status"]) == 0 and int(res[0]["total"]) == 20_000
+    # a duplicate voter: vote 15000's owner bytes replaced by vote 100's (hash and signature now
+    # fail too, so the first error is that vote's own validation failure, not the chain)
+    b = w.batch
+    o1, o2 = int(b.field_off[15_000, 0]), int(b.field_off[100, 0])
+    b.arena[o1:o1 + 20] = b.arena[o2:o2 + 20]
+    res = _wire_vs_oracle(engine, b, w.desc, w.now)
+    assert int(res[0]["status"]) != 0 and int(res[0]["bad_index"]) == 15_000
