@@ -2,6 +2,7 @@
 // and the orchestration of the kernels in hlc_prehash.hip / hlc_recover.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -100,6 +101,7 @@ struct hlc_ctx {
   // wire decode: staged inputs, walk / record workspace, decoded votes (hlc_votes SoA over the wire bytes)
   DBuf w_wire, w_moff, w_mlen, w_scope, w_vcount, w_vbegin, w_vrec_off, w_vrec_len, w_vrec_msg, w_first_bad,
       w_vote_err, w_props, w_wout, w_res, w_slab_off, w_slab_len, w_big;
+  DBuf w_huge, h_next, h_jump, h_mark, h_st, h_flag, h_rank, h_scan, h_off, h_len, h_fix;
   DBuf w_vid, w_pid, w_ts, w_vote, w_foff, w_flen;
   // streaming votes
   DBuf s_vsess, s_sessions, s_owners, s_osess, s_props, s_keys, s_iota, s_order, s_segb, s_sege, s_tab, s_sort_tmp,
@@ -287,14 +289,63 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
   CHK(c->w_big.ensure(16));
   uint64_t* vcount = c->w_vcount.as<uint64_t>();
   uint64_t* vbegin = c->w_vbegin.as<uint64_t>();
+  CHK(c->w_huge.ensure(nm * 16 + 16));
   uint64_t nv = 0;
   uint32_t big = 0;
+  // (message index, length) of the messages decoded by the parallel path; only a wire buffer
+  // longer than the threshold can hold one, so other calls skip the extra synchronisation.
+  std::vector<uint64_t> huge;
+  constexpr uint32_t kMaxFix = 1u << 16;  // top-level groups longer than 256 B on one huge message's chain
+  uint64_t huge_recs = 0;
   if (nm) {
     HIPCHK(hipMemsetAsync(c->w_big.p, 0, 4, s));
+    HIPCHK(hipMemsetAsync(c->w_huge.p, 0, 8, s));
     hlc::launch_wire_touch(wire, wire_len, c->w_big.as<uint32_t>() + 1, s);
     hlc::launch_wire_walk(0, wire, moff, mlen, nm, vcount, nullptr, dwout, dprops, scope, n_scope,
                           c->w_slab_off.as<uint64_t>(), c->w_slab_len.as<uint32_t>(), c->w_big.as<uint32_t>(), nullptr,
-                          nullptr, nullptr, s);
+                          nullptr, nullptr, c->w_huge.as<uint64_t>(), s);
+    if (wire_len > hlc::wire_huge_threshold()) {
+      uint64_t nh = 0;
+      HIPCHK(hipMemcpyAsync(&nh, c->w_huge.p, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      huge.resize(2 * nh);
+      if (nh) {
+        HIPCHK(hipMemcpyAsync(huge.data(), c->w_huge.as<uint64_t>() + 1, 16 * nh, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+      }
+      uint64_t maxlen = 0;
+      for (uint64_t i = 0; i < nh; ++i) {
+        maxlen = std::max(maxlen, huge[2 * i + 1]);
+        huge_recs += huge[2 * i + 1] / 2 + 1;  // a field takes >= 2 bytes
+      }
+      if (nh) {
+        const size_t tb = hlc::huge_scan_bytes((uint32_t)maxlen);
+        CHK(c->h_next.ensure(maxlen * 4 + 16));
+        CHK(c->h_jump.ensure(maxlen * 4 + 16));
+        CHK(c->h_mark.ensure(maxlen + 16));
+        CHK(c->h_st.ensure(64));
+        CHK(c->h_fix.ensure(8 * kMaxFix + 16));
+        CHK(c->h_flag.ensure(maxlen * 8 + 16));
+        CHK(c->h_rank.ensure(maxlen * 8 + 16));
+        CHK(c->h_scan.ensure(tb + 16));
+        CHK(c->h_off.ensure(huge_recs * 8 + 8));
+        CHK(c->h_len.ensure(huge_recs * 4 + 4));
+        std::vector<uint64_t> moff_h(nh);
+        for (uint64_t i = 0; i < nh; ++i)
+          HIPCHK(hipMemcpyAsync(&moff_h[i], moff + huge[2 * i], 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        uint64_t hb = 0;
+        for (uint64_t i = 0; i < nh; ++i) {
+          const uint32_t len = (uint32_t)huge[2 * i + 1];
+          hlc::launch_huge_decode(wire, huge[2 * i], moff_h[i], len, c->h_next.as<uint32_t>(),
+                                  c->h_jump.as<uint32_t>(), c->h_mark.as<uint8_t>(), c->h_st.as<uint32_t>(),
+                                  c->h_flag.as<uint64_t>(), c->h_rank.as<uint64_t>(), c->h_scan.p, tb,
+                                  c->h_off.as<uint64_t>() + hb, c->h_len.as<uint32_t>() + hb, vcount, dwout, dprops,
+                                  scope, n_scope, c->h_fix.as<uint32_t>(), kMaxFix, s);
+          hb += len / 2 + 1;
+        }
+      }
+    }
     size_t tb = 0;
     hlc::launch_exclusive_scan(vcount, vbegin, nm, nullptr, tb, s);
     CHK(c->scan_tmp.ensure(tb + 16));
@@ -334,7 +385,11 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
     if (big)  // messages with more vote records than the walker's slab: walk them again, writing in place
       hlc::launch_wire_walk(1, wire, moff, mlen, nm, vcount, vbegin, dwout, dprops, scope, n_scope, nullptr, nullptr,
                             nullptr, c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(),
-                            c->w_vrec_msg.as<uint32_t>(), s);
+                            c->w_vrec_msg.as<uint32_t>(), c->w_huge.as<uint64_t>(), s);
+    for (uint64_t i = 0, hb = 0; 2 * i < huge.size(); hb += huge[2 * i + 1] / 2 + 1, ++i)
+      hlc::launch_huge_place(huge[2 * i], vcount, vbegin, c->h_off.as<uint64_t>() + hb, c->h_len.as<uint32_t>() + hb,
+                             c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(),
+                             c->w_vrec_msg.as<uint32_t>(), s);
     HIPCHK(hipMemsetAsync(c->w_first_bad.p, 0xFF, nm * 4, s));
     hlc::launch_wire_votes(wire, moff, mlen, nv, c->w_vrec_off.as<uint64_t>(), c->w_vrec_len.as<uint32_t>(),
                            c->w_vrec_msg.as<uint32_t>(), vbegin, dv, c->w_vote_err.as<uint8_t>(),

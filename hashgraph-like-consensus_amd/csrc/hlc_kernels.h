@@ -88,7 +88,22 @@ void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const
 void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
                       uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout, hlc_proposal* pout,
                       const hlc_scope_config* scope, uint64_t n_scope, uint64_t* slab_off, uint32_t* slab_len,
-                      uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, hipStream_t s);
+                      uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, uint64_t* huge,
+                      hipStream_t s);
+// Messages longer than wire_huge_threshold() are skipped by the walker (mode 0 appends (m, len) to
+// huge[1..], count in huge[0]) and decoded by launch_huge_decode: parallel field-boundary discovery
+// (next[] per byte offset + pointer jumping), records into hoff/hlen in stream order, then
+// launch_huge_place moves them to vote_begin[m] after the scan.
+uint64_t wire_huge_threshold();
+size_t huge_scan_bytes(uint32_t len);
+void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
+                        uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
+                        size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
+                        hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
+                        uint32_t* fix, uint32_t max_fix, hipStream_t s);
+void launch_huge_place(uint64_t m, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* hoff,
+                       const uint32_t* hlen, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg,
+                       hipStream_t s);
 void launch_wire_place(uint64_t nm, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* slab_off,
                        const uint32_t* slab_len, hlc_proposal* pout, uint64_t* vrec_off, uint32_t* vrec_len,
                        uint32_t* vrec_msg, hipStream_t s);

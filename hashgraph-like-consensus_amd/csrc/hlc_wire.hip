@@ -16,6 +16,9 @@
 // All integer/byte work, latency-bound on dependent varint reads.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <utility>
+
 #include "hlc_kernels.h"
 
 namespace hlc {
@@ -202,7 +205,14 @@ struct WalkOut {
   uint32_t name_len, payload_len, owner_len;
 };
 
-constexpr uint32_t SLAB = 128;   // vote records a walker keeps per message before the vote count is known
+constexpr uint32_t SLAB = 128;
+// Messages longer than this are not walked by one lane (about 1 us per field) but by the parallel
+// boundary-discovery path below.  Lengths >= HUGE_ERR cannot be encoded in its next[] array.
+constexpr uint32_t HUGE_MSG = 1u << 20;
+constexpr uint32_t HUGE_ERR = 0xFFFFFF00u;
+constexpr uint32_t HUGE_UNRES = 0xFFu;  // not a prost error code
+constexpr uint64_t HUGE_GROUP_SCAN = 256;
+__host__ __device__ __forceinline__ bool is_huge(uint32_t len) { return len > HUGE_MSG && len < HUGE_ERR; }   // vote records a walker keeps per message before the vote count is known
 
 // Loads wire[wlo, whi) (wlo 16-byte aligned) into LDS with the calling block's threads.
 __device__ __forceinline__ void load_window(uint8_t* lds, const uint8_t* __restrict__ wire, uint64_t wlo,
@@ -258,6 +268,41 @@ __device__ __forceinline__ int walk_field(const Src& src, const uint8_t* __restr
   }
 }
 
+// Per-message outputs of a completed top-level walk (shared by the serial walker and the
+// parallel huge-message path).
+__device__ __forceinline__ void emit_message(uint64_t m, const WalkOut& o, uint32_t nv, int err,
+                                             uint64_t* __restrict__ vote_count, hlc_wire_proposal* __restrict__ wout,
+                                             hlc_proposal* __restrict__ pout, const hlc_scope_config* scope,
+                                             uint64_t n_scope) {
+  vote_count[m] = nv;
+  hlc_wire_proposal w;
+  w.name_off = o.name_off;  // relative to the message; 0 when the field is absent
+  w.payload_off = o.payload_off;
+  w.owner_off = o.owner_off;
+  w.name_len = o.name_len;
+  w.payload_len = o.payload_len;
+  w.owner_len = o.owner_len;
+  w.round = o.round;
+  w.decode_status = (uint8_t)err;  // k_wire_final folds in the votes' errors
+  w.bad_vote = 0xFFFFFFFFu;
+  for (int k = 0; k < 3; ++k) w._pad[k] = 0;
+  wout[m] = w;
+  const hlc_scope_config sc = scope[n_scope == 1 ? 0 : m];
+  hlc_proposal p;
+  p.vote_begin = 0;
+  p.vote_count = nv;
+  p.proposal_id = o.proposal_id;
+  p.timestamp = o.timestamp;
+  p.expiration_timestamp = o.expiration;
+  p.expected_voters_count = o.expected_voters;
+  p.max_rounds = sc.max_rounds;
+  p.consensus_threshold = sc.consensus_threshold;
+  p.use_gossipsub_rounds = sc.use_gossipsub_rounds;
+  p.liveness_criteria_yes = o.liveness;
+  for (int k = 0; k < 6; ++k) p._pad[k] = 0;
+  pout[m] = p;
+}
+
 // Top-level walk of message m, one lane per message.  The walk is a chain of dependent reads
 // (key, length, skip) -- about one cache miss per field -- so lanes are kept independent: a wave
 // walks 64 messages at once.  (A wave-per-message walker parsing out of an LDS window measured
@@ -277,9 +322,17 @@ __global__ void __launch_bounds__(WALK_TPB) k_wire_walk(int mode, const uint8_t*
                                                    uint64_t n_scope, uint64_t* __restrict__ slab_off,
                                                    uint32_t* __restrict__ slab_len, uint32_t* __restrict__ big,
                                                    uint64_t* __restrict__ vrec_off, uint32_t* __restrict__ vrec_len,
-                                                   uint32_t* __restrict__ vrec_msg) {
+                                                   uint32_t* __restrict__ vrec_msg, uint64_t* __restrict__ huge) {
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nm) return;
+  if (is_huge(msg_len[m])) {  // decoded by the parallel boundary-discovery path instead
+    if (mode == 0) {
+      const uint64_t i = atomicAdd((unsigned long long*)huge, 1ull);
+      huge[1 + 2 * i] = m;
+      huge[2 + 2 * i] = msg_len[m];
+    }
+    return;
+  }
   if (mode == 1 && vote_count[m] <= SLAB) return;
   const uint64_t base = msg_off[m];
   const uint64_t end = base + msg_len[m];
@@ -312,34 +365,198 @@ __global__ void __launch_bounds__(WALK_TPB) k_wire_walk(int mode, const uint8_t*
     for (uint32_t k = 0; k < nv; ++k) vrec_msg[vote_begin[m] + k] = (uint32_t)m;
     return;
   }
-  vote_count[m] = nv;
   if (nv > SLAB) atomicOr(big, 1u);
-  hlc_wire_proposal w;
-  w.name_off = o.name_off;  // relative to the message; 0 when the field is absent
-  w.payload_off = o.payload_off;
-  w.owner_off = o.owner_off;
-  w.name_len = o.name_len;
-  w.payload_len = o.payload_len;
-  w.owner_len = o.owner_len;
-  w.round = o.round;
-  w.decode_status = (uint8_t)err;  // k_wire_final folds in the votes' errors
-  w.bad_vote = 0xFFFFFFFFu;
-  for (int k = 0; k < 3; ++k) w._pad[k] = 0;
-  wout[m] = w;
-  const hlc_scope_config sc = scope[n_scope == 1 ? 0 : m];
-  hlc_proposal p;
-  p.vote_begin = 0;
-  p.vote_count = nv;
-  p.proposal_id = o.proposal_id;
-  p.timestamp = o.timestamp;
-  p.expiration_timestamp = o.expiration;
-  p.expected_voters_count = o.expected_voters;
-  p.max_rounds = sc.max_rounds;
-  p.consensus_threshold = sc.consensus_threshold;
-  p.use_gossipsub_rounds = sc.use_gossipsub_rounds;
-  p.liveness_criteria_yes = o.liveness;
-  for (int k = 0; k < 6; ++k) p._pad[k] = 0;
-  pout[m] = p;
+  emit_message(m, o, nv, err, vote_count, wout, pout, scope, n_scope);
+}
+
+// ---- Huge messages: parallel record-boundary discovery --------------------------------------
+// One lane walking a 180 MB gossip message costs about 1 us per field however the bytes are
+// staged (dependent reads, branchy 64-bit arithmetic).  Instead every byte offset p of the message
+// is parsed as a candidate top-level field start: next[p] = offset just past that field, or
+// HUGE_ERR | error code.  The fields of the message are the chain 0 -> next[0] -> ... ; pointer
+// jumping marks it in log2(len) rounds: round k, with J = next^(2^k), marks J[p] for every marked
+// p (steps [2^k, 2^(k+1)) from the start) and squares J.  The marked offsets are then parsed in
+// parallel; stream order is the byte offset itself (first error = smallest marked offset whose
+// parse fails, scalar fields = largest marked offset of their tag, vote records ranked by a scan).
+
+// next[p] for p in [0, len]; next[len] = len (the chain's regular end).
+__global__ void __launch_bounds__(TPB) k_huge_next(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
+                                                   uint32_t* __restrict__ next) {
+  const GSrc src{wire};
+  const uint64_t end = base + len;
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x) {
+    if (p == len) {
+      next[p] = len;
+      continue;
+    }
+    uint64_t pos = base + p;
+    uint32_t tag;
+    int wt;
+    int err = rd_key(src, pos, end, tag, wt);
+    if (!err) {
+      if (tag >= 10 && tag <= 19) {  // the same checks as walk_field, without the side effects
+        const bool is_len = tag == 10 || tag == 11 || tag == 13 || tag == 14;
+        if (wt != (is_len ? WT_LEN : WT_VARINT)) {
+          err = HLC_WIRE_WIRE_TYPE_MISMATCH;
+        } else if (is_len) {
+          uint64_t off;
+          uint32_t l;
+          err = rd_len(src, pos, end, off, l);
+        } else {
+          uint64_t v;
+          err = rd_varint(src, pos, end, v);
+        }
+      } else {
+        // A group can run on through every later record when started at a byte inside a record
+        // (quadratic over all offsets): bounded (256 B) here, and an offset whose bounded skip fails is
+        // HUGE_UNRES -- resolved by one lane (k_huge_resolve) only if it is on the chain.
+        const uint64_t lim = wt == WT_SGROUP && end - pos > HUGE_GROUP_SCAN ? pos + HUGE_GROUP_SCAN : end;
+        err = skip_field(wire, pos, lim, wt, tag, RECURSION_LIMIT);
+        if (err && lim < end) err = HUGE_UNRES;
+      }
+    }
+    next[p] = err ? (HUGE_ERR | (uint32_t)err) : (uint32_t)(pos - base);
+  }
+}
+
+// Offsets resolved by k_huge_resolve: fix[0] = count, then (offset, next) pairs.
+__global__ void k_huge_fix(const uint32_t* __restrict__ fix, uint32_t* __restrict__ next) {
+  for (uint32_t i = threadIdx.x; i < fix[0]; i += blockDim.x) next[fix[1 + 2 * i]] = fix[2 + 2 * i];
+}
+
+// The first unresolved offset on the chain (st[11]), parsed by one lane with no bound.
+__global__ void __launch_bounds__(TPB) k_huge_unres(uint32_t len, const uint32_t* __restrict__ next,
+                                                    const uint8_t* __restrict__ mark, uint32_t* st) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < len; p += (uint64_t)gridDim.x * blockDim.x)
+    if (mark[p] && next[p] == (HUGE_ERR | HUGE_UNRES)) atomicMin(st + 11, (uint32_t)p);
+}
+__global__ void k_huge_resolve(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len, const uint32_t* st,
+                               uint32_t* __restrict__ fix) {
+  if (threadIdx.x || blockIdx.x) return;
+  const uint32_t p = st[11];
+  uint64_t pos = base + p;
+  uint32_t tag;
+  int wt;
+  int err = rd_key(GSrc{wire}, pos, base + len, tag, wt);
+  if (!err) err = skip_field(wire, pos, base + len, wt, tag, RECURSION_LIMIT);
+  const uint32_t i = fix[0];
+  fix[1 + 2 * i] = p;
+  fix[2 + 2 * i] = err ? (HUGE_ERR | (uint32_t)err) : (uint32_t)(pos - base);
+  fix[0] = i + 1;
+}
+
+// One pointer-jumping round: marks J[p] for marked p, J1 = J o J.  Concurrent marks within a round
+// only ever add offsets reachable from the start, so the byte stores need no ordering.
+__global__ void __launch_bounds__(TPB) k_huge_round(const uint32_t* __restrict__ J, uint32_t* __restrict__ J1,
+                                                    uint8_t* mark, uint32_t len) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = J[p];
+    if (j < len) {
+      if (mark[p]) mark[j] = 1;
+      J1[p] = J[j];
+    } else {
+      J1[p] = j;
+    }
+  }
+}
+
+// First error in stream order: the smallest marked offset whose field fails (structure, or the
+// name's UTF-8 check).  st[0] = that offset (0xFFFFFFFF if none).
+__global__ void __launch_bounds__(TPB) k_huge_first_error(const uint8_t* __restrict__ wire, uint64_t base,
+                                                          uint32_t len, const uint32_t* __restrict__ next,
+                                                          const uint8_t* __restrict__ mark, uint32_t* st) {
+  const GSrc src{wire};
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < len; p += (uint64_t)gridDim.x * blockDim.x) {
+    if (!mark[p]) continue;
+    if (next[p] >= HUGE_ERR) {
+      atomicMin(st, (uint32_t)p);
+      continue;
+    }
+    uint64_t pos = base + p, off;
+    uint32_t tag, l;
+    int wt;
+    (void)rd_key(src, pos, base + len, tag, wt);  // parsed cleanly by k_huge_next
+    if (tag == 10 && !rd_len(src, pos, base + len, off, l) && !utf8_ok(wire + off, l)) atomicMin(st, (uint32_t)p);
+  }
+}
+
+// Marked fields at or before the first error that parsed: scalars record their last offset (+1)
+// in st[1 + tag - 10]; vote records get flag 1 for the rank scan.  (A name failing UTF-8 is at the
+// error offset and is still assigned, as the serial walker does.)
+__global__ void __launch_bounds__(TPB) k_huge_fields(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
+                                                     const uint32_t* __restrict__ next,
+                                                     const uint8_t* __restrict__ mark, uint32_t* st,
+                                                     uint64_t* __restrict__ flag) {
+  const GSrc src{wire};
+  const uint32_t e = st[0];
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t f = 0;
+    if (p < len && mark[p] && next[p] < HUGE_ERR && p <= e) {
+      uint64_t pos = base + p;
+      uint32_t tag;
+      int wt;
+      (void)rd_key(src, pos, base + len, tag, wt);  // parsed cleanly by k_huge_next
+      if (tag == 14) {
+        f = 1;
+      } else if (tag >= 10 && tag <= 19) {
+        atomicMax(st + 1 + (tag - 10), (uint32_t)p + 1);
+      }
+    }
+    flag[p] = f;
+  }
+}
+
+// Vote records in stream order: rank = exclusive scan of the flags.
+__global__ void __launch_bounds__(TPB) k_huge_records(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
+                                                      const uint64_t* __restrict__ flag,
+                                                      const uint64_t* __restrict__ rank, uint64_t* __restrict__ hoff,
+                                                      uint32_t* __restrict__ hlen) {
+  const GSrc src{wire};
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < len; p += (uint64_t)gridDim.x * blockDim.x) {
+    if (!flag[p]) continue;
+    uint64_t pos = base + p, off;
+    uint32_t tag, l;
+    int wt;
+    (void)rd_key(src, pos, base + len, tag, wt);
+    (void)rd_len(src, pos, base + len, off, l);
+    hoff[rank[p]] = off;
+    hlen[rank[p]] = l;
+  }
+}
+
+// One lane: the winning scalar fields are re-parsed with walk_field, then the same outputs as the
+// serial walker.
+__global__ void k_huge_emit(const uint8_t* __restrict__ wire, uint64_t m, uint64_t base, uint32_t len,
+                            const uint32_t* __restrict__ next, const uint32_t* st, const uint64_t* __restrict__ rank,
+                            uint64_t* __restrict__ vote_count, hlc_wire_proposal* __restrict__ wout,
+                            hlc_proposal* __restrict__ pout, const hlc_scope_config* scope, uint64_t n_scope) {
+  if (threadIdx.x || blockIdx.x) return;
+  const GSrc src{wire};
+  WalkOut o = {};
+  uint32_t dummy = 0;
+  for (int t = 0; t < 10; ++t) {
+    if (t == 4 || !st[1 + t]) continue;
+    uint64_t pos = base + st[1 + t] - 1;
+    (void)walk_field(src, wire, pos, base, base + len, o, dummy, nullptr, nullptr, 0);
+  }
+  const uint32_t e = st[0];
+  int err = HLC_WIRE_OK;
+  if (e != 0xFFFFFFFFu) err = next[e] >= HUGE_ERR ? (int)(next[e] & 0xFFu) : HLC_WIRE_INVALID_UTF8;
+  emit_message(m, o, (uint32_t)rank[len], err, vote_count, wout, pout, scope, n_scope);
+}
+
+// After the vote_begin scan: the huge message's records into place.
+__global__ void __launch_bounds__(TPB) k_huge_place(uint64_t m, const uint64_t* __restrict__ vote_count,
+                                                    const uint64_t* __restrict__ vote_begin,
+                                                    const uint64_t* __restrict__ hoff, const uint32_t* __restrict__ hlen,
+                                                    uint64_t* __restrict__ vrec_off, uint32_t* __restrict__ vrec_len,
+                                                    uint32_t* __restrict__ vrec_msg) {
+  const uint64_t n = vote_count[m], b = vote_begin[m];
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    vrec_off[b + k] = hoff[k];
+    vrec_len[b + k] = hlen[k];
+    vrec_msg[b + k] = (uint32_t)m;
+  }
 }
 
 // Streams the wire bytes once (16-byte loads, grid-stride) so the walker's dependent reads --
@@ -506,11 +723,69 @@ static int is_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
                       uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout, hlc_proposal* pout,
                       const hlc_scope_config* scope, uint64_t n_scope, uint64_t* slab_off, uint32_t* slab_len,
-                      uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, hipStream_t s) {
+                      uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, uint64_t* huge,
+                      hipStream_t s) {
   if (!nm) return;
   hipLaunchKernelGGL(k_wire_walk, dim3((unsigned)((nm + WALK_TPB - 1) / WALK_TPB)), dim3(WALK_TPB), 0, s, mode, wire, is_aligned16(wire), msg_off,
                      msg_len, nm,
                      vote_count, vote_begin, wout, pout, scope, n_scope, slab_off, slab_len, big, vrec_off,
+                     vrec_len, vrec_msg, huge);
+}
+
+uint64_t wire_huge_threshold() { return HUGE_MSG; }
+
+void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
+                        uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
+                        size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
+                        hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
+                        uint32_t* fix, uint32_t max_fix, hipStream_t s) {
+  const unsigned g = (unsigned)std::min<uint64_t>(((uint64_t)len + TPB) / TPB, 8192);
+  auto build_next = [&](uint32_t* dst) {
+    hipLaunchKernelGGL(k_huge_next, dim3(g), dim3(TPB), 0, s, wire, base, len, dst);
+    hipLaunchKernelGGL(k_huge_fix, dim3(1), dim3(TPB), 0, s, fix, dst);
+  };
+  (void)hipMemsetAsync(fix, 0, 4, s);
+  (void)hipMemsetAsync(mark, 0, (size_t)len + 1, s);
+  (void)hipMemsetAsync(mark, 1, 1, s);
+  for (uint32_t nfix = 0;; ++nfix) {
+    build_next(next);
+    uint32_t* a = next;
+    uint32_t* b = jump;
+    for (uint64_t reach = 1; reach <= len; reach <<= 1) {  // after the round, steps < 2 * reach are marked
+      hipLaunchKernelGGL(k_huge_round, dim3(g), dim3(TPB), 0, s, a, b, mark, len);
+      std::swap(a, b);
+    }
+    build_next(next);  // the rounds overwrote it
+    (void)hipMemsetAsync(st + 11, 0xFF, 4, s);
+    hipLaunchKernelGGL(k_huge_unres, dim3(g), dim3(TPB), 0, s, len, next, mark, st);
+    uint32_t u = 0;
+    (void)hipMemcpyAsync(&u, st + 11, 4, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    if (u == 0xFFFFFFFFu || nfix >= max_fix) break;  // (max_fix: the caller's fix capacity)
+    // the marks only grow: the next pass continues the chain from the resolved field
+    hipLaunchKernelGGL(k_huge_resolve, dim3(1), dim3(64), 0, s, wire, base, len, st, fix);
+  }
+  uint32_t* b = next;
+  (void)hipMemsetAsync(st, 0, 11 * 4, s);  // st[11] is the unresolved slot
+  (void)hipMemsetAsync(st, 0xFF, 4, s);
+  hipLaunchKernelGGL(k_huge_first_error, dim3(g), dim3(TPB), 0, s, wire, base, len, b, mark, st);
+  hipLaunchKernelGGL(k_huge_fields, dim3(g), dim3(TPB), 0, s, wire, base, len, b, mark, st, flag);
+  hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, flag, rank, (int)(len + 1), s);
+  hipLaunchKernelGGL(k_huge_records, dim3(g), dim3(TPB), 0, s, wire, base, len, flag, rank, hoff, hlen);
+  hipLaunchKernelGGL(k_huge_emit, dim3(1), dim3(64), 0, s, wire, m, base, len, b, st, rank, vote_count, wout, pout,
+                     scope, n_scope);
+}
+
+size_t huge_scan_bytes(uint32_t len) {
+  size_t tb = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(len + 1));
+  return tb;
+}
+
+void launch_huge_place(uint64_t m, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* hoff,
+                       const uint32_t* hlen, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_huge_place, dim3(2048), dim3(TPB), 0, s, m, vote_count, vote_begin, hoff, hlen, vrec_off,
                      vrec_len, vrec_msg);
 }
 

@@ -284,3 +284,32 @@ def test_gpu_wire_single_large_p2p_proposal(engine):
     b.arena[o1:o1 + 20] = b.arena[o2:o2 + 20]
     res = _wire_vs_oracle(engine, b, w.desc, w.now)
     assert int(res[0]["status"]) != 0 and int(res[0]["bad_index"]) == 15_000
+
+
+def test_gpu_decode_huge_messages_parallel_path(engine):
+    """Messages over 1 MiB (hlc_wire.hip's parallel boundary-discovery path: next[] per byte offset
+    + pointer jumping) == the prost oracle, mixed with small (serially walked) messages: a clean
+    one, scalars repeated after the votes (last wins), an unknown field, a bad UTF-8 name after the
+    votes, a top-level group longer than the bounded per-offset skip, a truncated one, one corrupted mid-records, and one whose huge payload holds no votes."""
+    from wire_fuzz import random_vote
+    from hashgraph_like_consensus.protos import Proposal
+    rnd = random.Random(31)
+    votes = [random_vote(rnd) for _ in range(6000)]
+    base = encode_proposal(Proposal(name="huge", proposal_id=7, votes=votes, expected_voters_count=9000,
+                                    timestamp=5, expiration_timestamp=99, round=2))
+    assert len(base) > (1 << 20)
+    bad_mid = bytearray(base)
+    bad_mid[len(bad_mid) // 2:len(bad_mid) // 2 + 12] = b"\xff" * 12
+    msgs = [
+        encode_proposal(random_proposal(rnd, max_votes=3)),
+        base,
+        base + b"\x52\x03abc" + b"\x60\x2a" + b"\x80\x01\x05",   # name, proposal_id again; tag 16 varint
+        base + b"\x98\x06\x07",                                  # unknown field 99, varint
+        base + b"\x52\x02\xff\xfe",                              # invalid UTF-8 name after the votes
+        base[:-5],                                               # truncated
+        base + b"\xfb\x01\x0a\x80\x02" + bytes(256) + b"\xfc\x01\x60\x2b",  # top-level group > 256 B, then a scalar
+        bytes(bad_mid),
+        encode_proposal(random_proposal(rnd, max_votes=2)),
+        encode_proposal(Proposal(name="p", payload=bytes(rnd.getrandbits(8) for _ in range(1_200_000)))),
+    ]
+    _check_decode(engine, msgs, _scope(1))

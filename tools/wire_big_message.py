@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Decode time of one huge Proposal message (1M vote records) on the device: the block walker
-path for messages above the 128-record slab."""
+"""Decode time of one huge Proposal message (1M vote records) on the device: messages over 1 MiB
+take the parallel boundary-discovery path (next[] per byte offset + pointer jumping)."""
 import json
 import os
 import sys
@@ -22,11 +22,13 @@ def main() -> None:
                received_hash=b"\x22" * 32, vote_hash=b"\x33" * 32, signature=b"\x44" * 65)
     msg = encode_proposal(Proposal(name="big", proposal_id=9, votes=[one] * n, expected_voters_count=n,
                                    timestamp=5, expiration_timestamp=9))
+    print("encoded", len(msg), flush=True)
     eng = Engine(0)
     sc = np.zeros(1, _ffi.SCOPE_CONFIG_DTYPE)
     wire = np.frombuffer(msg, np.uint8)
     off, ln = np.zeros(1, np.uint64), np.array([len(msg)], np.uint32)
     eng.decode_proposals(wire, off, ln, sc)  # warm-up (allocations)
+    print("warm-up done", flush=True)
     t0 = time.perf_counter()
     props, winfo, batch = eng.decode_proposals(wire, off, ln, sc)
     dt = time.perf_counter() - t0
