@@ -101,7 +101,7 @@ struct hlc_ctx {
   // wire decode: staged inputs, walk / record workspace, decoded votes (hlc_votes SoA over the wire bytes)
   DBuf w_wire, w_moff, w_mlen, w_scope, w_vcount, w_vbegin, w_vrec_off, w_vrec_len, w_vrec_msg, w_first_bad,
       w_vote_err, w_props, w_wout, w_res, w_slab_off, w_slab_len, w_big;
-  DBuf w_huge, h_next, h_jump, h_mark, h_st, h_flag, h_rank, h_scan, h_off, h_len, h_fix;
+  DBuf w_huge, h_next, h_jump, h_mark, h_st, h_flag, h_rank, h_scan, h_off, h_len, h_fix, h_save;
   DBuf w_vid, w_pid, w_ts, w_vote, w_foff, w_flen;
   // streaming votes
   DBuf s_vsess, s_sessions, s_owners, s_osess, s_props, s_keys, s_iota, s_order, s_segb, s_sege, s_tab, s_sort_tmp,
@@ -292,8 +292,8 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
   CHK(c->w_huge.ensure(nm * 16 + 16));
   uint64_t nv = 0;
   uint32_t big = 0;
-  // (message index, length) of the messages decoded by the parallel path; only a wire buffer
-  // longer than the threshold can hold one, so other calls skip the extra synchronisation.
+  // (message index, length) of the messages longer than wire_huge_threshold(): decoded by the
+  // parallel boundary-discovery path instead of the walker.
   std::vector<uint64_t> huge;
   constexpr uint32_t kMaxFix = 1u << 16;  // top-level groups longer than 256 B on one huge message's chain
   uint64_t huge_recs = 0;
@@ -304,57 +304,61 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
     hlc::launch_wire_walk(0, wire, moff, mlen, nm, vcount, nullptr, dwout, dprops, scope, n_scope,
                           c->w_slab_off.as<uint64_t>(), c->w_slab_len.as<uint32_t>(), c->w_big.as<uint32_t>(), nullptr,
                           nullptr, nullptr, c->w_huge.as<uint64_t>(), s);
-    if (wire_len > hlc::wire_huge_threshold()) {
-      uint64_t nh = 0;
-      HIPCHK(hipMemcpyAsync(&nh, c->w_huge.p, 8, hipMemcpyDeviceToHost, s));
+    // The huge-message count rides on the vote-total synchronisation; only when a message took the
+    // parallel path (skipped by the walker, vote_count 0 so far) is there a second round trip.
+    auto scan_totals = [&](uint64_t* h) -> int {
+      size_t tb = 0;
+      hlc::launch_exclusive_scan(vcount, vbegin, nm, nullptr, tb, s);
+      CHK(c->scan_tmp.ensure(tb + 16));
+      hlc::launch_exclusive_scan(vcount, vbegin, nm, c->scan_tmp.p, tb, s);
+      HIPCHK(hipMemcpyAsync(h, vbegin + (nm - 1), 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(h + 1, vcount + (nm - 1), 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(h + 2, c->w_big.p, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(h + 3, c->w_huge.p, 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
+      return 0;
+    };
+    uint64_t h[4] = {0, 0, 0, 0};  // last begin, last count, big flag, huge count
+    CHK(scan_totals(h));
+    const uint64_t nh = h[3];
+    if (nh) {
       huge.resize(2 * nh);
-      if (nh) {
-        HIPCHK(hipMemcpyAsync(huge.data(), c->w_huge.as<uint64_t>() + 1, 16 * nh, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-      }
+      HIPCHK(hipMemcpyAsync(huge.data(), c->w_huge.as<uint64_t>() + 1, 16 * nh, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
       uint64_t maxlen = 0;
       for (uint64_t i = 0; i < nh; ++i) {
         maxlen = std::max(maxlen, huge[2 * i + 1]);
         huge_recs += huge[2 * i + 1] / 2 + 1;  // a field takes >= 2 bytes
       }
-      if (nh) {
-        const size_t tb = hlc::huge_scan_bytes((uint32_t)maxlen);
-        CHK(c->h_next.ensure(maxlen * 4 + 16));
-        CHK(c->h_jump.ensure(maxlen * 4 + 16));
-        CHK(c->h_mark.ensure(maxlen + 16));
-        CHK(c->h_st.ensure(64));
-        CHK(c->h_fix.ensure(8 * kMaxFix + 16));
-        CHK(c->h_flag.ensure(maxlen * 8 + 16));
-        CHK(c->h_rank.ensure(maxlen * 8 + 16));
-        CHK(c->h_scan.ensure(tb + 16));
-        CHK(c->h_off.ensure(huge_recs * 8 + 8));
-        CHK(c->h_len.ensure(huge_recs * 4 + 4));
-        std::vector<uint64_t> moff_h(nh);
-        for (uint64_t i = 0; i < nh; ++i)
-          HIPCHK(hipMemcpyAsync(&moff_h[i], moff + huge[2 * i], 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        uint64_t hb = 0;
-        for (uint64_t i = 0; i < nh; ++i) {
-          const uint32_t len = (uint32_t)huge[2 * i + 1];
-          hlc::launch_huge_decode(wire, huge[2 * i], moff_h[i], len, c->h_next.as<uint32_t>(),
-                                  c->h_jump.as<uint32_t>(), c->h_mark.as<uint8_t>(), c->h_st.as<uint32_t>(),
-                                  c->h_flag.as<uint64_t>(), c->h_rank.as<uint64_t>(), c->h_scan.p, tb,
-                                  c->h_off.as<uint64_t>() + hb, c->h_len.as<uint32_t>() + hb, vcount, dwout, dprops,
-                                  scope, n_scope, c->h_fix.as<uint32_t>(), kMaxFix, s);
-          hb += len / 2 + 1;
-        }
+      const size_t tb = hlc::huge_scan_bytes((uint32_t)maxlen);
+      CHK(c->h_next.ensure(maxlen * 4 + 16));
+      CHK(c->h_jump.ensure(maxlen * 4 + 16));
+      CHK(c->h_save.ensure(maxlen * 4 + 16));
+      CHK(c->h_mark.ensure(maxlen + 16));
+      CHK(c->h_st.ensure(64));
+      CHK(c->h_fix.ensure(8 * kMaxFix + 16));
+      CHK(c->h_flag.ensure(maxlen * 8 + 16));
+      CHK(c->h_rank.ensure(maxlen * 8 + 16));
+      CHK(c->h_scan.ensure(tb + 16));
+      CHK(c->h_off.ensure(huge_recs * 8 + 8));
+      CHK(c->h_len.ensure(huge_recs * 4 + 4));
+      std::vector<uint64_t> moff_h(nh);
+      for (uint64_t i = 0; i < nh; ++i)
+        HIPCHK(hipMemcpyAsync(&moff_h[i], moff + huge[2 * i], 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      uint64_t hb = 0;
+      for (uint64_t i = 0; i < nh; ++i) {
+        const uint32_t len = (uint32_t)huge[2 * i + 1];
+        hlc::launch_huge_decode(wire, huge[2 * i], moff_h[i], len, c->h_next.as<uint32_t>(),
+                                c->h_jump.as<uint32_t>(), c->h_save.as<uint32_t>(), c->h_mark.as<uint8_t>(), c->h_st.as<uint32_t>(),
+                                c->h_flag.as<uint64_t>(), c->h_rank.as<uint64_t>(), c->h_scan.p, tb,
+                                c->h_off.as<uint64_t>() + hb, c->h_len.as<uint32_t>() + hb, vcount, dwout, dprops,
+                                scope, n_scope, c->h_fix.as<uint32_t>(), kMaxFix, s);
+        hb += len / 2 + 1;
       }
+      h[0] = h[1] = h[2] = h[3] = 0;
+      CHK(scan_totals(h));
     }
-    size_t tb = 0;
-    hlc::launch_exclusive_scan(vcount, vbegin, nm, nullptr, tb, s);
-    CHK(c->scan_tmp.ensure(tb + 16));
-    hlc::launch_exclusive_scan(vcount, vbegin, nm, c->scan_tmp.p, tb, s);
-    uint64_t h[3] = {0, 0, 0};  // last begin, last count, big flag: one synchronisation
-    HIPCHK(hipMemcpyAsync(h, vbegin + (nm - 1), 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(h + 1, vcount + (nm - 1), 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(h + 2, c->w_big.p, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
     nv = h[0] + h[1];
     big = (uint32_t)h[2];
   }

@@ -97,7 +97,7 @@ void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, co
 uint64_t wire_huge_threshold();
 size_t huge_scan_bytes(uint32_t len);
 void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
-                        uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
+                        uint32_t* save, uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
                         size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
                         hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
                         uint32_t* fix, uint32_t max_fix, hipStream_t s);

@@ -327,6 +327,7 @@ __global__ void __launch_bounds__(WALK_TPB) k_wire_walk(int mode, const uint8_t*
   if (m >= nm) return;
   if (is_huge(msg_len[m])) {  // decoded by the parallel boundary-discovery path instead
     if (mode == 0) {
+      vote_count[m] = 0;  // until launch_huge_decode
       const uint64_t i = atomicAdd((unsigned long long*)huge, 1ull);
       huge[1 + 2 * i] = m;
       huge[2 + 2 * i] = msg_len[m];
@@ -735,7 +736,7 @@ void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, co
 uint64_t wire_huge_threshold() { return HUGE_MSG; }
 
 void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
-                        uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
+                        uint32_t* save, uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
                         size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
                         hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
                         uint32_t* fix, uint32_t max_fix, hipStream_t s) {
@@ -749,15 +750,15 @@ void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t
   (void)hipMemsetAsync(mark, 1, 1, s);
   for (uint32_t nfix = 0;; ++nfix) {
     build_next(next);
+    (void)hipMemcpyAsync(save, next, ((size_t)len + 1) * 4, hipMemcpyDeviceToDevice, s);  // the rounds consume it
     uint32_t* a = next;
     uint32_t* b = jump;
     for (uint64_t reach = 1; reach <= len; reach <<= 1) {  // after the round, steps < 2 * reach are marked
       hipLaunchKernelGGL(k_huge_round, dim3(g), dim3(TPB), 0, s, a, b, mark, len);
       std::swap(a, b);
     }
-    build_next(next);  // the rounds overwrote it
     (void)hipMemsetAsync(st + 11, 0xFF, 4, s);
-    hipLaunchKernelGGL(k_huge_unres, dim3(g), dim3(TPB), 0, s, len, next, mark, st);
+    hipLaunchKernelGGL(k_huge_unres, dim3(g), dim3(TPB), 0, s, len, save, mark, st);
     uint32_t u = 0;
     (void)hipMemcpyAsync(&u, st + 11, 4, hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
@@ -765,12 +766,12 @@ void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t
     // the marks only grow: the next pass continues the chain from the resolved field
     hipLaunchKernelGGL(k_huge_resolve, dim3(1), dim3(64), 0, s, wire, base, len, st, fix);
   }
-  uint32_t* b = next;
+  uint32_t* b = save;
   (void)hipMemsetAsync(st, 0, 11 * 4, s);  // st[11] is the unresolved slot
   (void)hipMemsetAsync(st, 0xFF, 4, s);
   hipLaunchKernelGGL(k_huge_first_error, dim3(g), dim3(TPB), 0, s, wire, base, len, b, mark, st);
   hipLaunchKernelGGL(k_huge_fields, dim3(g), dim3(TPB), 0, s, wire, base, len, b, mark, st, flag);
-  hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, flag, rank, (int)(len + 1), s);
+  (void)hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, flag, rank, (int)(len + 1), s);
   hipLaunchKernelGGL(k_huge_records, dim3(g), dim3(TPB), 0, s, wire, base, len, flag, rank, hoff, hlen);
   hipLaunchKernelGGL(k_huge_emit, dim3(1), dim3(64), 0, s, wire, m, base, len, b, st, rank, vote_count, wout, pout,
                      scope, n_scope);
@@ -778,7 +779,7 @@ void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t
 
 size_t huge_scan_bytes(uint32_t len) {
   size_t tb = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(len + 1));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(len + 1));
   return tb;
 }
 
