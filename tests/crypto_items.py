@@ -1,0 +1,91 @@
+"""Random and adversarial (payload, prehash, signature) items for the crypto pin tests
+(tests/test_openssl_pin.py on the CPU, tests/test_gpu_openssl_pin.py through the C ABI).
+
+Every item is a message signed by EthereumConsensusSigner::sign semantics (RFC 6979, low s,
+v = 27 + parity; /root/reference/src/signing/ethereum.rs:58-64, signed here by the C oracle), then
+optionally mutated into one of the edge classes that /root/reference/src/signing/ethereum.rs:86-89
+must reject or accept (Appendix C of SURVEY.md).  TEST INFRASTRUCTURE ONLY.
+"""
+from __future__ import annotations
+
+import random
+from dataclasses import dataclass
+from typing import List
+
+import numpy as np
+
+import coracle
+import pyoracle as po
+
+KINDS = ["valid", "flip_rs", "bad_v", "eip155_v", "high_s", "r_range", "s_range", "no_point", "infinity"]
+
+
+@dataclass
+class Item:
+    priv: int
+    payload: bytes
+    prehash: bytes
+    sig: bytes
+    kind: str
+
+
+def _no_point_r(rnd: random.Random) -> int:
+    while True:
+        r = rnd.randrange(1, po.N)
+        if po.decompress(r, False) is None:
+            return r
+
+
+def _kg(k: int):
+    """Affine k G (input construction only): OpenSSL when loadable, else the Python oracle."""
+    try:
+        import openssl_ec
+        if openssl_ec.available():
+            e = openssl_ec.Secp256k1()
+            try:
+                pub = e.pubkey(k.to_bytes(32, "big"))
+            finally:
+                e.close()
+            return int.from_bytes(pub[:32], "big"), int.from_bytes(pub[32:], "big")
+    except OSError:
+        pass
+    return po.point_mul(k, po.G)
+
+
+def make_items(n: int, seed: int) -> List[Item]:
+    rnd = random.Random(seed)
+    privs = [rnd.randrange(1, po.N) for _ in range(n)]
+    pays = [bytes(rnd.randrange(256) for _ in range(rnd.randrange(0, 200))) for _ in range(n)]
+    pre = np.stack([np.frombuffer(coracle.eip191_hash(p), np.uint8) for p in pays])
+    keys = np.stack([np.frombuffer(d.to_bytes(32, "big"), np.uint8) for d in privs])
+    sigs = coracle.sign_batch(keys, pre, threads=8)
+    items = []
+    for i in range(n):
+        kind = KINDS[i % len(KINDS)]
+        sig = bytearray(sigs[i].tobytes())
+        z = int.from_bytes(pre[i].tobytes(), "big") % po.N
+        if kind == "flip_rs":
+            sig[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+        elif kind == "bad_v":
+            sig[64] = rnd.choice([2, 3, 26, 29, 30, 34])
+        elif kind == "eip155_v":  # chain-id style v >= 35: parity (v - 35) % 2
+            par = sig[64] - 27
+            sig[64] = 35 + 2 * rnd.randrange(0, 100) + par
+        elif kind == "high_s":  # must still be accepted (alloy normalized_s)
+            s = int.from_bytes(sig[32:64], "big")
+            sig[32:64] = (po.N - s).to_bytes(32, "big")
+            sig[64] = 55 - sig[64]
+        elif kind == "r_range":
+            sig[0:32] = rnd.choice([0, po.N, po.N + 1, 2**256 - 1]).to_bytes(32, "big")
+        elif kind == "s_range":
+            sig[32:64] = rnd.choice([0, po.N, 2**256 - 1, po.N // 2 + 1]).to_bytes(32, "big")
+        elif kind == "no_point":
+            sig[0:32] = _no_point_r(rnd).to_bytes(32, "big")
+        elif kind == "infinity":  # R = kG, s = z / k  =>  Q = r^-1 (s R - z G) = infinity
+            k = rnd.randrange(1, po.N)
+            rx, ry = _kg(k)
+            r = rx % po.N
+            s = z * pow(k, -1, po.N) % po.N or 1
+            sig = bytearray(r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([27 + (ry & 1)]))
+        items.append(Item(privs[i], pays[i], pre[i].tobytes(), bytes(sig), kind))
+    return items
