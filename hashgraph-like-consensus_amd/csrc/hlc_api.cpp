@@ -911,6 +911,32 @@ int hlc_consensus_timeout_batch(hlc_ctx* ctx, uint64_t n, const hlc_session_tall
   return 0;
 }
 
+uint64_t hlc_synth_arena_bytes(uint64_t n_proposals, uint32_t votes_per_proposal) {
+  return hlc::synth_arena_bytes(n_proposals, votes_per_proposal);
+}
+
+int hlc_synth_votes_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_proposal, uint64_t n_proposals,
+                           uint32_t votes_per_proposal, uint32_t expected_voters, int gossipsub,
+                           const hlc_votes* out_votes, hlc_proposal* out_proposals, uint8_t* out_priv, void* stream) {
+  if (!ctx || !out_votes) return set_err(HLC_EINVAL, "NULL argument");
+  const uint64_t n = n_proposals * (uint64_t)votes_per_proposal;
+  if (votes_per_proposal && n / votes_per_proposal != n_proposals) return set_err(HLC_EINVAL, "size overflow");
+  if (out_votes->n != n) return set_err(HLC_EINVAL, "out_votes->n must be n_proposals * votes_per_proposal");
+  if (n && (!out_votes->vote_id || !out_votes->proposal_id || !out_votes->timestamp || !out_votes->vote ||
+            !out_votes->bytes || !out_votes->field_off || !out_votes->field_len || !out_proposals))
+    return set_err(HLC_EINVAL, "NULL output array");
+  if (out_votes->bytes_len < hlc::synth_arena_bytes(n_proposals, votes_per_proposal))
+    return set_err(HLC_EINVAL, "out_votes->bytes smaller than hlc_synth_arena_bytes()");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  CHK(ensure_fbtab(ctx));
+  hlc::launch_synth(seed, start_proposal, n_proposals, votes_per_proposal, expected_voters, gossipsub, out_votes,
+                    out_proposals, out_priv, ctx->fbtab.as<uint32_t>(), s);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int hlc_eth_address_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, uint8_t* out_addr20) {
   if (!ctx || (n && (!priv32 || !out_addr20))) return set_err(HLC_EINVAL, "NULL argument");
   if (!n) return 0;

@@ -140,6 +140,12 @@ void launch_address(uint64_t n, const uint8_t* priv, const uint32_t* fbtab, uint
 void launch_sign(uint64_t n, const uint8_t* priv, const uint32_t* z_digest, const uint32_t* fbtab,
                  uint8_t* sig, hipStream_t s);
 
+// ---- synthetic workload (hlc_synth.hip) ----
+uint64_t synth_arena_bytes(uint64_t n_proposals, uint64_t votes_per_proposal);
+void launch_synth(uint64_t seed, uint64_t start, uint64_t n_proposals, uint32_t votes_per_proposal, uint32_t expected,
+                  int gossipsub, const hlc_votes* out, hlc_proposal* props, uint8_t* priv_out, const uint32_t* fbtab,
+                  hipStream_t s);
+
 constexpr size_t FBTAB_WORDS = 32 * 256 * 16;   // fixed-base comb: 32 windows x 256 affine points
 
 }  // namespace hlc

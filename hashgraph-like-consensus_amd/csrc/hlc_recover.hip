@@ -2,6 +2,7 @@
 // table construction, and the signing side (address derivation, RFC 6979 signing).
 #include "hlc_kernels.h"
 #include "hlc_recover.hpp"
+#include "hlc_sign.hpp"
 
 namespace hlc {
 
@@ -11,33 +12,6 @@ constexpr int REC_TPB = 256;
 #ifndef HLC_REC_WAVES
 #define HLC_REC_WAVES 4  // waves per SIMD the register allocator must admit for k_recover
 #endif
-
-__device__ __forceinline__ uint32_t load_be32(const uint8_t* p) {
-  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
-}
-__device__ __forceinline__ uint32_t load_le32(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-// 32 big-endian bytes -> limbs
-__device__ __forceinline__ void fe_load_be(fe& r, const uint8_t* p) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[7 - i] = load_be32(p + 4 * i);
-}
-__device__ __forceinline__ void fe_store_be(uint8_t* p, const fe& a) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint32_t w = a.v[7 - i];
-    p[4 * i] = (uint8_t)(w >> 24);
-    p[4 * i + 1] = (uint8_t)(w >> 16);
-    p[4 * i + 2] = (uint8_t)(w >> 8);
-    p[4 * i + 3] = (uint8_t)w;
-  }
-}
-// digest stored as 8 memory-order words -> big-endian integer limbs
-__device__ __forceinline__ void fe_from_digest(fe& r, const uint32_t* w) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[7 - i] = bswap32(w[i]);
-}
 
 __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
                                                      const uint8_t* bytes, const uint64_t* sig_off,
@@ -81,17 +55,6 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, 
   }
 }
 
-// k*P for small k by plain double-and-add from the generator (table construction only)
-__device__ void scalar_mul_g(gej& acc, const fe& k) {
-  ge g;
-  ge_generator(g);
-  gej_set_inf(acc);
-  for (int bit = 255; bit >= 0; --bit) {
-    gej_double(acc, acc);
-    if ((k.v[bit >> 5] >> (bit & 31)) & 1u) gej_add_ge(acc, acc, g);
-  }
-}
-
 // fixed-base comb for signing: T[w][j] = j * 2^(8w) * G, affine; j = 0 unused
 __global__ void k_build_fbtab(uint32_t* fb) {
   const int w = blockIdx.x, j = threadIdx.x;
@@ -112,19 +75,6 @@ __global__ void k_build_fbtab(uint32_t* fb) {
   for (int q = 0; q < 8; ++q) {
     fb[(w * 256 + j) * 16 + q] = x.v[q];
     fb[(w * 256 + j) * 16 + 8 + q] = y.v[q];
-  }
-}
-
-// k*G via the 8-bit comb (k < n)
-__device__ void fixed_base_mul(gej& acc, const fe& k, const uint32_t* fb) {
-  gej_set_inf(acc);
-  for (int w = 0; w < 32; ++w) {
-    uint32_t j = (k.v[w >> 2] >> (8 * (w & 3))) & 0xFFu;
-    if (j) {
-      ge g;
-      load_ge_global(g, fb + (size_t)(w * 256 + j) * 16);
-      gej_add_ge(acc, acc, g);
-    }
   }
 }
 
@@ -176,131 +126,14 @@ __global__ void k_address(uint64_t n, const uint8_t* priv, const uint32_t* fb, u
   for (int k = 0; k < 20; ++k) out[20 * i + k] = (uint8_t)(addr[k >> 2] >> (8 * (k & 3)));
 }
 
-// ---- HMAC-SHA256 over short byte strings held in private memory (RFC 6979) ----
-__device__ void sha256_bytes(const uint8_t* pre64, const uint8_t* msg, int len, uint32_t h[8]) {
-  // hashes pre64 (64 bytes, may be null) || msg (len bytes)
-  sha256_init(h);
-  uint32_t w[16];
-  int total = (pre64 ? 64 : 0) + len;
-  if (pre64) {
-    for (int k = 0; k < 16; ++k) w[k] = ((uint32_t)pre64[4 * k] << 24) | ((uint32_t)pre64[4 * k + 1] << 16) |
-                                        ((uint32_t)pre64[4 * k + 2] << 8) | pre64[4 * k + 3];
-    sha256_compress(h, w);
-  }
-  // remaining message with padding
-  int nblk = (len + 9 + 63) / 64;
-  for (int b = 0; b < nblk; ++b) {
-    uint32_t ww[16];
-    for (int k = 0; k < 16; ++k) {
-      uint32_t x = 0;
-      for (int t = 0; t < 4; ++t) {
-        int pos = b * 64 + 4 * k + t;
-        uint8_t byte;
-        if (pos < len) byte = msg[pos];
-        else if (pos == len) byte = 0x80;
-        else byte = 0;
-        x = (x << 8) | byte;
-      }
-      ww[k] = x;
-    }
-    if (b == nblk - 1) {
-      uint64_t bits = (uint64_t)total * 8;
-      ww[14] = (uint32_t)(bits >> 32);
-      ww[15] = (uint32_t)bits;
-    }
-    sha256_compress(h, ww);
-  }
-}
-
-__device__ void hmac_sha256(const uint8_t key[32], const uint8_t* msg, int len, uint8_t out[32]) {
-  uint8_t pad[64];
-  uint32_t ih[8], oh[8];
-  for (int k = 0; k < 64; ++k) pad[k] = (k < 32 ? key[k] : 0) ^ 0x36;
-  sha256_bytes(pad, msg, len, ih);
-  uint8_t inner[32];
-  for (int k = 0; k < 8; ++k) {
-    inner[4 * k] = (uint8_t)(ih[k] >> 24);
-    inner[4 * k + 1] = (uint8_t)(ih[k] >> 16);
-    inner[4 * k + 2] = (uint8_t)(ih[k] >> 8);
-    inner[4 * k + 3] = (uint8_t)ih[k];
-  }
-  for (int k = 0; k < 64; ++k) pad[k] = (k < 32 ? key[k] : 0) ^ 0x5c;
-  sha256_bytes(pad, inner, 32, oh);
-  for (int k = 0; k < 8; ++k) {
-    out[4 * k] = (uint8_t)(oh[k] >> 24);
-    out[4 * k + 1] = (uint8_t)(oh[k] >> 16);
-    out[4 * k + 2] = (uint8_t)(oh[k] >> 8);
-    out[4 * k + 3] = (uint8_t)oh[k];
-  }
-}
-
-// EthereumConsensusSigner::sign (signing/ethereum.rs:58-64) given the EIP-191 prehash:
-// k256 sign_prehash_recoverable = RFC 6979 (HMAC-SHA256) nonce, low-s normalisation,
-// alloy as_bytes() = r || s || (27 + y_parity).
+// EthereumConsensusSigner::sign (signing/ethereum.rs:58-64) given the EIP-191 prehash (hlc_sign.hpp).
 __global__ void k_sign(uint64_t n, const uint8_t* priv, const uint32_t* z_digest, const uint32_t* fb,
                        uint8_t* sig_out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  fe d, zr, z;
+  fe d;
   fe_load_be(d, priv + 32 * i);
-  fe_from_digest(zr, z_digest + 8 * i);
-  sc_reduce(z, zr);
-  uint8_t x[32], h1[32];
-  fe_store_be(x, d);
-  fe_store_be(h1, z);
-  uint8_t V[32], K[32], buf[97];
-  for (int k = 0; k < 32; ++k) {
-    V[k] = 1;
-    K[k] = 0;
-  }
-  for (int step = 0; step < 2; ++step) {
-    for (int k = 0; k < 32; ++k) buf[k] = V[k];
-    buf[32] = (uint8_t)step;
-    for (int k = 0; k < 32; ++k) {
-      buf[33 + k] = x[k];
-      buf[65 + k] = h1[k];
-    }
-    hmac_sha256(K, buf, 97, K);
-    hmac_sha256(K, V, 32, V);
-  }
-  fe k;
-  for (;;) {
-    hmac_sha256(K, V, 32, V);
-    fe_load_be(k, V);
-    if (!fe_is_zero(k) && !sc_is_ge_n(k)) break;
-    for (int q = 0; q < 32; ++q) buf[q] = V[q];
-    buf[32] = 0;
-    hmac_sha256(K, buf, 33, K);
-    hmac_sha256(K, V, 32, V);
-  }
-  gej Rj;
-  fixed_base_mul(Rj, k, fb);
-  fe rx, ry, r;
-  gej_to_affine(rx, ry, Rj);
-  uint32_t y_odd = ry.v[0] & 1u;
-  sc_reduce(r, rx);
-  // s = k^-1 (z + r d) mod n
-  fe r2c, km, kinv, rR, rd, t, s;
-  sc_r2(r2c);
-  sc_mont_mul(km, k, r2c);
-  fe kinv_plain;
-  sc_inv(kinv_plain, k);
-  sc_mont_mul(kinv, kinv_plain, r2c);  // k^-1 * R
-  sc_mont_mul(rR, r, r2c);
-  sc_mont_mul(rd, rR, d);
-  sc_add(t, z, rd);
-  sc_mont_mul(s, kinv, t);
-  fe h;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) h.v[q] = nhalf_limb(q);
-  if (u256_lt(h, s)) {
-    sc_neg(s, s);
-    y_odd ^= 1u;
-  }
-  uint8_t* o = sig_out + 65 * i;
-  fe_store_be(o, r);
-  fe_store_be(o + 32, s);
-  o[64] = (uint8_t)(27 + y_odd);
+  sign_prehash(d, z_digest + 8 * i, fb, sig_out + 65 * i);
 }
 
 inline unsigned blocks_for(uint64_t n, int tpb) { return (unsigned)((n + tpb - 1) / tpb); }

@@ -132,7 +132,7 @@ EXPORTED_SYMBOLS = (
     "hlc_validate_proposals_device", "hlc_eth_address_batch", "hlc_eth_sign_batch",
     "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_consensus_timeout_batch",
     "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
-    "hlc_process_votes", "hlc_process_votes_device",
+    "hlc_process_votes", "hlc_process_votes_device", "hlc_synth_arena_bytes", "hlc_synth_votes_device",
 )
 
 _lib = None
@@ -195,6 +195,11 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_process_votes_device.argtypes = [vp, POINTER(hlc_votes), vp, vp, c_uint64, vp, vp, c_uint64, c_uint64,
                                              vp, vp, vp, vp, vp]
     lib.hlc_process_votes_device.restype = c_int
+    lib.hlc_synth_arena_bytes.argtypes = [c_uint64, c_uint32]
+    lib.hlc_synth_arena_bytes.restype = c_uint64
+    lib.hlc_synth_votes_device.argtypes = [vp, c_uint64, c_uint64, c_uint64, c_uint32, c_uint32, c_int,
+                                           POINTER(hlc_votes), vp, vp, vp]
+    lib.hlc_synth_votes_device.restype = c_int
     lib.hlc_ctx_set_kernel_timing.argtypes = [vp, c_int]
     lib.hlc_ctx_set_kernel_timing.restype = c_int
     lib.hlc_ctx_take_kernel_time.argtypes = [vp, POINTER(ctypes.c_double), u64p, POINTER(ctypes.c_double), u64p]

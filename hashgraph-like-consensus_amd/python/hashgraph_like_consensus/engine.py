@@ -228,8 +228,17 @@ class Engine:
         enqueued on `stream_handle` (a hipStream_t as int; 0 = the context's stream)."""
         _ffi.check(self.lib.hlc_validate_proposals_device(
             self.ctx, ctypes.byref(dbatch.view), dbatch.props_ptr, dbatch.n_proposals, dbatch.now,
-            dbatch.results_ptr, dbatch.status_ptr, dbatch.reason_ptr, None,
+            dbatch.results_ptr, dbatch.status_ptr, dbatch.reason_ptr, dbatch.recovered_ptr,
             c_void_p(stream_handle) if stream_handle else None))
+
+    def synth_votes_device(self, dbatch, seed: int, start_proposal: int, n_proposals: int, votes_per_proposal: int,
+                           expected_voters: int, gossipsub: bool, priv_ptr: int = 0, stream_handle: int = 0) -> None:
+        """hlc_synth_votes_device into a `device.DeviceBatch.allocate`d batch (see
+        DeviceBatch.synthetic)."""
+        _ffi.check(self.lib.hlc_synth_votes_device(
+            self.ctx, seed, start_proposal, n_proposals, votes_per_proposal, expected_voters, 1 if gossipsub else 0,
+            ctypes.byref(dbatch.view), c_void_p(ctypes.cast(dbatch.props_ptr, c_void_p).value),
+            c_void_p(priv_ptr) if priv_ptr else None, c_void_p(stream_handle) if stream_handle else None))
 
     def validate_wire_proposals_device(self, dwire, stream_handle: int = 0) -> None:
         """hlc_validate_wire_proposals_device over a `device.DeviceWire` (wire bytes, message

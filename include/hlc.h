@@ -277,6 +277,21 @@ int hlc_eth_sign_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, const ui
                        uint64_t bytes_len, const uint64_t* payload_off,
                        const uint32_t* payload_len, uint8_t* out_sig65);
 
+/* Synthetic signed-vote workload of SURVEY.md §8d, generated on the device (the same bytes as
+ * python/hashgraph_like_consensus/synth.py): n_proposals chains of votes_per_proposal distinct
+ * voters each, every vote built like `build_vote` (utils.rs:55-98) and signed like
+ * EthereumConsensusSigner::sign (ethereum.rs:58-64), for global proposals
+ * [start_proposal, start_proposal + n_proposals) of the seed -- rank r of a sharded run generates
+ * only its own shard.  Every pointer is DEVICE memory: out_votes->n must be
+ * n_proposals * votes_per_proposal, out_votes->bytes must hold hlc_synth_arena_bytes() bytes;
+ * out_proposals[n_proposals]; out_priv (optional, n * 32) receives the signer keys.
+ * Enqueued on `stream` (NULL: the context's stream) without host synchronisation. */
+uint64_t hlc_synth_arena_bytes(uint64_t n_proposals, uint32_t votes_per_proposal);
+int hlc_synth_votes_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_proposal, uint64_t n_proposals,
+                           uint32_t votes_per_proposal, uint32_t expected_voters, int gossipsub,
+                           const hlc_votes* out_votes, hlc_proposal* out_proposals, uint8_t* out_priv,
+                           void* stream);
+
 /* ---- Streaming votes ---------------------------------------------- */
 
 /* `ConsensusService::process_incoming_vote` (service.rs:286-305) for n votes delivered in

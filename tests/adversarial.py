@@ -56,6 +56,60 @@ def resign(v: po.Vote, priv: int, rehash: bool = True) -> None:
     v.signature = c_sign(priv, v)
 
 
+class _Deferred:
+    """Deferred signing for the mutation pass.  A signature never feeds a vote hash or a signed
+    payload (utils.rs:37-47, 150-152), so every re-sign only records (payload snapshot, key) and
+    one multithreaded C-oracle pass signs them all at the end; signature-level mutations (which
+    read the signature) are queued and applied after it, in order.  The output is byte-identical
+    to signing immediately (tests/test_adversarial_fast.py)."""
+
+    def __init__(self):
+        self.pending = {}   # vote index -> (payload, priv)
+        self.sig_ops = []   # (vote index, op, args) in mutation order
+
+    def resign(self, votes, i: int, priv: int, rehash: bool = True) -> None:
+        v = votes[i]
+        if rehash:
+            v.vote_hash = po.compute_vote_hash(v)
+        v.signature = b""
+        self.pending[i] = (po.signed_payload(v), priv)
+
+    def sign_other(self, votes, i: int, priv: int) -> None:
+        self.pending[i] = (po.signed_payload(votes[i]), priv)
+
+    def flush(self, votes, threads: int = 16, sign_payloads=None) -> None:
+        """sign_payloads(keys u8[m,32], payloads) -> sig u8[m,65] (e.g. the GPU engine's
+        sign_batch); default: the C oracle."""
+        idx = list(self.pending)
+        if idx:
+            keys = np.stack([np.frombuffer(self.pending[i][1].to_bytes(32, "big"), np.uint8) for i in idx])
+            if sign_payloads is not None:
+                sigs = sign_payloads(keys, [self.pending[i][0] for i in idx])
+            else:
+                pre = np.stack([np.frombuffer(coracle.eip191_hash(self.pending[i][0]), np.uint8) for i in idx])
+                sigs = coracle.sign_batch(keys, pre, threads=threads)
+            for k, i in enumerate(idx):
+                votes[i].signature = sigs[k].tobytes()
+        for i, op, arg in self.sig_ops:
+            v = votes[i]
+            s = bytearray(v.signature)
+            if op == "xor":
+                s[arg[0]] ^= arg[1]
+            elif op == "v":
+                s[64] = arg
+            elif op == "high_s":
+                sv = int.from_bytes(s[32:64], "big")
+                s[32:64] = (po.N - sv).to_bytes(32, "big")
+                s[64] = 55 - s[64]
+            elif op == "r":
+                s[0:32] = arg
+            elif op == "set":
+                s = bytearray(arg)
+            elif op == "trunc":
+                s = s[:64] if arg else s + b"\x00"
+            v.signature = bytes(s)
+
+
 _NO_POINT_R = None
 
 
@@ -69,78 +123,78 @@ def no_point_r() -> int:
     return _NO_POINT_R
 
 
-def relink_after(votes: List[po.Vote], privs: List[int], i: int, end: int) -> None:
+def relink_after(votes: List[po.Vote], privs: List[int], i: int, end: int, dfr: "_Deferred") -> None:
     """Re-chain votes i+1 .. end-1 after vote i's hash changed: received_hash -> previous vote,
     then re-hash and re-sign, so the chain stays valid (the mutation's own class surfaces)."""
     for k in range(i + 1, end):
         votes[k].received_hash = votes[k - 1].vote_hash
-        resign(votes[k], privs[k])
+        dfr.resign(votes, k, privs[k])
+
+
+def _kg(k: int):
+    from crypto_items import _kg as kg
+    return kg(k)
 
 
 def mutate(votes: List[po.Vote], privs: List[int], i: int, j: int, kind: str, rnd: random.Random,
-           begin: int, end: int = 0) -> None:
-    """Mutate votes[i] (index j within its proposal [begin, end))."""
+           begin: int, end: int = 0, dfr: "_Deferred" = None) -> None:
+    """Mutate votes[i] (index j within its proposal [begin, end)).  Signing is deferred to
+    dfr.flush() (see _Deferred)."""
+    own = dfr is None
+    if own:
+        dfr = _Deferred()
     v = votes[i]
     priv = privs[i]
     if kind == "wrong_key":
-        v.signature = c_sign(rnd.randrange(1, po.N), v)
+        dfr.sign_other(votes, i, rnd.randrange(1, po.N))
     elif kind == "flip_rs":
-        s = bytearray(v.signature)
-        s[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
-        v.signature = bytes(s)
+        pos = rnd.randrange(64)
+        dfr.sig_ops.append((i, "xor", (pos, 1 << rnd.randrange(8))))
     elif kind == "bad_v":
-        s = bytearray(v.signature)
-        s[64] = rnd.choice([2, 29, 34])
-        v.signature = bytes(s)
+        dfr.sig_ops.append((i, "v", rnd.choice([2, 29, 34])))
     elif kind == "high_s":
-        s = bytearray(v.signature)
-        sv = int.from_bytes(s[32:64], "big")
-        s[32:64] = (po.N - sv).to_bytes(32, "big")
-        s[64] = 55 - s[64]
-        v.signature = bytes(s)
+        dfr.sig_ops.append((i, "high_s", None))
     elif kind == "no_point":
-        s = bytearray(v.signature)
-        s[0:32] = no_point_r().to_bytes(32, "big")
-        v.signature = bytes(s)
+        dfr.sig_ops.append((i, "r", no_point_r().to_bytes(32, "big")))
     elif kind == "infinity":
         z = int.from_bytes(coracle.eip191_hash(po.signed_payload(v)), "big") % po.N
         k = rnd.randrange(1, po.N)
-        R = po.point_mul(k, po.G)
-        r = R[0] % po.N
+        rx, ry = _kg(k)
+        r = rx % po.N
         s = z * pow(k, -1, po.N) % po.N
         if s == 0:
             s = 1
-        v.signature = r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([27 + (R[1] & 1)])
+        dfr.sig_ops.append((i, "set", r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([27 + (ry & 1)])))
     elif kind == "tamper_hash":
         h = bytearray(v.vote_hash)
         h[rnd.randrange(32)] ^= 0x10
         v.vote_hash = bytes(h)
     elif kind == "bad_received":
         v.received_hash = bytes(rnd.randrange(256) for _ in range(32))
-        resign(v, priv)
+        dfr.resign(votes, i, priv)
     elif kind == "parent_other":
         if j >= 2:
             other = votes[begin + rnd.randrange(j - 1)]
             v.parent_hash = other.vote_hash
         else:
             v.parent_hash = bytes(32)
-        resign(v, priv)
+        dfr.resign(votes, i, priv)
     elif kind == "ts_regress":
         v.timestamp = max(votes[i - 1].timestamp - 1, 0) if j > 0 else v.timestamp
-        resign(v, priv)
+        dfr.resign(votes, i, priv)
     elif kind == "ts_old":
         v.timestamp = v.timestamp - 10_000
-        resign(v, priv)
+        dfr.resign(votes, i, priv)
     elif kind == "duplicate":
         if j >= 1:
             src = begin + rnd.randrange(j)
             v.vote_owner = votes[src].vote_owner
             privs[i] = privs[src]
-            resign(v, privs[i])
-            relink_after(votes, privs, i, end)
+            dfr.resign(votes, i, privs[i])
+            relink_after(votes, privs, i, end, dfr)
     elif kind == "wrong_pid":
         v.proposal_id = (v.proposal_id + 1) & 0xFFFFFFFF
-        resign(v, priv)
+        dfr.resign(votes, i, priv)
     elif kind == "empty":
         which = rnd.randrange(3)
         if which == 0:
@@ -148,21 +202,26 @@ def mutate(votes: List[po.Vote], privs: List[int], i: int, j: int, kind: str, rn
         elif which == 1:
             v.vote_hash = b""
         else:
-            v.signature = b""
+            dfr.sig_ops.append((i, "set", b""))
     elif kind == "sig_len":
-        v.signature = v.signature[:64] if rnd.random() < 0.5 else v.signature + b"\x00"
+        dfr.sig_ops.append((i, "trunc", rnd.random() < 0.5))
     else:
         raise ValueError(kind)
+    if own:
+        dfr.flush(votes, threads=1)
 
 
-def byzantine(workload, fraction: float = 1 / 3, seed: int = 5, kinds_pool=None) -> Tuple[object, np.ndarray, List[str]]:
-    """-> (VoteBatch with mutations, desc, per-vote kind or '').  kinds_pool restricts the kinds."""
+def byzantine(workload, fraction: float = 1 / 3, seed: int = 5, kinds_pool=None,
+              sign_payloads=None) -> Tuple[object, np.ndarray, List[str]]:
+    """-> (VoteBatch with mutations, desc, per-vote kind or '').  kinds_pool restricts the kinds;
+    sign_payloads: the re-signing backend (see _Deferred.flush)."""
     pool = list(kinds_pool) if kinds_pool else KINDS
     rnd = random.Random(seed)
     votes = batch_to_votes(workload.batch)
     privs = [int.from_bytes(bytes(k), "big") for k in workload.priv]
     kinds = [""] * len(votes)
     desc = workload.desc
+    dfr = _Deferred()
     k = 0
     for p in range(desc.shape[0]):
         b, c = int(desc[p]["vote_begin"]), int(desc[p]["vote_count"])
@@ -170,8 +229,9 @@ def byzantine(workload, fraction: float = 1 / 3, seed: int = 5, kinds_pool=None)
             if rnd.random() < fraction:
                 kind = pool[k % len(pool)]
                 k += 1
-                mutate(votes, privs, b + j, j, kind, rnd, b, b + c)
+                mutate(votes, privs, b + j, j, kind, rnd, b, b + c, dfr)
                 kinds[b + j] = kind
+    dfr.flush(votes, threads=max(1, min(16, __import__("os").cpu_count() or 1)), sign_payloads=sign_payloads)
     return pack_votes(votes), desc, kinds
 
 

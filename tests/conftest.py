@@ -17,6 +17,10 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def engine():
     from hashgraph_like_consensus.engine import Engine
+    # torch (device-memory plumbing of DeviceBatch) must bring up its HIP runtime before libhlc
+    # creates a context in this process, as bench.py does
+    import torch
+    torch.zeros(1, device="cuda:0")
     eng = Engine(0)
     yield eng
     eng.close()

@@ -36,16 +36,17 @@ def _no_point_r(rnd: random.Random) -> int:
             return r
 
 
+_EC = []
+
+
 def _kg(k: int):
     """Affine k G (input construction only): OpenSSL when loadable, else the Python oracle."""
     try:
         import openssl_ec
-        if openssl_ec.available():
-            e = openssl_ec.Secp256k1()
-            try:
-                pub = e.pubkey(k.to_bytes(32, "big"))
-            finally:
-                e.close()
+        if not _EC and openssl_ec.available():
+            _EC.append(openssl_ec.Secp256k1())
+        if _EC:
+            pub = _EC[0].pubkey(k.to_bytes(32, "big"))
             return int.from_bytes(pub[:32], "big"), int.from_bytes(pub[32:], "big")
     except OSError:
         pass

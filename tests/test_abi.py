@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "hlc.h")
 
 def declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|void|const char\*)\s+(hlc_[a-z0-9_]+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^(?:int|void|uint64_t|const char\*)\s+(hlc_[a-z0-9_]+)\(", text, re.M)))
 
 
 def header_defines():

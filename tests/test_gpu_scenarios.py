@@ -1,9 +1,10 @@
 """GPU parity at scale and on the reference's behavioural cases (C ABI -> HIP kernels vs oracle).
 
-Covers BASELINE.json configs 1, 2, 3 and 5 (config 4 is config 2 sharded over 8 GPUs: the
-same kernel per rank, exercised by bench.py / test_parallel.py):
+Covers BASELINE.json configs 1, 2, 3 and 5 (config 4 -- rank shards of 12.5M votes -- is in
+test_gpu_synth.py):
   * golden fixtures (config 1, the reference's scenarios, a small config-5 mix),
-  * config 5 at 12,800 votes (1/3 Byzantine, every mutation kind),
+  * config 5 at 12,800 votes and at the full config-2 shape, 640,000 votes (1/3 Byzantine,
+    every mutation kind),
   * config 2 at full size (640,000 votes generated + signed on the GPU), bit-exact vs the oracle,
   * config 3: one P2P proposal with 1,000,000 chained votes (chain hash table + tally at scale).
 """
@@ -51,6 +52,25 @@ def test_gpu_config5_byzantine_12800_votes(engine):
     res, vst = compare(engine, batch, desc, w.now, "config5")
     assert len(set(int(s) for s in vst)) >= 9          # every per-vote reject class
     assert (res["status"] != 0).sum() > 150
+
+
+@pytest.mark.timeout(900)
+def test_gpu_config5_byzantine_full_640k(engine):
+    """Config 5 at the full config-2 shape: 10,000 proposals x 64 votes, 1/3 of
+    them mutated over every Byzantine kind, bit-exact against the C oracle for every vote and
+    proposal.  The honest workload is generated on the device, the mutations re-signed by the
+    engine (EthereumConsensusSigner::sign, the C oracle checks the outcome)."""
+    from hashgraph_like_consensus.device import DeviceBatch
+    db = DeviceBatch.synthetic(engine, 10_000, 64, 64, True, synth.config_seed(5), want_priv=True)
+    hb, hd, priv = db.to_host()
+    w = synth.Workload(hb, hd, db.now, priv, "config5")
+    batch, desc, kinds = byzantine(w, fraction=1 / 3, seed=0x484C4305,
+                                   sign_payloads=lambda keys, pays: engine.sign_batch(keys, pays))
+    assert set(k for k in kinds if k) == set(KINDS)
+    assert abs(sum(1 for k in kinds if k) / batch.n - 1 / 3) < 0.01
+    res, vst = compare(engine, batch, desc, w.now, "config5-full")
+    assert len(set(int(s) for s in vst)) >= 9
+    assert (res["status"] != 0).sum() > 9_000
 
 
 def test_gpu_chain_and_duplicate_mutations(engine):
