@@ -7,15 +7,18 @@ synthetic signed votes already resident in HBM: SHA-256 vote-hash recompute, pro
 EIP-191 keccak, secp256k1 ecrecover + address compare, timestamp checks, chain-link hash
 table, duplicate-owner table, per-proposal tally/threshold/round limit.
 
-Workload (the largest single-GPU config of BASELINE.json):
-10,000 proposals x 64 voters (Gossipsub, n = 64) = 640,000 votes per GPU, deterministic,
-generated and signed on the GPU by the engine's own signer (RFC 6979, EthereumConsensusSigner).
-Multi-GPU (torch.distributed.run, one process per GPU, RCCL): every rank validates its own
-proposal shard (weak scaling, no data-path collective); the per-proposal results (16 B each)
-are all-gathered over RCCL once per step, the exchange the north star names.
+Workload at N = 1 (the configuration BASELINE.json's metric is quoted
+on): 10,000 proposals x 64 voters (Gossipsub, n = 64) = 640,000 votes per GPU, deterministic,
+generated and signed on the GPU (hlc_synth_votes_device, bit-identical to synth.py).
+At N > 1 (torch.distributed.run, one process per GPU, RCCL): config 4 -- rank r generates and
+validates its own 1/8 shard of the 100M-vote workload (195,313 proposals x 64 = 12.5M votes), so
+N = 8 is exactly config 4 (weak scaling, no data-path collective).  The one exchange per step is
+the all_gather of the 16-byte per-proposal results plus an all_reduce(sum) of the verified /
+rejected-by-code counters.
 
 cpu_baseline: the C restatement of validate_vote (recover + k256's re-verify, as upstream) on
-the host cores, rank 0 at N = 1 only, on a bounded sample of the same workload.
+every host thread the process may use, one thread, and the two-pass (process_incoming_proposal)
+rate, rank 0 at N = 1 only, on a bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -80,28 +83,69 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(workload, sample_proposals: int) -> dict:
-    """Times the oracle's C restatement (oracle/, the checker) on the host cores."""
+def _cpu_quota():
+    """Host CPUs this process may use: the affinity mask and, when set, the cgroup v2 quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def cpu_baseline(batch, desc, now, sample_proposals: int, single_proposals: int) -> dict:
+    """Times the oracle's C restatement (oracle/, the checker) on the host cores: the reference's
+    per-vote validate_vote (utils.rs:127-171) with k256's recover + re-verify, on every host thread
+    the process may use; the same on one thread; and the process_incoming_proposal-equivalent rate
+    where from_proposal validates every vote twice (session.rs:203, 284-287)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle  # noqa: E402  (test infrastructure; cpu_baseline leg only)
 
-    threads = max(1, min(16, os.cpu_count() or 1))
-    desc = workload.desc[:sample_proposals].copy()
-    votes = int(desc["vote_count"].sum())
-    t0 = time.perf_counter()
-    ok = coracle.validate_votes_only(workload.batch, desc, workload.now, threads, reverify=True)
-    dt = time.perf_counter() - t0
-    assert ok == votes, f"CPU baseline rejected {votes - ok} valid votes"
+    aff, quota = _cpu_quota()
+    # every CPU the process may run on: the affinity mask, capped by the cgroup quota when one is set
+    # (the GPU box grants 16 CPUs of a 256-thread host; 256 threads on 16 CPUs only time-slice --
+    # measured 49.9k votes/s vs 79k with 16 threads, profiles/r02_bench_cpu_threads.txt)
+    threads = max(1, min(aff, int(quota + 0.999))) if quota else aff
+    d_all = desc[:sample_proposals].copy()
+    votes = int(d_all["vote_count"].sum())
+
+    def timed(d, thr, passes=1):
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            ok = coracle.validate_votes_only(batch, d, now, thr, reverify=True)
+            assert ok == int(d["vote_count"].sum()), "CPU baseline rejected valid votes"
+        return time.perf_counter() - t0
+
+    dt = timed(d_all, threads)
+    d1 = desc[:single_proposals].copy()
+    v1 = int(d1["vote_count"].sum())
+    dt1 = timed(d1, 1)
+    dt2 = timed(d_all, threads, passes=2)
     return {
         "value": votes / dt,
         "unit": "votes/s",
         "cores": threads,
+        "cores_note": ("threads = CPUs this process may use (affinity mask capped by the cgroup CPU quota); the "
+                       "single-thread rate below scales the figure to any other core count"),
         "kind": "port",
+        "algorithm": ("C restatement (oracle/hlc_oracle.c): 4x64-bit limbs, Shamir 4-bit fixed windows WITHOUT the "
+                      "GLV endomorphism, Fermat inversions -- k256 0.13 uses GLV, so the reference's own rate on "
+                      "this host would be higher than this port's"),
         "sample": f"{sample_proposals} proposals x {votes // max(sample_proposals, 1)} votes = {votes} votes of the "
                   f"same workload; validate_vote restated in C (SHA-256 + prost + EIP-191 keccak + ecrecover + "
                   f"k256 re-verify + timestamp checks), {threads} threads, {dt:.2f} s wall",
         "cpu_model": cpu_model(),
+        "affinity_cpus": aff,
+        "cgroup_cpu_quota": quota,
         "seconds": dt,
+        "single_thread": {"value": v1 / dt1, "unit": "votes/s", "votes": v1, "seconds": dt1},
+        "two_pass_rate": {"value": votes / dt2, "unit": "proposal votes/s", "votes": votes, "seconds": dt2,
+                          "what": "process_incoming_proposal equivalent: every vote validated twice "
+                                  "(validate_proposal + initialize_with_votes, session.rs:203, 284-287)"},
     }
 
 
@@ -220,14 +264,29 @@ def stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, Device
     }
 
 
+CONFIG4_PROPOSALS = 1_562_500   # 100,000,000 votes = 1,562,500 x 64
+CONFIG4_SHARDS = 8               # sharded by proposal over one 8-GPU node
+
+
+def config4_shard(rank: int):
+    """(first global proposal, count) of rank `rank`'s share of config 4 (8-way split)."""
+    per = -(-CONFIG4_PROPOSALS // CONFIG4_SHARDS)
+    start = min(rank * per, CONFIG4_PROPOSALS)
+    return start, min(per, CONFIG4_PROPOSALS - start)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--proposals", type=int, default=10_000)
+    ap.add_argument("--config", type=int, choices=[2, 4], default=None,
+                    help="2: 10,000 x 64 votes per GPU (default at N=1); 4: this rank's 1/8 shard of the "
+                         "100M-vote config 4, 195,313 x 64 votes (default at N>1)")
+    ap.add_argument("--proposals", type=int, default=None, help="override the per-GPU proposal count")
     ap.add_argument("--votes-per-proposal", type=int, default=64)
     ap.add_argument("--cpu-sample-proposals", type=int, default=10_000)
+    ap.add_argument("--cpu-single-proposals", type=int, default=250)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-bytes leg (device protobuf decode)")
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming process_incoming_vote leg")
@@ -244,34 +303,44 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    else:
-        torch.cuda.set_device(local_rank)
     dev = f"cuda:{local_rank}"
+    config = args.config or (2 if world == 1 else 4)
 
     eng = Engine(local_rank)
-    P, V = args.proposals, args.votes_per_proposal
+    V = args.votes_per_proposal
+    if config == 2:
+        P = args.proposals or 10_000
+        start, seed, max_p = rank * P, synth.config_seed(2), P
+    else:
+        start, P = config4_shard(rank)
+        if args.proposals:
+            P = args.proposals
+            start = rank * P
+        seed, max_p = synth.config_seed(4), max(config4_shard(r)[1] for r in range(max(world, 1)))
+        max_p = max(max_p, P)
+    # the workload is generated and signed on this rank's GPU (hlc_synth_votes_device, the synth.py
+    # spec bit for bit): a rank builds only its own shard and nothing crosses PCIe
     t_gen = time.perf_counter()
-    addr_fn, sign_fn = synth.engine_signers(eng)
-    w = synth.generate(P, V, V, True, synth.config_seed(2), addr_fn, sign_fn, start_proposal=rank * P,
-                       name="config2")
+    db = DeviceBatch.synthetic(eng, P, V, V, True, seed, start_proposal=start, device=dev)
     t_gen = time.perf_counter() - t_gen
-    db = DeviceBatch(w.batch, w.desc, w.now, device=dev)
-    eng.reserve(db.n, P, int(w.batch.arena.size))
+    eng.reserve(db.n, P, db.bytes_len)
     stream = torch.cuda.Stream(device=dev)
     handle = stream.cuda_stream
-    gathered = None
-    if dist is not None:
-        gathered = [torch.empty_like(db.results) for _ in range(world)]
+    # the one exchange step (parallel.ShardExchange): every rank's 16-byte per-proposal
+    # results all-gathered over RCCL plus an all_reduce(sum) of the verified / rejected-by-code
+    # counters; at N = 1 only the local counters
+    from hashgraph_like_consensus.parallel import ShardExchange
+    ex = ShardExchange(max_p, world, dev)
 
     def step():
         eng.validate_proposals_device(db, handle)
         if dist is not None:
             with torch.cuda.stream(stream):
-                dist.all_gather(gathered, db.results)
+                ex(db.results, db.status, P, db.n)
 
     for _ in range(args.warmup):
         step()
@@ -300,12 +369,30 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        nt = torch.tensor([db.n], dtype=torch.int64, device=dev)
+        dist.all_reduce(nt)
+        votes_per_step = int(nt.item())
+    else:
+        votes_per_step = db.n
+    if dist is None:  # one GPU: no exchange; the same counters, computed once outside the timed steps
+        with torch.cuda.stream(stream):
+            ex.local_counters(db.results, db.status, P, db.n)
+        torch.cuda.synchronize()
+    counters = ex.summary()
+    assert counters["verified_votes"] == votes_per_step, "all-reduced verified-vote counter != votes processed"
 
-    votes_total = db.n * world * args.steps
-    value = votes_total / elapsed
+    value = votes_per_step * args.steps / elapsed
     rec_avg_s = rec_ms / max(rec_n, 1) / 1e3
     achieved = W_LIMB_PRODUCTS_PER_VOTE * db.n / rec_avg_s / 1e12
     traffic = pmc_traffic("k_recover")
+    if config == 2:
+        workload = (f"config2: {P} proposals x {V} voters (Gossipsub, n={V}) per GPU, full from_proposal validation"
+                    if (P, V) == (10_000, 64) else
+                    f"config2-shaped: {P} proposals x {V} voters (Gossipsub, n={V}) per GPU, full from_proposal "
+                    f"validation")
+    else:
+        workload = (f"config4: rank shards of the 100M-vote workload (1,562,500 proposals x 64, 8-way split by "
+                    f"proposal_id), {world} rank(s) = {votes_per_step:,} votes per step, full from_proposal validation")
     out = {
         "metric": METRIC,
         "value": value,
@@ -320,15 +407,15 @@ def main() -> int:
         "dtype": "u32",
         "data": "synthetic: deterministic signed votes (SURVEY §8d spec), generated + RFC6979-signed on the GPU",
         "config": {
-            "workload": (f"config2: {P} proposals x {V} voters (Gossipsub, n={V}) per GPU, full from_proposal validation"
-                         if (P, V) == (10_000, 64) else
-                         f"config2-shaped: {P} proposals x {V} voters (Gossipsub, n={V}) per GPU, full from_proposal "
-                         f"validation" + (" (one rank's shard of config 4, 100M votes / 8 GPUs)" if P == 195_313 else "")),
+            "workload": workload,
             "proposals_per_gpu": P,
             "votes_per_proposal": V,
             "votes_per_step_per_gpu": db.n,
-            "parallelism": f"proposal-sharded x{world}" + (", RCCL all_gather of results" if world > 1 else ""),
+            "votes_per_step": votes_per_step,
+            "parallelism": f"proposal-sharded x{world}" + (", RCCL all_gather of results + all_reduce of counters"
+                                                          if world > 1 else ""),
         },
+        "counters_per_step": counters,
         "roofline": {
             "bound": "valu",
             "kernel": "k_recover",
@@ -349,13 +436,19 @@ def main() -> int:
         },
         "gen_seconds": t_gen,
     }
-    if not args.no_wire:
+    need_host = world == 1 and ((not args.no_wire) or (not args.no_stream) or (rank == 0 and not args.no_cpu_baseline))
+    w = None
+    if need_host:
+        hb, hd, _ = db.to_host()
+        w = synth.Workload(hb, hd, db.now, None, "config%d" % config)
+    if w is not None and not args.no_wire:
         out["wire"] = wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire,
                                elapsed / args.steps)
-    if not args.no_stream:
+    if w is not None and not args.no_stream:
         out["stream"] = stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(w, min(args.cpu_sample_proposals, P))
+        out["cpu_baseline"] = cpu_baseline(w.batch, w.desc, w.now, min(args.cpu_sample_proposals, P),
+                                           min(args.cpu_single_proposals, P))
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)

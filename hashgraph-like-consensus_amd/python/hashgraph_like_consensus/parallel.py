@@ -80,32 +80,107 @@ def _gather_rows(rows: np.ndarray, bounds: np.ndarray, rank: int, world: int, gr
     return np.concatenate([out[r][:int(counts[r])].cpu().numpy() for r in range(world)], axis=0)
 
 
+N_CODES = 32  # status histogram width (HLC_* codes are < 32)
+
+
+class ShardExchange:
+    """The one exchange step of a proposal-sharded run, device-resident: every
+    rank's 16-byte per-proposal results are all-gathered (padded to the largest shard) and the
+    outcome counters -- a histogram of per-vote statuses (code 0 = verified) and one of
+    per-proposal statuses -- are all-reduced (sum).  Over RCCL on GPUs (bench.py), gloo on CPU
+    tensors in the tests.  Nothing else crosses ranks: every check is intra-proposal."""
+
+    def __init__(self, max_proposals: int, world: int, device, group=None):
+        import torch
+        self.torch = torch
+        self.group = group
+        self.world = world
+        self.max_p = int(max_proposals)
+        self.send = torch.zeros(max(self.max_p, 1) * 16, dtype=torch.uint8, device=device)
+        self.rows = torch.empty(world * max(self.max_p, 1) * 16, dtype=torch.uint8, device=device)
+        self.counters = torch.zeros(2 * N_CODES, dtype=torch.int64, device=device)
+
+    def local_counters(self, results_u8, status_u8, n_props: int, n_votes: int) -> None:
+        t = self.torch
+        self.counters[:N_CODES] = t.bincount(status_u8[:n_votes], minlength=N_CODES)[:N_CODES]
+        self.counters[N_CODES:] = t.bincount(results_u8[: n_props * 16].view(-1, 16)[:, 0],
+                                             minlength=N_CODES)[:N_CODES]
+
+    def __call__(self, results_u8, status_u8, n_props: int, n_votes: int) -> None:
+        import torch.distributed as dist
+        self.local_counters(results_u8, status_u8, n_props, n_votes)
+        self.send[: n_props * 16].copy_(results_u8[: n_props * 16])
+        if n_props < self.max_p:
+            self.send[n_props * 16:].zero_()
+        dist.all_gather_into_tensor(self.rows, self.send, group=self.group)
+        dist.all_reduce(self.counters, group=self.group)
+
+    def results(self, counts) -> np.ndarray:
+        """The gathered results of every rank in rank order (counts[r] = rank r's proposals)."""
+        rows = self.rows.cpu().numpy().reshape(self.world, -1)
+        return np.concatenate([rows[r, : int(counts[r]) * 16] for r in range(self.world)]).view(_ffi.RESULT_DTYPE)
+
+    def summary(self) -> dict:
+        c = self.counters.cpu().numpy()
+        return {"verified_votes": int(c[0]),
+                "rejected_votes_by_status": {str(k): int(c[k]) for k in range(1, N_CODES) if c[k]},
+                "proposals_ok": int(c[N_CODES]),
+                "proposals_by_status": {str(k): int(c[N_CODES + k]) for k in range(1, N_CODES) if c[N_CODES + k]}}
+
+
+def validate_shard(engine, local: VoteBatch, local_desc: np.ndarray, now: int, group=None,
+                   device: Optional[str] = None, want_votes: bool = False):
+    """Each rank passes ONLY its own shard (its proposals and their votes, generated or loaded by
+    that rank) and receives every rank's per-proposal results in rank order, the all-reduced
+    outcome counters, and (want_votes) every rank's per-vote statuses in rank order."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if device is None:
+        device = "cpu" if dist.get_backend(group) == "gloo" else f"cuda:{torch.cuda.current_device()}"
+    P = int(local_desc.shape[0])
+    n = int(local_desc["vote_count"].astype(np.int64).sum()) if P else 0
+    res, vst, _, _ = engine.validate_proposals(local, local_desc, now, want_votes=True)
+    sizes = torch.tensor([P, n], dtype=torch.int64, device=device)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    counts = np.array([int(x[0]) for x in all_sizes], np.int64)
+    vcounts = np.array([int(x[1]) for x in all_sizes], np.int64)
+    ex = ShardExchange(int(counts.max()) if counts.size else 0, world, device, group)
+    res_t = torch.from_numpy(np.ascontiguousarray(res[:P]).view(np.uint8).reshape(-1).copy()).to(device)
+    # per-vote statuses of the proposals' votes, in proposal order
+    idx = np.concatenate([np.arange(int(d["vote_begin"]), int(d["vote_begin"]) + int(d["vote_count"]),
+                                    dtype=np.int64) for d in local_desc]) if P else np.zeros(0, np.int64)
+    st_local = np.asarray(vst, np.uint8)[idx] if idx.size else np.zeros(0, np.uint8)
+    st_t = torch.from_numpy(st_local.copy()).to(device)
+    ex(res_t, st_t, P, n)
+    full = ex.results(counts).copy()
+    if not want_votes:
+        return full, None, ex.summary()
+    vb = np.concatenate([[0], np.cumsum(vcounts)])
+    vrows = _gather_rows(st_local.reshape(-1, 1), vb, dist.get_rank(group), world, group, device)
+    return full, vrows[:, 0].copy(), ex.summary()
+
+
 def validate_sharded(engine, batch: VoteBatch, desc: np.ndarray, now: int, group=None,
                      device: Optional[str] = None, want_votes: bool = False):
-    """Every rank passes the same (batch, desc); rank r validates its shard on its own engine and
-    all ranks receive the full per-proposal results (and per-vote statuses if `want_votes`),
-    identical to one `engine.validate_proposals` over the whole batch."""
+    """Convenience over validate_shard when every rank holds the same (batch, desc): rank r cuts
+    its shard out and validates only that; all ranks receive the full per-proposal results (and
+    per-vote statuses if `want_votes`), identical to one `engine.validate_proposals` over the
+    whole batch.  At scale, generate or load only the rank's shard and call validate_shard."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if device is None:
-        device = "cpu" if dist.get_backend(group) == "gloo" else f"cuda:{__import__('torch').cuda.current_device()}"
     bounds = shard_bounds(desc, world)
     p0, p1 = int(bounds[rank]), int(bounds[rank + 1])
-    local, sub, idx = slice_shard(batch, desc, p0, p1)
-    res, vst, _, _ = engine.validate_proposals(local, sub, now, want_votes=want_votes)
-    res = np.ascontiguousarray(res[:p1 - p0])
-    rows = _gather_rows(res.view(np.uint8).reshape(-1, _ffi.RESULT_DTYPE.itemsize), bounds, rank, world, group, device)
-    full = rows.reshape(-1).view(_ffi.RESULT_DTYPE).copy()
+    local, sub, _ = slice_shard(batch, desc, p0, p1)
+    full, vst, _ = validate_shard(engine, local, sub, now, group, device, want_votes)
     if not want_votes:
         return full, None
-    vcount = desc["vote_count"].astype(np.int64)
-    vb = np.concatenate([[0], np.cumsum([int(vcount[int(bounds[r]):int(bounds[r + 1])].sum()) for r in range(world)])])
-    vrows = _gather_rows(np.asarray(vst[:idx.size], np.uint8).reshape(-1, 1), vb, rank, world, group, device)
     status = np.full(batch.n, 0xFF, np.uint8)
     all_idx = np.concatenate([np.arange(int(d["vote_begin"]), int(d["vote_begin"]) + int(d["vote_count"]), dtype=np.int64)
                               for d in desc]) if desc.shape[0] else np.zeros(0, np.int64)
-    status[all_idx] = vrows[:, 0]
+    status[all_idx] = vst
     return full, status
 
 

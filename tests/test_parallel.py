@@ -174,3 +174,68 @@ def test_gloo_world2_stream_sharded_equals_single():
                 batch.field_len), vsess, sarr, owners, osess, now)
     for rank, got in _run2("stream", payload):
         assert got == ref, f"rank {rank}: sharded streaming outcomes differ"
+
+
+# ---- per-rank shards: each rank generates only its own proposals (config 4 style) -----------------
+def _shard_workload(rank: int):
+    from adversarial import byzantine
+    w = oracle_workload(4, 6, 8, True, seed=0x484C4304, start=4 * rank)
+    batch, desc, _ = byzantine(w, fraction=0.3, seed=100 + rank)
+    return batch, desc, w.now
+
+
+def _worker_shard(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "hashgraph-like-consensus_amd", "python"),
+              os.path.join(os.path.dirname(here), "oracle"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from hashgraph_like_consensus.parallel import validate_shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        batch, desc, now = _shard_workload(rank)   # this rank's shard only
+        if rank == 1:                               # ragged shards: rank 1 holds one proposal fewer
+            desc = desc[:3].copy()
+        res, st, counters = validate_shard(OracleEngine(), batch, desc, now, want_votes=True)
+        q.put((rank, res.tobytes(), st.tobytes(), counters))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_rank_shards_gather_and_counters():
+    """validate_shard: ranks hold disjoint, self-generated shards (no rank sees the whole batch);
+    everyone receives all results in rank order and the all-reduced verified / rejected counters."""
+    refs, sts = [], []
+    hist_v = np.zeros(32, np.int64)
+    hist_p = np.zeros(32, np.int64)
+    for r in range(2):
+        batch, desc, now = _shard_workload(r)
+        if r == 1:
+            desc = desc[:3].copy()
+        res, vst, _, _ = coracle.validate_proposals(batch, desc, now, threads=2)
+        idx = np.concatenate([np.arange(int(d["vote_begin"]), int(d["vote_begin"]) + int(d["vote_count"]))
+                              for d in desc])
+        refs.append(res.tobytes())
+        sts.append(vst[idx].tobytes())
+        hist_v += np.bincount(vst[idx], minlength=32)[:32]
+        hist_p += np.bincount(res["status"], minlength=32)[:32]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_shard, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res, st, counters in got:
+        assert res == b"".join(refs), f"rank {rank}: gathered results differ"
+        assert st == b"".join(sts), f"rank {rank}: gathered statuses differ"
+        assert counters["verified_votes"] == int(hist_v[0])
+        assert counters["rejected_votes_by_status"] == {str(k): int(hist_v[k]) for k in range(1, 32) if hist_v[k]}
+        assert counters["proposals_ok"] == int(hist_p[0])
+        assert sum(counters["rejected_votes_by_status"].values()) > 0
