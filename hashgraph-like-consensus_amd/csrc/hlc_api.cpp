@@ -101,7 +101,7 @@ struct hlc_ctx {
   // wire decode: staged inputs, walk / record workspace, decoded votes (hlc_votes SoA over the wire bytes)
   DBuf w_wire, w_moff, w_mlen, w_scope, w_vcount, w_vbegin, w_vrec_off, w_vrec_len, w_vrec_msg, w_first_bad,
       w_vote_err, w_props, w_wout, w_res, w_slab_off, w_slab_len, w_big;
-  DBuf w_huge, h_next, h_jump, h_mark, h_st, h_flag, h_rank, h_scan, h_off, h_len, h_fix, h_save;
+  DBuf w_huge, h_next, h_jump, h_mark, h_st, h_flag, h_rank, h_scan, h_off, h_len, h_save;
   DBuf w_vid, w_pid, w_ts, w_vote, w_foff, w_flen;
   // streaming votes
   DBuf s_vsess, s_sessions, s_owners, s_osess, s_props, s_keys, s_iota, s_order, s_segb, s_sege, s_tab, s_sort_tmp,
@@ -186,10 +186,11 @@ int ensure_fbtab(hlc_ctx* c) {
 
 // Per-vote validate_vote stage (utils.rs:127-171; plus the proposal_id match of utils.rs:113-115)
 // for votes already mapped to proposals (vote_prop, NO_PROP = skip): fused LDS prehash, the
-// general path for oversize votes, signature recovery, status assembly.  c->flag must hold the
-// flags of the mapping step (cleared or set by launch_assign_props); *flags receives them.
+// streaming general path for oversize votes (skipped on the device when no vote needs it),
+// signature recovery, status assembly.  c->flag must hold the flags of the mapping step (cleared
+// or set by launch_assign_props).  Everything is enqueued on `s`: no host synchronisation.
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t now,
-               uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* flags, hipStream_t s) {
+               uint8_t* status, uint8_t* reason, uint8_t* drec, hipStream_t s) {
   const uint64_t n = dv->n;
   CHK(c->pre.ensure(n));
   CHK(c->pre_reason.ensure(n));
@@ -197,13 +198,8 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   CHK(c->kec_dig.ensure(n * 32));
   hlc::launch_prehash_fused(dv, n, vote_prop, dprops, c->kec_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
                             c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
-  HIPCHK(hipMemcpyAsync(flags, c->flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  if (*flags & hlc::FLAG_GENERAL_PATH) {  // some votes exceed the LDS window: general global-memory pipeline for those
-    CHK(run_prehash(c, dv, n, hlc::MSG_VOTE, nullptr, nullptr, nullptr, s));
-    hlc::launch_pre_status(dv, n, vote_prop, dprops, c->sha_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
-                           c->pre_reason.as<uint8_t>(), s);
-  }
+  hlc::launch_prehash_stream(dv, n, vote_prop, dprops, c->flag.as<uint32_t>(), c->kec_dig.as<uint32_t>(),
+                             c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
   CHK(ensure_recover_scratch(c));
   if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
   hipEvent_t r0 = nullptr, r1 = nullptr;
@@ -240,7 +236,6 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   CHK(c->flag.ensure(16));
   HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(uint32_t), s));
   hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s);
-  uint32_t flags = hlc::FLAG_LARGE_PROPOSAL;  // without votes nothing was read back: be general
   uint8_t* status = dstatus;
   uint8_t* reason = dreason;
   if (!status) {
@@ -251,20 +246,20 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     CHK(c->reason.ensure(n + 1));
     reason = c->reason.as<uint8_t>();
   }
-  if (n) CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, now, status, reason, drec, &flags, s));
+  if (n) CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, now, status, reason, drec, s));
   CHK(c->chain_code.ensure(n + 1));
   CHK(c->red.ensure(np * 16 + 16));
-  if (flags & hlc::FLAG_LARGE_PROPOSAL) {  // proposals > 512 votes: global chain / duplicate tables
-    uint64_t cap = 64;
-    while (cap < 2 * n) cap <<= 1;
-    CHK(c->chain_tab.ensure(cap * 4));
-    CHK(c->dup_tab.ensure(cap * 4));
-    hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
-                       c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), s);
-    hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
-                            c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
-                            c->red.as<uint32_t>(), np, s);
-  }
+  // proposals > 512 votes use global chain / duplicate tables; the kernels are always enqueued and
+  // do nothing unless k_assign_props raised FLAG_LARGE_PROPOSAL (no host read-back)
+  uint64_t cap = 64;
+  while (cap < 2 * n) cap <<= 1;
+  CHK(c->chain_tab.ensure(cap * 4));
+  CHK(c->dup_tab.ensure(cap * 4));
+  hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
+                     c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->flag.as<uint32_t>(), s);
+  hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
+                          c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
+                          c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
   hlc::launch_chain_small(dv, dprops, np, status, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), s);
   hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
   HIPCHK(hipGetLastError());
@@ -295,7 +290,6 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
   // (message index, length) of the messages longer than wire_huge_threshold(): decoded by the
   // parallel boundary-discovery path instead of the walker.
   std::vector<uint64_t> huge;
-  constexpr uint32_t kMaxFix = 1u << 16;  // top-level groups longer than 256 B on one huge message's chain
   uint64_t huge_recs = 0;
   if (nm) {
     HIPCHK(hipMemsetAsync(c->w_big.p, 0, 4, s));
@@ -336,9 +330,8 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
       CHK(c->h_save.ensure(maxlen * 4 + 16));
       CHK(c->h_mark.ensure(maxlen + 16));
       CHK(c->h_st.ensure(64));
-      CHK(c->h_fix.ensure(8 * kMaxFix + 16));
-      CHK(c->h_flag.ensure(maxlen * 8 + 16));
-      CHK(c->h_rank.ensure(maxlen * 8 + 16));
+      CHK(c->h_flag.ensure(maxlen * 4 + 16));
+      CHK(c->h_rank.ensure(maxlen * 4 + 16));
       CHK(c->h_scan.ensure(tb + 16));
       CHK(c->h_off.ensure(huge_recs * 8 + 8));
       CHK(c->h_len.ensure(huge_recs * 4 + 4));
@@ -349,11 +342,12 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
       uint64_t hb = 0;
       for (uint64_t i = 0; i < nh; ++i) {
         const uint32_t len = (uint32_t)huge[2 * i + 1];
-        hlc::launch_huge_decode(wire, huge[2 * i], moff_h[i], len, c->h_next.as<uint32_t>(),
-                                c->h_jump.as<uint32_t>(), c->h_save.as<uint32_t>(), c->h_mark.as<uint8_t>(), c->h_st.as<uint32_t>(),
-                                c->h_flag.as<uint64_t>(), c->h_rank.as<uint64_t>(), c->h_scan.p, tb,
-                                c->h_off.as<uint64_t>() + hb, c->h_len.as<uint32_t>() + hb, vcount, dwout, dprops,
-                                scope, n_scope, c->h_fix.as<uint32_t>(), kMaxFix, s);
+        if (hlc::launch_huge_decode(wire, huge[2 * i], moff_h[i], len, c->h_next.as<uint32_t>(),
+                                    c->h_jump.as<uint32_t>(), c->h_save.as<uint32_t>(), c->h_mark.as<uint8_t>(),
+                                    c->h_st.as<uint32_t>(), c->h_flag.as<uint32_t>(), c->h_rank.as<uint32_t>(),
+                                    c->h_scan.p, tb, c->h_off.as<uint64_t>() + hb, c->h_len.as<uint32_t>() + hb, vcount,
+                                    dwout, dprops, scope, n_scope, s) != 0)
+          return set_err(HLC_EDEVICE, std::string("huge-message decode: ") + hipGetErrorString(hipGetLastError()));
         hb += len / 2 + 1;
       }
       h[0] = h[1] = h[2] = h[3] = 0;
@@ -733,8 +727,7 @@ int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vses
   }
   CHK(ctx->flag.ensure(16));
   HIPCHK(hipMemsetAsync(ctx->flag.p, 0, sizeof(uint32_t), s));
-  uint32_t flags = 0;
-  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, now, ctx->status.as<uint8_t>(), rs, nullptr, &flags, s));
+  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, now, ctx->status.as<uint8_t>(), rs, nullptr, s));
   // 2. each session's votes in delivery order
   CHK(ctx->s_keys.ensure(n * 4 + 4));
   CHK(ctx->s_iota.ensure(n * 4 + 4));

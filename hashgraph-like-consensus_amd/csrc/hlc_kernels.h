@@ -46,6 +46,11 @@ void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_l
 // messages fit the per-lane LDS window; others get PRE_GENERAL and *general is set non-zero
 void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                           uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason, uint32_t* general, hipStream_t s);
+// general path without host round trips: streams the PRE_GENERAL votes' messages from the arena
+// (SHA-256 compare + EIP-191 keccak + pre-status); exits at once unless *flags has FLAG_GENERAL_PATH
+void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                           const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason,
+                           hipStream_t s);
 // general-path pre-status: decides only the votes marked PRE_GENERAL
 void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                        const uint32_t* sha_digest, uint8_t* pre, uint8_t* pre_reason, hipStream_t s);
@@ -66,11 +71,14 @@ size_t gcomb_words();
 void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         uint64_t now, const uint8_t* pre, const uint8_t* pre_reason, const uint8_t* verify,
                         uint8_t* status, uint8_t* reason, hipStream_t s);
+// large-proposal chain / duplicate tables: always enqueued, skipped on the device unless the call's
+// flag word has FLAG_LARGE_PROPOSAL (flags == nullptr: always run)
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, hipStream_t s);
+                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, const uint32_t* flags, hipStream_t s);
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
-                        uint32_t mask, uint8_t* chain_code, uint32_t* red, uint64_t np, hipStream_t s);
+                        uint32_t mask, uint8_t* chain_code, uint32_t* red, uint64_t np, const uint32_t* flags,
+                        hipStream_t s);
 // batched handle_consensus_timeout: new state + status per session
 void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status, hipStream_t s);
 // proposals with <= 512 votes: chain / duplicate / YES count in LDS, one wave per proposal
@@ -96,11 +104,12 @@ void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, co
 // launch_huge_place moves them to vote_begin[m] after the scan.
 uint64_t wire_huge_threshold();
 size_t huge_scan_bytes(uint32_t len);
-void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
-                        uint32_t* save, uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
-                        size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
-                        hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
-                        uint32_t* fix, uint32_t max_fix, hipStream_t s);
+// returns 0, or -1 when a HIP call failed (the caller reports HLC_EDEVICE)
+int launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
+                       uint32_t* save, uint8_t* mark, uint32_t* st, uint32_t* flag, uint32_t* rank, void* scan_tmp,
+                       size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
+                       hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
+                       hipStream_t s);
 void launch_huge_place(uint64_t m, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* hoff,
                        const uint32_t* hlen, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg,
                        hipStream_t s);

@@ -318,7 +318,8 @@ __device__ void table_insert(uint32_t* tab, uint32_t mask, const hlc_votes& v, c
 }
 
 __global__ void k_tables(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                         uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask) {
+                         uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, const uint32_t* flags) {
+  if (flags && !(*flags & FLAG_LARGE_PROPOSAL)) return;  // every proposal is small: k_chain_small
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t p = vote_prop[i];
@@ -344,7 +345,8 @@ __device__ __forceinline__ uint32_t table_find(const uint32_t* tab, uint32_t mas
 // red layout per proposal: [0] first bad vote (local idx), [1] first chain error, [2] first dup, [3] yes
 __global__ void k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                               const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
-                              uint32_t mask, uint8_t* chain_code, uint32_t* red) {
+                              uint32_t mask, uint8_t* chain_code, uint32_t* red, const uint32_t* flags) {
+  if (flags && !(*flags & FLAG_LARGE_PROPOSAL)) return;  // every proposal is small: k_chain_small
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t p = i < n ? vote_prop[i] : NO_PROP;
   if (p != NO_PROP && props[p].vote_count <= SMALL_CAP) p = NO_PROP;  // small: k_chain_small
@@ -734,6 +736,214 @@ __global__ void __launch_bounds__(FUSED_TPB) k_prehash_fused(hlc_votes v, uint64
   pre_reason[i] = rs;
 }
 
+// ---------------- general path without host round trips ----------------
+// Votes whose messages exceed the fused kernel's LDS window (PRE_GENERAL: long or non-canonical
+// fields) are hashed by streaming their bytes straight from the arena: each message is a short
+// list of segments (inline key / varint / integer bytes, or a field in the arena), read byte by
+// byte into the SHA-256 / keccak blocks with the padding generated on the fly.  No staging
+// buffer, no size scan, no host synchronisation: the kernel is always enqueued and exits at once
+// unless k_prehash_fused raised FLAG_GENERAL_PATH.  One lane per vote; rare and not on the fast
+// path, so it favours simplicity over speed.
+struct Seg {
+  const uint8_t* p;  // arena bytes, or nullptr: the inline bytes
+  uint32_t len;
+  uint8_t inl[12];
+};
+
+struct SegStream {
+  static constexpr int MAXSEG = 24;
+  Seg seg[MAXSEG];
+  int nseg = 0;
+  uint64_t total = 0;
+  int cur = 0;
+  uint32_t off = 0;
+  __device__ void add_inline(const uint8_t* b, int n) {
+    Seg& g = seg[nseg++];
+    g.p = nullptr;
+    g.len = (uint32_t)n;
+    for (int k = 0; k < n; ++k) g.inl[k] = b[k];
+    total += (uint64_t)n;
+  }
+  __device__ void add_bytes(const uint8_t* p, uint32_t n) {
+    if (!n) return;
+    Seg& g = seg[nseg++];
+    g.p = p;
+    g.len = n;
+    total += n;
+  }
+  __device__ void add_le(uint64_t x, int n) {
+    uint8_t b[8];
+    for (int k = 0; k < n; ++k) b[k] = (uint8_t)(x >> (8 * k));
+    add_inline(b, n);
+  }
+  // key (2 bytes) + varint(x)
+  __device__ void add_key_varint(uint8_t k0, uint64_t x) {
+    uint8_t b[12];
+    int n = 0;
+    b[n++] = k0;
+    b[n++] = 0x01;
+    do {
+      const uint8_t c = x & 0x7F;
+      x >>= 7;
+      b[n++] = x ? (uint8_t)(c | 0x80) : c;
+    } while (x);
+    add_inline(b, n);
+  }
+  __device__ void add_decimal(uint64_t x) {
+    uint8_t d[20], b[12];
+    int nd = 0;
+    do {
+      d[nd++] = (uint8_t)('0' + x % 10);
+      x /= 10;
+    } while (x);
+    int n = 0;
+    while (nd && n < 12) b[n++] = d[--nd];
+    add_inline(b, n);
+    if (nd) {  // > 12 digits (never for real lengths): second piece
+      int m = 0;
+      while (nd) b[m++] = d[--nd];
+      add_inline(b, m);
+    }
+  }
+  __device__ void rewind() {
+    cur = 0;
+    off = 0;
+  }
+  // next message byte (caller tracks the position against total)
+  __device__ uint8_t next() {
+    while (cur < nseg && off >= seg[cur].len) {
+      ++cur;
+      off = 0;
+    }
+    const Seg& g = seg[cur];
+    const uint8_t b = g.p ? g.p[off] : g.inl[off];
+    ++off;
+    return b;
+  }
+};
+
+__global__ void k_prehash_stream(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                                 const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason) {
+  if (!(*flags & FLAG_GENERAL_PATH)) return;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (pre[i] != PRE_GENERAL) continue;  // decided by k_prehash_fused
+    // k_prehash_fused only defers votes that passed the proposal_id match and the empty checks
+    const uint32_t lo = flen(v, i, HLC_F_OWNER), lp = flen(v, i, HLC_F_PARENT), lr = flen(v, i, HLC_F_RECEIVED);
+    const uint32_t lh = flen(v, i, HLC_F_VOTE_HASH), ls = flen(v, i, HLC_F_SIGNATURE);
+    const uint32_t id = v.vote_id[i], pid = v.proposal_id[i];
+    const uint64_t ts = v.timestamp[i];
+    uint8_t st = PRE_PENDING, rs = 0;
+    // SHA-256 of compute_vote_hash's input (utils.rs:39-45)
+    SegStream m;
+    m.add_le(id, 4);
+    m.add_bytes(fptr(v, i, HLC_F_OWNER), lo);
+    m.add_le(pid, 4);
+    m.add_le(ts, 8);
+    m.add_le(v.vote[i] ? 1 : 0, 1);
+    m.add_bytes(fptr(v, i, HLC_F_PARENT), lp);
+    m.add_bytes(fptr(v, i, HLC_F_RECEIVED), lr);
+    uint32_t h[8];
+    sha256_init(h);
+    {
+      const uint64_t L = m.total, nb = (L + 9 + 63) / 64;
+      uint64_t pos = 0;
+      for (uint64_t b = 0; b < nb; ++b) {
+        uint32_t w[16];
+        for (int k = 0; k < 16; ++k) {
+          uint32_t x = 0;
+          for (int q = 0; q < 4; ++q, ++pos) {
+            uint8_t c;
+            if (pos < L) c = m.next();
+            else if (pos == L) c = 0x80;
+            else if (pos >= nb * 64 - 8) c = (uint8_t)((L * 8) >> (8 * (nb * 64 - 1 - pos)));
+            else c = 0;
+            x = (x << 8) | c;
+          }
+          w[k] = x;
+        }
+        sha256_compress(h, w);
+      }
+    }
+    bool eq = lh == 32;
+    if (eq) {
+      const uint8_t* hb = fptr(v, i, HLC_F_VOTE_HASH);
+      uint32_t diff = 0;
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t want = (uint32_t)hb[4 * k] << 24 | (uint32_t)hb[4 * k + 1] << 16 |
+                              (uint32_t)hb[4 * k + 2] << 8 | (uint32_t)hb[4 * k + 3];
+        diff |= want ^ h[k];
+      }
+      eq = diff == 0;
+    }
+    if (!eq) {
+      st = HLC_INVALID_VOTE_HASH;
+    } else if (ls != 65) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = HLC_SCHEME_SIG_LEN;
+    } else if (lo != 20) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = HLC_SCHEME_ID_LEN;
+    } else {
+      // keccak256 of the EIP-191 message of the prost encoding, signature cleared (utils.rs:150-152)
+      SegStream k;
+      const uint8_t pfx[12] = {0x19, 'E', 't', 'h', 'e', 'r', 'e', 'u', 'm', ' ', 'S', 'i'};
+      const uint8_t pfx2[12] = {'g', 'n', 'e', 'd', ' ', 'M', 'e', 's', 's', 'a', 'g', 'e'};
+      const uint8_t pfx3[2] = {':', '\n'};
+      k.add_inline(pfx, 12);
+      k.add_inline(pfx2, 12);
+      k.add_inline(pfx3, 2);
+      k.add_decimal(vote_enc_len(v, i));
+      if (id) k.add_key_varint(0xA0, id);
+      k.add_key_varint(0xAA, lo);
+      k.add_bytes(fptr(v, i, HLC_F_OWNER), lo);
+      if (pid) k.add_key_varint(0xB0, pid);
+      if (ts) k.add_key_varint(0xB8, ts);
+      if (v.vote[i]) k.add_key_varint(0xC0, 1);
+      if (lp) { k.add_key_varint(0xCA, lp); k.add_bytes(fptr(v, i, HLC_F_PARENT), lp); }
+      if (lr) { k.add_key_varint(0xD2, lr); k.add_bytes(fptr(v, i, HLC_F_RECEIVED), lr); }
+      k.add_key_varint(0xDA, lh);
+      k.add_bytes(fptr(v, i, HLC_F_VOTE_HASH), lh);
+      uint64_t sk[25];
+      for (int q = 0; q < 25; ++q) sk[q] = 0;
+      const uint64_t L = k.total, nb = L / 136 + 1;
+      uint64_t pos = 0;
+      for (uint64_t b = 0; b < nb; ++b) {
+        for (int q = 0; q < 17; ++q) {
+          uint64_t w = 0;
+          for (int t = 0; t < 8; ++t, ++pos) {
+            uint8_t c;
+            if (pos < L) c = k.next();
+            else c = (pos == L ? 0x01 : 0) | (pos == nb * 136 - 1 ? 0x80 : 0);
+            w |= (uint64_t)c << (8 * t);
+          }
+          sk[q] ^= w;
+        }
+        keccak_f1600(sk);
+      }
+      for (int q = 0; q < 4; ++q) {
+        kec_dig[i * 8 + 2 * q] = (uint32_t)sk[q];
+        kec_dig[i * 8 + 2 * q + 1] = (uint32_t)(sk[q] >> 32);
+      }
+    }
+    pre[i] = st;
+    pre_reason[i] = rs;
+  }
+}
+
+// per-proposal reduction records: first bad / chain / duplicate = none, YES = 0
+__global__ void k_red_init(uint32_t* red, uint64_t np) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < np) reinterpret_cast<uint4*>(red)[p] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
+}
+
+// clears a table when the device flag word has `bit` set (the large-proposal chain tables)
+__global__ void k_clear_if(const uint32_t* flags, uint32_t bit, uint32_t* tab, uint64_t words) {
+  if (!(*flags & bit)) return;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += stride) tab[k] = EMPTY_SLOT;
+}
+
 __global__ void k_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
                              uint8_t* verify_out) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -820,24 +1030,33 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
 }
 
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, hipStream_t s) {
+                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, const uint32_t* flags, hipStream_t s) {
   if (!n) return;
-  hipMemsetAsync(chain_tab, 0xFF, ((size_t)mask + 1) * sizeof(uint32_t), s);
-  hipMemsetAsync(dup_tab, 0xFF, ((size_t)mask + 1) * sizeof(uint32_t), s);
+  const uint64_t words = (uint64_t)mask + 1;
+  const unsigned cb = (unsigned)std::min<uint64_t>((words + TPB - 1) / TPB, 4096);
+  hipLaunchKernelGGL(k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PROPOSAL, chain_tab, words);
+  hipLaunchKernelGGL(k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PROPOSAL, dup_tab, words);
   hipLaunchKernelGGL(k_tables, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, chain_tab, dup_tab,
-                     mask);
+                     mask, flags);
+}
+
+void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+                           const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason,
+                           hipStream_t s) {
+  if (!n) return;
+  const unsigned blocks = (unsigned)std::min<uint64_t>(blocks_for(n), 1024);
+  hipLaunchKernelGGL(k_prehash_stream, dim3(blocks), dim3(TPB), 0, s, *v, n, vote_prop, props, flags, kec_dig, pre,
+                     pre_reason);
 }
 
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab, uint32_t mask,
-                        uint8_t* chain_code, uint32_t* red, uint64_t np, hipStream_t s) {
+                        uint8_t* chain_code, uint32_t* red, uint64_t np, const uint32_t* flags, hipStream_t s) {
   if (!np) return;
-  hipMemsetAsync(red, 0xFF, np * 4 * sizeof(uint32_t), s);
-  // yes counters start at zero: clear word 3 of each record with a strided memset kernel-free pass
-  hipMemset2DAsync(red + 3, 4 * sizeof(uint32_t), 0, sizeof(uint32_t), np, s);
+  hipLaunchKernelGGL(k_red_init, dim3((unsigned)((np + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np);
   if (n)
     hipLaunchKernelGGL(k_chain_check, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, status,
-                       chain_tab, dup_tab, mask, chain_code, red);
+                       chain_tab, dup_tab, mask, chain_code, red, flags);
 }
 
 void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status,

@@ -205,14 +205,16 @@ struct WalkOut {
   uint32_t name_len, payload_len, owner_len;
 };
 
-constexpr uint32_t SLAB = 128;
+constexpr uint32_t SLAB = 128;  // vote records a walker keeps per message before the vote count is known
 // Messages longer than this are not walked by one lane (about 1 us per field) but by the parallel
-// boundary-discovery path below.  Lengths >= HUGE_ERR cannot be encoded in its next[] array.
+// boundary-discovery path below.  Its next[] array encodes offsets below HUGE_ERR and its scans
+// count items in an int, so messages of 2^31 - 2 bytes or more stay with the (slow, exact) walker.
 constexpr uint32_t HUGE_MSG = 1u << 20;
+constexpr uint32_t HUGE_MAX = 0x7FFFFFFEu;
 constexpr uint32_t HUGE_ERR = 0xFFFFFF00u;
-constexpr uint32_t HUGE_UNRES = 0xFFu;  // not a prost error code
+constexpr uint32_t HUGE_UNRES = 0xFFu;  // internal marker, never reported (not a prost error code)
 constexpr uint64_t HUGE_GROUP_SCAN = 256;
-__host__ __device__ __forceinline__ bool is_huge(uint32_t len) { return len > HUGE_MSG && len < HUGE_ERR; }   // vote records a walker keeps per message before the vote count is known
+__host__ __device__ __forceinline__ bool is_huge(uint32_t len) { return len > HUGE_MSG && len < HUGE_MAX; }
 
 // Loads wire[wlo, whi) (wlo 16-byte aligned) into LDS with the calling block's threads.
 __device__ __forceinline__ void load_window(uint8_t* lds, const uint8_t* __restrict__ wire, uint64_t wlo,
@@ -380,70 +382,70 @@ __global__ void __launch_bounds__(WALK_TPB) k_wire_walk(int mode, const uint8_t*
 // parallel; stream order is the byte offset itself (first error = smallest marked offset whose
 // parse fails, scalar fields = largest marked offset of their tag, vote records ranked by a scan).
 
+// The candidate top-level field at offset p: the offset just past it, or HUGE_ERR | error code.
+// bounded: a group is scanned at most HUGE_GROUP_SCAN bytes (HUGE_UNRES beyond), since a group
+// started at a byte inside a record can run on through every later record -- quadratic over all
+// offsets.  Unbounded (the tail walk below), it is exactly walk_field's structure check.
+__device__ __forceinline__ uint32_t huge_parse(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
+                                               uint64_t p, bool bounded) {
+  const GSrc src{wire};
+  const uint64_t end = base + len;
+  uint64_t pos = base + p;
+  uint32_t tag;
+  int wt;
+  int err = rd_key(src, pos, end, tag, wt);
+  if (!err) {
+    if (tag >= 10 && tag <= 19) {  // the same checks as walk_field, without the side effects
+      const bool is_len = tag == 10 || tag == 11 || tag == 13 || tag == 14;
+      if (wt != (is_len ? WT_LEN : WT_VARINT)) {
+        err = HLC_WIRE_WIRE_TYPE_MISMATCH;
+      } else if (is_len) {
+        uint64_t off;
+        uint32_t l;
+        err = rd_len(src, pos, end, off, l);
+      } else {
+        uint64_t v;
+        err = rd_varint(src, pos, end, v);
+      }
+    } else {
+      const uint64_t lim = bounded && wt == WT_SGROUP && end - pos > HUGE_GROUP_SCAN ? pos + HUGE_GROUP_SCAN : end;
+      err = skip_field(wire, pos, lim, wt, tag, RECURSION_LIMIT);
+      if (err && lim < end) err = HUGE_UNRES;
+    }
+  }
+  return err ? (HUGE_ERR | (uint32_t)err) : (uint32_t)(pos - base);
+}
+
 // next[p] for p in [0, len]; next[len] = len (the chain's regular end).
 __global__ void __launch_bounds__(TPB) k_huge_next(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
                                                    uint32_t* __restrict__ next) {
-  const GSrc src{wire};
-  const uint64_t end = base + len;
-  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x) {
-    if (p == len) {
-      next[p] = len;
-      continue;
-    }
-    uint64_t pos = base + p;
-    uint32_t tag;
-    int wt;
-    int err = rd_key(src, pos, end, tag, wt);
-    if (!err) {
-      if (tag >= 10 && tag <= 19) {  // the same checks as walk_field, without the side effects
-        const bool is_len = tag == 10 || tag == 11 || tag == 13 || tag == 14;
-        if (wt != (is_len ? WT_LEN : WT_VARINT)) {
-          err = HLC_WIRE_WIRE_TYPE_MISMATCH;
-        } else if (is_len) {
-          uint64_t off;
-          uint32_t l;
-          err = rd_len(src, pos, end, off, l);
-        } else {
-          uint64_t v;
-          err = rd_varint(src, pos, end, v);
-        }
-      } else {
-        // A group can run on through every later record when started at a byte inside a record
-        // (quadratic over all offsets): bounded (256 B) here, and an offset whose bounded skip fails is
-        // HUGE_UNRES -- resolved by one lane (k_huge_resolve) only if it is on the chain.
-        const uint64_t lim = wt == WT_SGROUP && end - pos > HUGE_GROUP_SCAN ? pos + HUGE_GROUP_SCAN : end;
-        err = skip_field(wire, pos, lim, wt, tag, RECURSION_LIMIT);
-        if (err && lim < end) err = HUGE_UNRES;
-      }
-    }
-    next[p] = err ? (HUGE_ERR | (uint32_t)err) : (uint32_t)(pos - base);
-  }
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x)
+    next[p] = p == len ? len : huge_parse(wire, base, len, p, true);
 }
 
-// Offsets resolved by k_huge_resolve: fix[0] = count, then (offset, next) pairs.
-__global__ void k_huge_fix(const uint32_t* __restrict__ fix, uint32_t* __restrict__ next) {
-  for (uint32_t i = threadIdx.x; i < fix[0]; i += blockDim.x) next[fix[1 + 2 * i]] = fix[2 + 2 * i];
-}
-
-// The first unresolved offset on the chain (st[11]), parsed by one lane with no bound.
+// The first unresolved offset on the chain (st[11], 0xFFFFFFFF if none).  The chain stops there
+// (its next[] is an error code), so no offset after it is marked.
 __global__ void __launch_bounds__(TPB) k_huge_unres(uint32_t len, const uint32_t* __restrict__ next,
                                                     const uint8_t* __restrict__ mark, uint32_t* st) {
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < len; p += (uint64_t)gridDim.x * blockDim.x)
     if (mark[p] && next[p] == (HUGE_ERR | HUGE_UNRES)) atomicMin(st + 11, (uint32_t)p);
 }
-__global__ void k_huge_resolve(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len, const uint32_t* st,
-                               uint32_t* __restrict__ fix) {
+
+// From the first unresolved offset on, one lane walks the rest of the top-level fields with
+// unbounded group skips, writing their next[] entries and marks: linear in the message, however
+// many long top-level groups it holds, with no host round trip (a no-op when st[11] is unset).
+__global__ void k_huge_tail(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len, uint32_t* __restrict__ next,
+                            uint8_t* __restrict__ mark, const uint32_t* st) {
   if (threadIdx.x || blockIdx.x) return;
-  const uint32_t p = st[11];
-  uint64_t pos = base + p;
-  uint32_t tag;
-  int wt;
-  int err = rd_key(GSrc{wire}, pos, base + len, tag, wt);
-  if (!err) err = skip_field(wire, pos, base + len, wt, tag, RECURSION_LIMIT);
-  const uint32_t i = fix[0];
-  fix[1 + 2 * i] = p;
-  fix[2 + 2 * i] = err ? (HUGE_ERR | (uint32_t)err) : (uint32_t)(pos - base);
-  fix[0] = i + 1;
+  uint32_t p = st[11];
+  if (p == 0xFFFFFFFFu) return;
+  while (p < len) {
+    const uint32_t q = huge_parse(wire, base, len, p, false);
+    next[p] = q;
+    mark[p] = 1;
+    if (q >= HUGE_ERR) break;
+    p = q;
+  }
 }
 
 // One pointer-jumping round: marks J[p] for marked p, J1 = J o J.  Concurrent marks within a round
@@ -487,11 +489,11 @@ __global__ void __launch_bounds__(TPB) k_huge_first_error(const uint8_t* __restr
 __global__ void __launch_bounds__(TPB) k_huge_fields(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
                                                      const uint32_t* __restrict__ next,
                                                      const uint8_t* __restrict__ mark, uint32_t* st,
-                                                     uint64_t* __restrict__ flag) {
+                                                     uint32_t* __restrict__ flag) {
   const GSrc src{wire};
   const uint32_t e = st[0];
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t f = 0;
+    uint32_t f = 0;
     if (p < len && mark[p] && next[p] < HUGE_ERR && p <= e) {
       uint64_t pos = base + p;
       uint32_t tag;
@@ -509,8 +511,8 @@ __global__ void __launch_bounds__(TPB) k_huge_fields(const uint8_t* __restrict__
 
 // Vote records in stream order: rank = exclusive scan of the flags.
 __global__ void __launch_bounds__(TPB) k_huge_records(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
-                                                      const uint64_t* __restrict__ flag,
-                                                      const uint64_t* __restrict__ rank, uint64_t* __restrict__ hoff,
+                                                      const uint32_t* __restrict__ flag,
+                                                      const uint32_t* __restrict__ rank, uint64_t* __restrict__ hoff,
                                                       uint32_t* __restrict__ hlen) {
   const GSrc src{wire};
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < len; p += (uint64_t)gridDim.x * blockDim.x) {
@@ -528,7 +530,7 @@ __global__ void __launch_bounds__(TPB) k_huge_records(const uint8_t* __restrict_
 // One lane: the winning scalar fields are re-parsed with walk_field, then the same outputs as the
 // serial walker.
 __global__ void k_huge_emit(const uint8_t* __restrict__ wire, uint64_t m, uint64_t base, uint32_t len,
-                            const uint32_t* __restrict__ next, const uint32_t* st, const uint64_t* __restrict__ rank,
+                            const uint32_t* __restrict__ next, const uint32_t* st, const uint32_t* __restrict__ rank,
                             uint64_t* __restrict__ vote_count, hlc_wire_proposal* __restrict__ wout,
                             hlc_proposal* __restrict__ pout, const hlc_scope_config* scope, uint64_t n_scope) {
   if (threadIdx.x || blockIdx.x) return;
@@ -735,51 +737,46 @@ void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, co
 
 uint64_t wire_huge_threshold() { return HUGE_MSG; }
 
-void launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
-                        uint32_t* save, uint8_t* mark, uint32_t* st, uint64_t* flag, uint64_t* rank, void* scan_tmp,
-                        size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
-                        hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
-                        uint32_t* fix, uint32_t max_fix, hipStream_t s) {
+int launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t len, uint32_t* next, uint32_t* jump,
+                       uint32_t* save, uint8_t* mark, uint32_t* st, uint32_t* flag, uint32_t* rank, void* scan_tmp,
+                       size_t scan_bytes, uint64_t* hoff, uint32_t* hlen, uint64_t* vote_count,
+                       hlc_wire_proposal* wout, hlc_proposal* pout, const hlc_scope_config* scope, uint64_t n_scope,
+                       hipStream_t s) {
+#define HUGE_CHK(x)                     \
+  do {                                  \
+    if ((x) != hipSuccess) return -1;   \
+  } while (0)
   const unsigned g = (unsigned)std::min<uint64_t>(((uint64_t)len + TPB) / TPB, 8192);
-  auto build_next = [&](uint32_t* dst) {
-    hipLaunchKernelGGL(k_huge_next, dim3(g), dim3(TPB), 0, s, wire, base, len, dst);
-    hipLaunchKernelGGL(k_huge_fix, dim3(1), dim3(TPB), 0, s, fix, dst);
-  };
-  (void)hipMemsetAsync(fix, 0, 4, s);
-  (void)hipMemsetAsync(mark, 0, (size_t)len + 1, s);
-  (void)hipMemsetAsync(mark, 1, 1, s);
-  for (uint32_t nfix = 0;; ++nfix) {
-    build_next(next);
-    (void)hipMemcpyAsync(save, next, ((size_t)len + 1) * 4, hipMemcpyDeviceToDevice, s);  // the rounds consume it
-    uint32_t* a = next;
-    uint32_t* b = jump;
-    for (uint64_t reach = 1; reach <= len; reach <<= 1) {  // after the round, steps < 2 * reach are marked
-      hipLaunchKernelGGL(k_huge_round, dim3(g), dim3(TPB), 0, s, a, b, mark, len);
-      std::swap(a, b);
-    }
-    (void)hipMemsetAsync(st + 11, 0xFF, 4, s);
-    hipLaunchKernelGGL(k_huge_unres, dim3(g), dim3(TPB), 0, s, len, save, mark, st);
-    uint32_t u = 0;
-    (void)hipMemcpyAsync(&u, st + 11, 4, hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    if (u == 0xFFFFFFFFu || nfix >= max_fix) break;  // (max_fix: the caller's fix capacity)
-    // the marks only grow: the next pass continues the chain from the resolved field
-    hipLaunchKernelGGL(k_huge_resolve, dim3(1), dim3(64), 0, s, wire, base, len, st, fix);
+  HUGE_CHK(hipMemsetAsync(mark, 0, (size_t)len + 1, s));
+  HUGE_CHK(hipMemsetAsync(mark, 1, 1, s));
+  hipLaunchKernelGGL(k_huge_next, dim3(g), dim3(TPB), 0, s, wire, base, len, next);
+  HUGE_CHK(hipMemcpyAsync(save, next, ((size_t)len + 1) * 4, hipMemcpyDeviceToDevice, s));  // the rounds consume it
+  uint32_t* a = next;
+  uint32_t* b = jump;
+  for (uint64_t reach = 1; reach <= len; reach <<= 1) {  // after the round, steps < 2 * reach are marked
+    hipLaunchKernelGGL(k_huge_round, dim3(g), dim3(TPB), 0, s, a, b, mark, len);
+    std::swap(a, b);
   }
-  uint32_t* b = save;
-  (void)hipMemsetAsync(st, 0, 11 * 4, s);  // st[11] is the unresolved slot
-  (void)hipMemsetAsync(st, 0xFF, 4, s);
-  hipLaunchKernelGGL(k_huge_first_error, dim3(g), dim3(TPB), 0, s, wire, base, len, b, mark, st);
-  hipLaunchKernelGGL(k_huge_fields, dim3(g), dim3(TPB), 0, s, wire, base, len, b, mark, st, flag);
-  (void)hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, flag, rank, (int)(len + 1), s);
+  // a long top-level group on the chain: one lane finishes the chain from there (linear)
+  HUGE_CHK(hipMemsetAsync(st + 11, 0xFF, 4, s));
+  hipLaunchKernelGGL(k_huge_unres, dim3(g), dim3(TPB), 0, s, len, save, mark, st);
+  hipLaunchKernelGGL(k_huge_tail, dim3(1), dim3(64), 0, s, wire, base, len, save, mark, st);
+  HUGE_CHK(hipMemsetAsync(st, 0, 11 * 4, s));  // st[11] is the unresolved slot
+  HUGE_CHK(hipMemsetAsync(st, 0xFF, 4, s));
+  hipLaunchKernelGGL(k_huge_first_error, dim3(g), dim3(TPB), 0, s, wire, base, len, save, mark, st);
+  hipLaunchKernelGGL(k_huge_fields, dim3(g), dim3(TPB), 0, s, wire, base, len, save, mark, st, flag);
+  HUGE_CHK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, flag, rank, (int)(len + 1), s));
   hipLaunchKernelGGL(k_huge_records, dim3(g), dim3(TPB), 0, s, wire, base, len, flag, rank, hoff, hlen);
-  hipLaunchKernelGGL(k_huge_emit, dim3(1), dim3(64), 0, s, wire, m, base, len, b, st, rank, vote_count, wout, pout,
+  hipLaunchKernelGGL(k_huge_emit, dim3(1), dim3(64), 0, s, wire, m, base, len, save, st, rank, vote_count, wout, pout,
                      scope, n_scope);
+  HUGE_CHK(hipGetLastError());
+#undef HUGE_CHK
+  return 0;
 }
 
 size_t huge_scan_bytes(uint32_t len) {
   size_t tb = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(len + 1));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)(len + 1));
   return tb;
 }
 

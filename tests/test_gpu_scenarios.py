@@ -99,8 +99,13 @@ def test_gpu_config2_full_size_bit_exact(engine):
 
 @pytest.mark.timeout(420)
 def test_gpu_config3_million_vote_chain(engine):
+    from hashgraph_like_consensus.device import DeviceBatch
     n = 1_000_000
-    w = synth.generate(1, n, 1_500_000, False, synth.config_seed(3), *synth.engine_signers(engine))
+    # generated on the device (bit-identical to synth.generate, tests/test_gpu_synth.py)
+    db = DeviceBatch.synthetic(engine, 1, n, 1_500_000, False, synth.config_seed(3), want_priv=True)
+    hb, hd, priv = db.to_host()
+    del db
+    w = synth.Workload(hb, hd, synth.NOW, priv, "config3")
     res, vst = compare(engine, w.batch, w.desc, w.now, "config3")
     assert int(res[0]["status"]) == 0 and int(res[0]["total"]) == n
     # The mutated runs below are checked by property (one oracle pass over 1M votes is enough):
@@ -144,3 +149,49 @@ def test_gpu_edge_batches(engine):
     # votes not covered by any proposal are ignored; a proposal over a sub-range still validates
     d2 = w.desc[1:2].copy()
     compare(engine, w.batch, d2, w.now, "subrange")
+
+
+def test_gpu_general_path_random_lengths(engine):
+    """Votes with random, mostly non-canonical field lengths (0-600 bytes), zero / small / large
+    ids and timestamps: most exceed the fused kernel's LDS window and take the streaming general
+    path (k_prehash_stream), which must equal the oracle on every vote -- including re-signed
+    votes that reach recovery and succeed."""
+    import random
+    import pyoracle as po
+    from adversarial import c_sign
+    from hashgraph_like_consensus.batch import pack_votes
+    from hashgraph_like_consensus import _ffi
+    rnd = random.Random(0x6E4)
+    votes, desc = [], []
+    T0 = synth.T0
+    for p in range(40):
+        pid = rnd.choice([0, 1, 300, 2**31 + 5, 2**32 - 1])
+        b = len(votes)
+        for j in range(rnd.randrange(1, 9)):
+            d = rnd.randrange(1, po.N)
+            lo = rnd.choice([20, 20, 20, 0, 19, 21, 200])
+            owner = po.privkey_to_address(d) if lo == 20 and rnd.random() < 0.7 else bytes(rnd.randrange(256) for _ in range(lo))
+            v = po.Vote(vote_id=rnd.choice([0, 7, 2**31 + 1]), vote_owner=owner, proposal_id=pid,
+                        timestamp=rnd.choice([T0 + 1, T0 + 10, 0, 2**40]), vote=rnd.random() < 0.5,
+                        parent_hash=bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 0, 32, 100, 600]))),
+                        received_hash=bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 32, 64, 300]))))
+            v.vote_hash = po.compute_vote_hash(v) if rnd.random() < 0.9 else bytes(32)
+            if rnd.random() < 0.2:
+                v.vote_hash = v.vote_hash + b"\x01" * rnd.randrange(1, 200)
+            v.signature = c_sign(d, v) if rnd.random() < 0.9 else bytes(rnd.randrange(256) for _ in range(65))
+            votes.append(v)
+        desc.append((b, len(votes) - b, pid))
+    batch = pack_votes(votes)
+    dd = np.zeros(len(desc), dtype=_ffi.PROPOSAL_DTYPE)
+    for k, (b, c, pid) in enumerate(desc):
+        dd[k]["vote_begin"], dd[k]["vote_count"], dd[k]["proposal_id"] = b, c, pid
+    dd["timestamp"] = T0
+    dd["expiration_timestamp"] = T0 + 3600
+    dd["expected_voters_count"] = 16
+    dd["max_rounds"] = 2
+    dd["consensus_threshold"] = 2.0 / 3.0
+    dd["use_gossipsub_rounds"] = 1
+    dd["liveness_criteria_yes"] = 1
+    res, vst = compare(engine, batch, dd, synth.NOW, "general-path")
+    got = set(int(x) for x in vst)
+    assert {0, 6, 7}.issubset(got), got   # some pass, some hash mismatches, some scheme errors

@@ -313,3 +313,26 @@ def test_gpu_decode_huge_messages_parallel_path(engine):
         encode_proposal(Proposal(name="p", payload=bytes(rnd.getrandbits(8) for _ in range(1_200_000)))),
     ]
     _check_decode(engine, msgs, _scope(1))
+
+
+def test_gpu_decode_huge_message_many_long_groups(engine):
+    """Thousands of top-level unknown groups longer than the bounded per-offset skip (256 B) in
+    messages over 1 MiB: the chain stops at the first one and a single lane finishes the walk
+    (k_huge_tail), linear in the message -- the outcome must equal the prost oracle, including
+    votes and scalars after the groups, an unterminated group, and an error after them."""
+    from wire_fuzz import random_vote
+    from hashgraph_like_consensus.protos import Proposal
+    rnd = random.Random(37)
+    grp = b"\xfb\x01\x0a\x90\x02" + bytes(272) + b"\xfc\x01"          # group (field 31) holding a 272-B blob
+    votes = [random_vote(rnd) for _ in range(300)]
+    head = encode_proposal(Proposal(name="g", proposal_id=9, votes=votes[:150], expected_voters_count=400))
+    tail = encode_proposal(Proposal(votes=votes[150:], timestamp=11, expiration_timestamp=77))
+    many = head + grp * 4000 + tail + b"\x60\x2c"                    # > 1 MiB, 4000 groups, then a scalar
+    assert len(many) > (1 << 20)
+    msgs = [
+        many,
+        head + grp * 4000 + b"\xfb\x01\x0a\x02ab",                 # unterminated group at the end
+        head + grp * 3000 + b"\x60\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\x01" + tail,  # bad varint after groups
+        encode_proposal(random_proposal(rnd, max_votes=2)),
+    ]
+    _check_decode(engine, msgs, _scope(1))
