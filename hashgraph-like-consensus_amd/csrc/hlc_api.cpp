@@ -69,7 +69,7 @@ struct hlc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DBuf gtab, fbtab, rec_scratch;
+  DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
@@ -201,6 +201,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   hlc::launch_prehash_stream(dv, n, vote_prop, dprops, c->flag.as<uint32_t>(), c->kec_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
   CHK(ensure_recover_scratch(c));
+  CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
   hipEvent_t r0 = nullptr, r1 = nullptr;
   if (c->timing) {
@@ -210,7 +211,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   }
   hlc::launch_recover(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_SIGNATURE,
                       dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(),
-                      c->rec_lanes, c->verify.as<uint8_t>(), drec, s);
+                      c->rec_lanes, c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s);
   if (c->timing) {
     HIPCHK(hipEventRecord(r1, s));
     c->rec_ev.emplace_back(r0, r1);
@@ -512,6 +513,7 @@ int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, ui
   CHK(activate(ctx));
   const uint64_t n = max_votes;
   CHK(ensure_recover_scratch(ctx));
+  CHK(ctx->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   for (DBuf* b : {&ctx->sha_sz, &ctx->sha_off, &ctx->kec_sz, &ctx->kec_off}) CHK(b->ensure(n * 8));
   for (DBuf* b : {&ctx->sha_dig, &ctx->kec_dig}) CHK(b->ensure(n * 32));
   for (DBuf* b : {&ctx->pre, &ctx->pre_reason, &ctx->verify, &ctx->status, &ctx->reason, &ctx->chain_code})
@@ -875,9 +877,10 @@ int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_
     drec = ctx->out_rec.as<uint8_t>();
     HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
   }
+  CHK(ctx->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   hlc::launch_recover(n, ctx->pre.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), dbytes, ctx->in_off3.as<uint64_t>(),
                       ctx->in_off.as<uint64_t>(), 1, ctx->gtab.as<uint32_t>(), ctx->rec_scratch.as<uint32_t>(),
-                      ctx->rec_lanes, ctx->verify.as<uint8_t>(), drec, s);
+                      ctx->rec_lanes, ctx->rec_work.as<uint32_t>(), ctx->verify.as<uint8_t>(), drec, s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_status, ctx->verify.p, n, hipMemcpyDeviceToHost, s));
   if (out_addr) HIPCHK(hipMemcpyAsync(out_addr, drec, n * 20, hipMemcpyDeviceToHost, s));

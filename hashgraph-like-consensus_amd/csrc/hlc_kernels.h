@@ -58,12 +58,15 @@ void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop
 // ---- recovery ----
 // items: i in [0, n) with pre[i] == PRE_PENDING; signature bytes / identity bytes read from
 // bytes + sig_off[i*stride_f] etc.  verify_out[i]: HLC_VERIFY_TRUE/FALSE or 1+SCHEME.
+// three kernels (hlc_recover.hpp): k_rec_prep, k_rec_main, k_rec_final; `work` holds
+// recover_work_words(n) words of per-vote records for the call
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                     const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride,
-                    const uint32_t* gtab, uint32_t* scratch, uint64_t scratch_lanes,
+                    const uint32_t* gtab, uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work,
                     uint8_t* verify_out, uint8_t* addr_out, hipStream_t s);
 uint64_t recover_grid_lanes();
-uint64_t recover_scratch_words();  // per-lane workspace words of k_recover
+uint64_t recover_scratch_words();  // per-lane workspace words of k_rec_main
+uint64_t recover_work_words(uint64_t n);
 void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s);  // needs fbtab
 size_t gcomb_words();
 

@@ -13,43 +13,136 @@ constexpr int REC_TPB = 256;
 #define HLC_REC_WAVES 4  // waves per SIMD the register allocator must admit for k_recover
 #endif
 
-__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
-                                                     const uint8_t* bytes, const uint64_t* sig_off,
-                                                     const uint64_t* id_off, size_t off_stride,
-                                                     const uint32_t* gcomb, uint32_t* scratch, uint64_t lanes,
-                                                     uint8_t* verify_out, uint8_t* addr_out) {
+// ---- prep: parse + batched r^-1 + scalars (REC_BATCH votes per lane, one safegcd) ----
+// Lane t owns votes t + k * L (k < REC_BATCH): a wave reads 64 consecutive votes per k.
+// Forward: acc_k = mont(acc_{k-1}, r_k) = (prod r) R^-k over the lane's valid votes, each acc_{k-1}
+// kept in `pfx`; one inversion cur = acc^-1; backward: r_k^-1 = mont(acc_{k-1}, cur),
+// cur = mont(cur, r_k).  Invalid votes multiply nothing (their state is final already).
+constexpr int PREP_TPB = 64;
+
+__global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, const uint8_t* pre,
+                                                       const uint32_t* z_digest, const uint8_t* bytes,
+                                                       const uint64_t* sig_off, size_t off_stride, uint8_t* state,
+                                                       uint32_t* rec, uint32_t* pfx) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L) return;
+  fe acc;
+  fe_set(acc, 1);
+#pragma unroll 1
+  for (int k = 0; k < REC_BATCH; ++k) {
+    const uint64_t i = t + (uint64_t)k * L;
+    if (i >= n) break;
+    if (pre && pre[i] != PRE_PENDING) continue;  // not recovered: state untouched (may hold a caller code)
+    const uint8_t* sig = bytes + sig_off[i * off_stride];
+    fe r, s;
+    fe_load_be(r, sig);
+    fe_load_be(s, sig + 32);
+    int parity;
+    const int code = rec_parse(s, r, sig[64], parity);
+    if (code != SCHEME_NONE) {
+      state[i] = (uint8_t)(1 + code);
+      continue;
+    }
+    state[i] = REC_PENDING;
+    store_fe_ws(acc, pfx + (size_t)k * 8 * L + t, L);
+    sc_mont_mul(acc, acc, r);
+  }
+  fe cur;
+  sc_inv(cur, acc);
+#pragma unroll 1
+  for (int k = REC_BATCH - 1; k >= 0; --k) {
+    const uint64_t i = t + (uint64_t)k * L;
+    if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
+    const uint8_t* sig = bytes + sig_off[i * off_stride];
+    fe r, s, z, prev, rinv;
+    fe_load_be(r, sig);
+    fe_load_be(s, sig + 32);
+    int parity;
+    (void)rec_parse(s, r, sig[64], parity);
+    load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
+    sc_mont_mul(rinv, prev, cur);  // r_k^-1
+    sc_mont_mul(cur, cur, r);      // acc_{k-1}^-1
+    fe_from_digest(z, z_digest + 8 * i);
+    rec_prep_scalars(z, s, rinv, parity, rec + i, n);
+  }
+}
+
+// ---- main: decompress + u1 G + u2 R, one vote per lane at a time (persistent grid) ----
+__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n, const uint8_t* pre, const uint8_t* bytes,
+                                                                     const uint64_t* sig_off, size_t off_stride,
+                                                                     const uint32_t* gcomb, uint32_t* scratch,
+                                                                     uint64_t lanes, uint8_t* state,
+                                                                     const uint32_t* rec, uint32_t* q) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
   uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tid * RTAB_WORDS;
   for (uint64_t i = tid; i < n; i += lanes) {
-    if (pre && pre[i] != PRE_PENDING) continue;
-    const uint8_t* sig = bytes + sig_off[i * off_stride];
-    fe r, s, z;
-    fe_load_be(r, sig);
-    fe_load_be(s, sig + 32);
-    fe_from_digest(z, z_digest + 8 * i);
-    uint32_t addr[5];
-    int code = ecrecover_lane(z, r, s, sig[64], addr, gcomb, ws, lanes, tab);
-    uint8_t vr;
+    if ((pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
+    fe r;
+    fe_load_be(r, bytes + sig_off[i * off_stride]);
+    gej acc;
+    const int code = rec_main(r, rec + i, n, acc, gcomb, ws, lanes, tab);
     if (code != SCHEME_NONE) {
-      vr = (uint8_t)(1 + code);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) addr[k] = 0;
-    } else {
-      const uint8_t* id = bytes + id_off[i * off_stride];
-      uint32_t diff = 0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) diff |= addr[k] ^ load_le32(id + 4 * k);
-      vr = diff == 0 ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
+      state[i] = (uint8_t)(1 + code);
+      continue;
     }
-    verify_out[i] = vr;
+    store_fe_ws(acc.x, q + i, n);
+    store_fe_ws(acc.y, q + (size_t)8 * n + i, n);
+    store_fe_ws(acc.z, q + (size_t)16 * n + i, n);
+  }
+}
+
+// ---- final: batched Z^-1 (one safegcd per REC_BATCH votes), affine, keccak, owner compare ----
+__global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, const uint8_t* pre, const uint8_t* bytes,
+                                                        const uint64_t* id_off, size_t off_stride, uint8_t* state,
+                                                        const uint32_t* q, uint32_t* pfx, uint8_t* addr_out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L) return;
+  fe acc;
+  fe_set(acc, 1);
+#pragma unroll 1
+  for (int k = 0; k < REC_BATCH; ++k) {
+    const uint64_t i = t + (uint64_t)k * L;
+    if (i >= n) break;
+    if ((pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
+    fe z;
+    load_fe_ws(z, q + (size_t)16 * n + i, n);
+    store_fe_ws(acc, pfx + (size_t)k * 8 * L + t, L);
+    fe_mul(acc, acc, z);
+  }
+  fe cur;
+  fe_inv(cur, acc);
+#pragma unroll 1
+  for (int k = REC_BATCH - 1; k >= 0; --k) {
+    const uint64_t i = t + (uint64_t)k * L;
+    if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
+    fe x, y, z, prev, zi, zi2, zi3;
+    load_fe_ws(x, q + i, n);
+    load_fe_ws(y, q + (size_t)8 * n + i, n);
+    load_fe_ws(z, q + (size_t)16 * n + i, n);
+    load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
+    fe_mul(zi, prev, cur);  // Z_k^-1
+    fe_mul(cur, cur, z);
+    fe_sqr(zi2, zi);
+    fe_mul(zi3, zi2, zi);
+    fe_mul(x, x, zi2);
+    fe_mul(y, y, zi3);
+    fe_normalize(x, x);
+    fe_normalize(y, y);
+    uint32_t addr[5];
+    pubkey_address(x, y, addr);
+    const uint8_t* id = bytes + id_off[i * off_stride];
+    uint32_t diff = 0;
+#pragma unroll
+    for (int w = 0; w < 5; ++w) diff |= addr[w] ^ load_le32(id + 4 * w);
+    state[i] = diff == 0 ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
     if (addr_out) {
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        addr_out[20 * i + 4 * k] = (uint8_t)addr[k];
-        addr_out[20 * i + 4 * k + 1] = (uint8_t)(addr[k] >> 8);
-        addr_out[20 * i + 4 * k + 2] = (uint8_t)(addr[k] >> 16);
-        addr_out[20 * i + 4 * k + 3] = (uint8_t)(addr[k] >> 24);
+      for (int w = 0; w < 5; ++w) {
+        addr_out[20 * i + 4 * w] = (uint8_t)addr[w];
+        addr_out[20 * i + 4 * w + 1] = (uint8_t)(addr[w] >> 8);
+        addr_out[20 * i + 4 * w + 2] = (uint8_t)(addr[w] >> 16);
+        addr_out[20 * i + 4 * w + 3] = (uint8_t)(addr[w] >> 24);
       }
     }
   }
@@ -142,25 +235,39 @@ inline unsigned blocks_for(uint64_t n, int tpb) { return (unsigned)((n + tpb - 1
 
 uint64_t recover_scratch_words() { return SCRATCH_WORDS; }
 
+uint64_t recover_work_words(uint64_t n) {
+  const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH;
+  return n * (uint64_t)(REC_WORDS + Q_WORDS) + L * REC_BATCH * 8 + 64;
+}
+
 uint64_t recover_grid_lanes() {
   int dev = 0, cus = 256, per_cu = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_recover, REC_TPB, 0) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rec_main, REC_TPB, 0) != hipSuccess || per_cu < 1)
     per_cu = 2;
   return (uint64_t)cus * (uint64_t)per_cu * REC_TPB;
 }
 
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                     const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb,
-                    uint32_t* scratch, uint64_t scratch_lanes, uint8_t* verify_out, uint8_t* addr_out,
+                    uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, uint8_t* verify_out, uint8_t* addr_out,
                     hipStream_t s) {
   if (!n) return;
+  uint32_t* rec = work;
+  uint32_t* q = rec + n * (uint64_t)REC_WORDS;
+  uint32_t* pfx = q + n * (uint64_t)Q_WORDS;
+  const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH;
+  const unsigned pb = (unsigned)((L + PREP_TPB - 1) / PREP_TPB);
+  hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, L, pre, z_digest, bytes, sig_off, off_stride,
+                     verify_out, rec, pfx);
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (n + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
-  hipLaunchKernelGGL(k_recover, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, z_digest, bytes, sig_off,
-                     id_off, off_stride, gcomb, scratch, (uint64_t)blocks * REC_TPB, verify_out, addr_out);
+  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, bytes, sig_off, off_stride, gcomb,
+                     scratch, (uint64_t)blocks * REC_TPB, verify_out, rec, q);
+  hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, L, pre, bytes, id_off, off_stride, verify_out, q, pfx,
+                     addr_out);
 }
 
 void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s) {

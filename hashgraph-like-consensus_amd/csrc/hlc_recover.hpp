@@ -1,4 +1,5 @@
-// hlc_recover.hpp -- per-lane secp256k1 public-key recovery (ecrecover).
+// hlc_recover.hpp -- secp256k1 public-key recovery (ecrecover) for a batch of votes, in three
+// stages (hlc_recover.hip: k_rec_prep, k_rec_main, k_rec_final).
 //
 // Restates, bit-exactly, `Signature::from_raw_array(sig)?.recover_address_from_msg(payload)`
 // of alloy-primitives 1.6.0 on top of k256 0.13.4 `VerifyingKey::recover_from_prehash`
@@ -9,11 +10,24 @@
 // k256's post-recovery verify_prehash always succeeds on a recovered key (it re-derives R)
 // and is therefore not repeated.
 //
-// Scalar multiplication Q = u1 G + u2 R, in two independent parts:
+// Stages (one lane per vote in the main stage; REC_BATCH votes per lane in the other two):
+//   prep : v / s / range checks, then r^-1 mod n for REC_BATCH votes with ONE inversion
+//          (Montgomery's trick: prefix products forward, one safegcd, a backward sweep), u1, u2,
+//          the GLV split of u2 and its regular signed digits -> a per-vote record in HBM;
+//   main : R = decompress(r) (square root), the R table, the u2 R chain, the u1 G comb and the
+//          final addition -> Jacobian Q in HBM (the VALU-bound bulk, ~97% of the work);
+//   final: Z^-1 mod p for REC_BATCH votes with one inversion (the same trick), affine Q,
+//          keccak address, owner compare.
+// In SIMT a per-lane inversion already costs the wave ONE instruction stream for 64 values, so
+// a cross-lane (DPP / ds_swizzle) prefix-product scan only adds multiplications and saves no issue
+// slots; the inversion count per wave only drops when each lane folds several of its own values
+// into one inversion -- which is what the batch does (measured in DESIGN.md §4.1).
+//
+// Scalar multiplication Q = u1 G + u2 R (main stage), in two independent parts:
 //   u2 R: GLV endomorphism (lambda, beta) splits u2 into 128-bit halves b1 + b2 lambda; one
 //       doubling chain of 125 steps adds, every 5 bits, one odd multiple of R and one of
 //       lambda R ("regular" signed digits: every lane adds at the same positions).  The 16
-//       odd multiples 1..31 R live per lane in a lane-interleaved HBM/L2 workspace.  The R
+//       odd multiples 1..31 R live per lane in a lane-contiguous HBM/L2 workspace.  The R
 //       table is built on the isomorphic curve y^2 = x^3 + 7 C^6 (C = Z(2R)) and brought to one
 //       common Z ("effective affine", as libsecp256k1's ecmult_odd_multiples_table +
 //       ge_table_set_globalz), so every chain addition is one mixed Jacobian+affine add.
@@ -23,7 +37,6 @@
 //       recoding's top digit is provably 1, so window 16 is the constant start point 2^256 G.
 //       16 mixed additions, each table entry prefetched one window ahead.
 //   Q = (u2 R) + (u1 G) with one Jacobian addition (exceptional cases exact).
-// Inversions (r^-1 mod n, final Z^-1 mod p) use safegcd divsteps (hlc_modinv.hpp).
 #pragma once
 #include "hlc_hash.hpp"
 #include "hlc_point.hpp"
@@ -39,17 +52,25 @@ constexpr int M_R = 26;                         // windows: 26 * 5 = 130 >= 129 
 constexpr int TOP_BIT = W_R * (M_R - 1);        // first (most significant) chain position: 125
 constexpr int RTAB_N = 1 << (W_R - 1);          // 16 odd multiples 1..31 (per lane)
 constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
-// Per-lane workspace, two regions:
+// Per-lane workspace of the main stage (persistent grid):
 //  * lane-interleaved (word w of lane t at w * lanes + t: every lane touches the same word, so
-//    each access is one coalesced 256-B row per wave): the signed digits and the z-ratios;
+//    each access is one coalesced 256-B row per wave): the z-ratios of the table build;
 //  * per-lane contiguous R table (RTAB_WORDS words, 64-B entries read by 16-B vector loads):
 //    entries are gathered at lane-dependent indices, so each lane's entry must be one block.
 constexpr int RTAB_WORDS = RTAB_N * 16;         // per lane (affine, common-Z frame)
-constexpr int DIG_OFF = 0;                      // digits: b1, b2 (R, lambda R)
-constexpr int DIG_WORDS = 2 * DIG_R_WORDS;
-constexpr int ZR_OFF = DIG_OFF + DIG_WORDS;     // z-ratios of the table build
+constexpr int ZR_OFF = 0;                       // z-ratios of the table build
 constexpr int IL_WORDS = ZR_OFF + 8 * (RTAB_N - 1);       // interleaved words per lane
 constexpr int SCRATCH_WORDS = IL_WORDS + RTAB_WORDS;      // per lane workspace words
+
+// Per-vote records between the stages, word-major (word w of vote i at w * n + i: a wave's 64
+// consecutive votes read one coalesced 256-B row per word).
+constexpr int REC_U1 = 0;                       // 8 words: odd representative of u1
+constexpr int REC_DIG = 8;                      // 2 x DIG_R_WORDS: int16 digit pairs of b1, b2
+constexpr int REC_FLAGS = REC_DIG + 2 * DIG_R_WORDS;  // bit 0-1 negs, 2-3 skews, 4 neg_g, 5 parity
+constexpr int REC_WORDS = REC_FLAGS + 1;
+constexpr int Q_WORDS = 24;                     // main -> final: Jacobian X, Y, Z
+constexpr int REC_BATCH = 8;                    // votes per lane (one inversion) in prep / final
+constexpr uint8_t REC_PENDING = 0xFF;           // verify_out state between the stages
 
 // fixed-base comb for u1 G (global memory, built once per context by k_build_gcomb)
 constexpr int GC_W = 16;                        // bits per window
@@ -315,33 +336,67 @@ HLC_DEV void pubkey_address(const fe& x, const fe& y, uint32_t addr[5]) {
   addr[4] = (uint32_t)(st[3] >> 32);
 }
 
-// Full recovery for one lane.  gcomb: the fixed-base comb table (global).  ws: this lane's
-// interleaved workspace column base, stride = total lanes; tab: this lane's R table.
-// Returns SCHEME_* (0 on success and addr filled).
-HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr[5],
-                           const uint32_t* gcomb, uint32_t* ws, size_t stride, uint32_t* tab) {
-  // alloy normalize_v
-  int parity;
+// alloy normalize_v + normalized_s + k256 from_scalars (range): SCHEME_NONE with the recovery
+// parity and the normalised s, or the scheme error.
+HLC_DEV int rec_parse(fe& s, const fe& r, uint32_t v, int& parity) {
   if (v == 0u || v == 27u) parity = 0;
   else if (v == 1u || v == 28u) parity = 1;
   else if (v >= 35u) parity = (int)((v - 35u) & 1u);
   else return SCHEME_BAD_PARITY;
-  // alloy normalized_s: s > n/2 -> n - s (wrapping U256 subtraction), parity flipped
   {
     fe h;
 #pragma unroll
     for (int i = 0; i < 8; ++i) h.v[i] = nhalf_limb(i);
-    if (u256_lt(h, s)) {
+    if (u256_lt(h, s)) {  // s > n/2 -> n - s (wrapping U256 subtraction), parity flipped
       uint32_t bw = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) s.v[i] = sub_cc(n_limb(i), s.v[i], bw);
       parity ^= 1;
     }
   }
-  // k256 Signature::from_scalars: r, s in [1, n)
   if (fe_is_zero(r) || sc_is_ge_n(r) || fe_is_zero(s) || sc_is_ge_n(s)) return SCHEME_SCALAR_RANGE;
+  return SCHEME_NONE;
+}
+
+// Prep stage, after r^-1 is known: u1 = -z/r (odd representative), u2 = s/r split by GLV and
+// recoded; writes the vote's record (stride = n, vote-major words).
+HLC_DEV void rec_prep_scalars(const fe& zraw, const fe& s, const fe& rinv, int parity, uint32_t* rec, size_t stride) {
   fe z;
   sc_reduce(z, zraw);
+  fe u1, u2;
+  {
+    fe r2c, rinvR;
+    sc_r2(r2c);
+    sc_mont_mul(rinvR, rinv, r2c);  // r^-1 * R (Montgomery form)
+    sc_mont_mul(u2, s, rinvR);      // s * r^-1
+    sc_mont_mul(u1, z, rinvR);      // z * r^-1
+    sc_neg(u1, u1);
+  }
+  const bool neg_g = (u1.v[0] & 1u) == 0u;
+  if (neg_g) {
+    uint32_t bw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u1.v[i] = sub_cc(n_limb(i), u1.v[i], bw);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rec[(size_t)(REC_U1 + i) * stride] = u1.v[i];
+  fe b1, b2;
+  bool nb1, nb2;
+  glv_split(u2, b1, nb1, b2, nb2);
+  const uint32_t s2 = recode_regular<W_R, M_R>(b1, rec + (size_t)REC_DIG * stride, stride);
+  const uint32_t s3 = recode_regular<W_R, M_R>(b2, rec + (size_t)(REC_DIG + DIG_R_WORDS) * stride, stride);
+  rec[(size_t)REC_FLAGS * stride] = (nb1 ? 1u : 0u) | (nb2 ? 2u : 0u) | (s2 << 2) | (s3 << 3) | (neg_g ? 16u : 0u) |
+                                    ((uint32_t)parity << 5);
+}
+
+// Main stage for one vote: R = decompress(r, parity), Q = u1 G + u2 R (Jacobian, not normalised).
+// Returns SCHEME_NONE, SCHEME_NO_POINT or SCHEME_INFINITY.  rec: the vote's record (stride n);
+// gcomb: the fixed-base comb; ws: this lane's interleaved workspace column (stride = lanes);
+// tab: this lane's R table.
+HLC_DEV int rec_main(const fe& r, const uint32_t* rec, size_t stride, gej& acc, const uint32_t* gcomb, uint32_t* ws,
+                     size_t ws_stride, uint32_t* tab) {
+  const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
+  const int parity = (int)((flags >> 5) & 1u);
   // R = decompress(r, parity): y^2 = x^3 + 7 (x = r < n < p)
   ge R;
   R.x = r;
@@ -354,36 +409,8 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
     if (!fe_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
     if ((int)(R.y.v[0] & 1u) != parity) fe_neg(R.y, R.y);
   }
-  // u1 = -z/r, u2 = s/r (mod n)
-  fe u1, u2;
-  {
-    fe r2c, rinv, rinvR;
-    sc_inv(rinv, r);               // safegcd
-    sc_r2(r2c);
-    sc_mont_mul(rinvR, rinv, r2c);  // r^-1 * R (Montgomery form)
-    sc_mont_mul(u2, s, rinvR);      // s * r^-1
-    sc_mont_mul(u1, z, rinvR);      // z * r^-1
-    sc_neg(u1, u1);
-  }
-  // u1 for the comb: its odd representative (u1 or n - u1, sign carried separately)
-  const bool neg_g = (u1.v[0] & 1u) == 0u;
-  if (neg_g) {
-    uint32_t bw = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) u1.v[i] = sub_cc(n_limb(i), u1.v[i], bw);
-  }
-  // GLV halves of u2 + regular digits into the workspace
-  int negs, skews;
-  {
-    fe b1, b2;
-    bool nb1, nb2;
-    glv_split(u2, b1, nb1, b2, nb2);
-    uint32_t* dws = ws + (size_t)DIG_OFF * stride;
-    uint32_t s2 = recode_regular<W_R, M_R>(b1, dws, stride);
-    uint32_t s3 = recode_regular<W_R, M_R>(b2, dws + (size_t)DIG_R_WORDS * stride, stride);
-    negs = (nb1 ? 1 : 0) | (nb2 ? 2 : 0);
-    skews = (int)(s2 | (s3 << 1));
-  }
+  const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
+  const bool neg_g = (flags & 16u) != 0;
   // R table on the isomorphic curve with C = Z(2R): entries (2i+1)R, i < 16, common Z
   fe zg;  // real Z of the table frame
   {
@@ -396,24 +423,24 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
     fe c2, c3;
     fe_sqr(c2, d.z);
     fe_mul(c3, c2, d.z);
-    gej acc;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve
-    fe_mul(acc.x, R.x, c2);
-    fe_mul(acc.y, R.y, c3);
-    fe_set(acc.z, 1);
-    store_ge_tab(acc.x, acc.y, tab);
-    uint32_t* zrws = ws + (size_t)ZR_OFF * stride;
+    gej a;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve
+    fe_mul(a.x, R.x, c2);
+    fe_mul(a.y, R.y, c3);
+    fe_set(a.z, 1);
+    store_ge_tab(a.x, a.y, tab);
+    uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
     for (int i = 1; i < RTAB_N; ++i) {
       fe zr;
-      gej_madd_zr(acc, dp, zr);  // (2i+1)R, Z_i = Z_{i-1} * zr
-      store_ge_tab(acc.x, acc.y, tab + 16 * i);
-      store_fe_ws(zr, zrws + (size_t)(8 * (i - 1)) * stride, stride);
+      gej_madd_zr(a, dp, zr);  // (2i+1)R, Z_i = Z_{i-1} * zr
+      store_ge_tab(a.x, a.y, tab + 16 * i);
+      store_fe_ws(zr, zrws + (size_t)(8 * (i - 1)) * ws_stride, ws_stride);
     }
     // common Z = Z_15: entry i scaled by s_i = Z_15 / Z_i = prod_{k > i} zr_k
     fe sc;
     fe_set(sc, 1);
     for (int i = RTAB_N - 2; i >= 0; --i) {
       fe zr, s2, s3;
-      load_fe_ws(zr, zrws + (size_t)(8 * i) * stride, stride);  // zr_{i+1}
+      load_fe_ws(zr, zrws + (size_t)(8 * i) * ws_stride, ws_stride);  // zr_{i+1}
       fe_mul(sc, sc, zr);
       fe_sqr(s2, sc);
       fe_mul(s3, s2, sc);
@@ -423,12 +450,11 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
       fe_mul(e.y, e.y, s3);
       store_ge_tab(e.x, e.y, tab + 16 * i);
     }
-    fe_mul(zg, acc.z, d.z);  // real Z of the frame: Z_15 * C
+    fe_mul(zg, a.z, d.z);  // real Z of the frame: Z_15 * C
   }
   fe beta;
   fe_beta(beta);
-  const uint32_t* dws = ws + (size_t)DIG_OFF * stride;
-  gej acc;
+  const uint32_t* dws = rec + (size_t)REC_DIG * stride;
   gej_set_inf(acc);
   // Additions in order (window 25, b1), (25, b2), 5 doublings, (24, b1), ... -- the two halves
   // add at the same positions (uniform across the wave).  The next addition's table entry is
@@ -469,14 +495,13 @@ HLC_DEV int ecrecover_lane(const fe& zraw, fe r, fe s, uint32_t v, uint32_t addr
     gej_add_ge(acc, acc, g);
   }
   if (!acc.inf) fe_mul(acc.z, acc.z, zg);  // u2 R back on the real curve
+  fe u1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u1.v[i] = rec[(size_t)(REC_U1 + i) * stride];
   gej ag;
   comb_mul_g(ag, u1, neg_g, gcomb);
   gej_add(acc, acc, ag);
-  if (acc.inf) return SCHEME_INFINITY;
-  fe qx, qy;
-  gej_to_affine(qx, qy, acc);
-  pubkey_address(qx, qy, addr);
-  return SCHEME_NONE;
+  return acc.inf ? SCHEME_INFINITY : SCHEME_NONE;
 }
 
 }  // namespace hlc
