@@ -1,0 +1,259 @@
+// hlc_point29.hpp -- the secp256k1 group law (a = 0, b = 7, Jacobian coordinates) over the 29-bit
+// unsaturated field layer (hlc_fe29.hpp), for the VALU-bound main recovery stage.  The formulas are
+// those of hlc_point.hpp (dbl-2009-l, madd-2007-bl, add-2007-bl) with every intermediate kept
+// inside hlc_fe29.hpp's magnitude contract: multiplication inputs are normalised values or sums of
+// two; every subtraction / small multiple carries once.  Exceptional cases (identity operand,
+// P == Q, P == -Q) are exact, so adversarial signatures (a crafted Q = infinity) match k256.
+#pragma once
+#include "hlc_fe29.hpp"
+#include "hlc_field.hpp"
+
+namespace hlc {
+
+struct gej29 {
+  fe29 x, y, z;
+  uint32_t inf;  // 1 = point at infinity
+};
+
+struct ge29 {
+  fe29 x, y;
+};
+
+// beta (cube root of unity mod p) in radix 2^29
+HLC_DEV void fe29_beta(fe29& r) {
+  const uint32_t b[9] = {0x119501EEu, 0x09CB6143u, 0x1D626570u, 0x0092EA25u, 0x034E99CFu,
+                         0x03CF561Au, 0x1C41B991u, 0x056CAF80u, 0x007AE96Au};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = b[i];
+}
+
+HLC_DEV void gej29_set_inf(gej29& r) {
+  fe29_set(r.x, 0);
+  fe29_set(r.y, 1);
+  fe29_set(r.z, 0);
+  r.inf = 1;
+}
+
+HLC_DEV void gej29_set_ge(gej29& r, const ge29& a) {
+  r.x = a.x;
+  r.y = a.y;
+  fe29_set(r.z, 1);
+  r.inf = 0;
+}
+
+// dbl-2009-l: 2M + 5S.  (secp256k1 has prime order: no point with y = 0.)  Subtractions that only
+// feed a multiplication by a normalised value, or another subtraction, stay lazy (hlc_fe29.hpp):
+// six carry steps per doubling.
+HLC_DEV void gej29_double(gej29& r, const gej29& a) {
+  fe29 A, B, C, D, D2, E, F, t;
+  fe29_sqr(A, a.x);
+  fe29_sqr(B, a.y);
+  fe29_sqr(C, B);
+  fe29_add(t, a.x, B);
+  fe29_sqr(t, t);
+  fe29_sub_lazy(t, t, A);
+  fe29_sub_lazy(t, t, C);
+  fe29_norm(t);                 // t = 2 X B (normalised)
+  fe29_add(D, t, t);            // D = 2t, lazy (< 2^30.01)
+  fe29_mul_small(D2, t, 4);     // 2D, normalised
+  fe29_mul_small(E, A, 3);
+  fe29_sqr(F, E);
+  fe29 z2;
+  fe29_add(z2, a.z, a.z);       // 2 Z (< 2^30.01) times normalised Y
+  fe29_mul(r.z, a.y, z2);
+  fe29_sub(r.x, F, D2);
+  fe29_sub_lazy(t, D, r.x);     // D - X3, lazy; times normalised E
+  fe29_mul(r.y, E, t);
+  fe29_mul_small(C, C, 4);      // 4C normalised; Y3 = E (D - X3) - 4C - 4C
+  fe29_sub_lazy(r.y, r.y, C);
+  fe29_sub_lazy(r.y, r.y, C);
+  fe29_norm(r.y);
+  r.inf = a.inf;
+}
+
+// r = a + b, b affine (madd-2007-bl: 7M + 4S).  r may alias a.  Eight carry steps (lazy
+// subtractions where the result only feeds a multiplication by a normalised value).
+HLC_DEV void gej29_add_ge(gej29& r, const gej29& a, const ge29& b) {
+  if (a.inf) {
+    gej29_set_ge(r, b);
+    return;
+  }
+  fe29 z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+  fe29_sqr(z1z1, a.z);
+  fe29_mul(u2, b.x, z1z1);
+  fe29_mul(s2, b.y, a.z);
+  fe29_mul(s2, s2, z1z1);
+  fe29_sub(h, u2, a.x);
+  fe29_sub_lazy(rr, s2, a.y);
+  if (fe29_is_zero_modp(h)) {
+    if (fe29_is_zero_modp(rr)) {
+      gej29_double(r, a);
+    } else {
+      gej29_set_inf(r);
+    }
+    return;
+  }
+  fe29_sqr(hh, h);
+  fe29_mul_small(i4, hh, 4);
+  fe29_mul(j, h, i4);
+  fe29_mul_small(rr, rr, 2);  // lazy in, normalised out
+  fe29_mul(v, a.x, i4);
+  // z3 = (z1 + h)^2 - z1z1 - hh
+  fe29 z3;
+  fe29_add(z3, a.z, h);
+  fe29_sqr(z3, z3);
+  fe29_sub_lazy(z3, z3, z1z1);
+  fe29_sub_lazy(z3, z3, hh);
+  fe29_norm(z3);
+  // x3 = r^2 - j - 2v
+  fe29 x3;
+  fe29_sqr(x3, rr);
+  fe29_sub_lazy(x3, x3, j);
+  fe29_dbl(t, v);
+  fe29_sub_lazy(x3, x3, t);
+  fe29_norm(x3);
+  // y3 = r (v - x3) - 2 y1 j
+  fe29 y3;
+  fe29_sub_lazy(t, v, x3);
+  fe29_mul(y3, rr, t);
+  fe29_mul(t, a.y, j);
+  fe29_dbl(t, t);
+  fe29_sub(y3, y3, t);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+  r.inf = 0;
+}
+
+// a += b (b affine, a finite, a != +-b: the R-table build, where (2i-1)R and 2R are distinct,
+// non-opposite multiples of a point of prime order n); zr = Z(a') / Z(a) = 2H.
+HLC_DEV void gej29_madd_zr(gej29& a, const ge29& b, fe29& zr) {
+  fe29 z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+  fe29_sqr(z1z1, a.z);
+  fe29_mul(u2, b.x, z1z1);
+  fe29_mul(s2, b.y, a.z);
+  fe29_mul(s2, s2, z1z1);
+  fe29_sub(h, u2, a.x);
+  fe29_sub(rr, s2, a.y);
+  fe29_sqr(hh, h);
+  fe29_mul_small(i4, hh, 4);
+  fe29_mul(j, h, i4);
+  fe29_dbl(rr, rr);
+  fe29_mul(v, a.x, i4);
+  fe29_dbl(zr, h);
+  fe29_mul(a.z, a.z, zr);
+  fe29 x3;
+  fe29_sqr(x3, rr);
+  fe29_sub(x3, x3, j);
+  fe29_dbl(t, v);
+  fe29_sub(x3, x3, t);
+  fe29_sub(t, v, x3);
+  fe29 y3;
+  fe29_mul(y3, rr, t);
+  fe29_mul(t, a.y, j);
+  fe29_dbl(t, t);
+  fe29_sub(a.y, y3, t);
+  a.x = x3;
+  a.inf = 0;
+}
+
+// r = a + b, both Jacobian (add-2007-bl: 11M + 5S).  r may alias a.
+HLC_DEV void gej29_add(gej29& r, const gej29& a, const gej29& b) {
+  if (b.inf) {
+    r = a;
+    return;
+  }
+  if (a.inf) {
+    r = b;
+    return;
+  }
+  fe29 z1z1, z2z2, u1, u2, s1, s2, h, i4, j, rr, v, t;
+  fe29_sqr(z1z1, a.z);
+  fe29_sqr(z2z2, b.z);
+  fe29_mul(u1, a.x, z2z2);
+  fe29_mul(u2, b.x, z1z1);
+  fe29_mul(s1, a.y, b.z);
+  fe29_mul(s1, s1, z2z2);
+  fe29_mul(s2, b.y, a.z);
+  fe29_mul(s2, s2, z1z1);
+  fe29_sub(h, u2, u1);
+  fe29_sub(rr, s2, s1);
+  if (fe29_is_zero_modp(h)) {
+    if (fe29_is_zero_modp(rr)) {
+      gej29_double(r, a);
+    } else {
+      gej29_set_inf(r);
+    }
+    return;
+  }
+  fe29_dbl(i4, h);
+  fe29_sqr(i4, i4);
+  fe29_mul(j, h, i4);
+  fe29_dbl(rr, rr);
+  fe29_mul(v, u1, i4);
+  fe29 z3;
+  fe29_add(z3, a.z, b.z);
+  fe29_sqr(z3, z3);
+  fe29_sub(z3, z3, z1z1);
+  fe29_sub(z3, z3, z2z2);
+  fe29_mul(z3, z3, h);
+  fe29 x3;
+  fe29_sqr(x3, rr);
+  fe29_sub(x3, x3, j);
+  fe29_dbl(t, v);
+  fe29_sub(x3, x3, t);
+  fe29 y3;
+  fe29_sub(t, v, x3);
+  fe29_mul(y3, rr, t);
+  fe29_mul(t, s1, j);
+  fe29_dbl(t, t);
+  fe29_sub(y3, y3, t);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+  r.inf = 0;
+}
+
+HLC_DEV void fe29_sqr_n(fe29& r, const fe29& a, int n) {
+  r = a;
+  for (int i = 0; i < n; ++i) fe29_sqr(r, r);
+}
+
+// r = a^((p+1)/4) (canonical); returns whether r^2 == a (a quadratic residue).  The addition
+// chain of hlc_field.hpp's fe_sqrt (253 S + 13 M).
+HLC_DEV bool fe29_sqrt(fe29& r, const fe29& a) {
+  fe29 x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  fe29_sqr(t, a);
+  fe29_mul(x2, t, a);
+  fe29_sqr(t, x2);
+  fe29_mul(x3, t, a);
+  fe29_sqr_n(t, x3, 3);
+  fe29_mul(x6, t, x3);
+  fe29_sqr_n(t, x6, 3);
+  fe29_mul(x9, t, x3);
+  fe29_sqr_n(t, x9, 2);
+  fe29_mul(x11, t, x2);
+  fe29_sqr_n(t, x11, 11);
+  fe29_mul(x22, t, x11);
+  fe29_sqr_n(t, x22, 22);
+  fe29_mul(x44, t, x22);
+  fe29_sqr_n(t, x44, 44);
+  fe29_mul(x88, t, x44);
+  fe29_sqr_n(t, x88, 88);
+  fe29_mul(x176, t, x88);
+  fe29_sqr_n(t, x176, 44);
+  fe29_mul(x220, t, x44);
+  fe29_sqr_n(t, x220, 3);
+  fe29_mul(x223, t, x3);
+  fe29_sqr_n(t, x223, 23);
+  fe29_mul(t, t, x22);
+  fe29_sqr_n(t, t, 6);
+  fe29_mul(t, t, x2);
+  fe29_sqr_n(r, t, 2);
+  fe29_normalize(r, r);
+  fe29_sqr(t, r);
+  fe29_sub(t, t, a);
+  return fe29_is_zero_modp(t);
+}
+
+}  // namespace hlc

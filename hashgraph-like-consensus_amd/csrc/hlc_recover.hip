@@ -10,7 +10,7 @@ namespace {
 
 constexpr int REC_TPB = 256;
 #ifndef HLC_REC_WAVES
-#define HLC_REC_WAVES 4  // waves per SIMD the register allocator must admit for k_recover
+#define HLC_REC_WAVES 3  // waves per SIMD the register allocator must admit for k_rec_main (best of 2/3/4, profiles/r02_variants.txt)
 #endif
 
 // ---- prep: parse + batched r^-1 + scalars (REC_BATCH votes per lane, one safegcd) ----
@@ -80,15 +80,26 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
     if ((pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
     fe r;
     fe_load_be(r, bytes + sig_off[i * off_stride]);
+    fe qx, qy, qz;
+#ifdef HLC_FIELD32
+    // A/B variant (make variants): the saturated 8 x 32 field layer
     gej acc;
-    const int code = rec_main(r, rec + i, n, acc, gcomb, ws, lanes, tab);
+    int code = rec_main(r, rec + i, n, acc, gcomb, ws, lanes, tab);
+    if (code == SCHEME_NONE) {
+      qx = acc.x;
+      qy = acc.y;
+      qz = acc.z;
+    }
+#else
+    const int code = rec_main29(r, rec + i, n, qx, qy, qz, gcomb, ws, lanes, tab);
+#endif
     if (code != SCHEME_NONE) {
       state[i] = (uint8_t)(1 + code);
       continue;
     }
-    store_fe_ws(acc.x, q + i, n);
-    store_fe_ws(acc.y, q + (size_t)8 * n + i, n);
-    store_fe_ws(acc.z, q + (size_t)16 * n + i, n);
+    store_fe_ws(qx, q + i, n);
+    store_fe_ws(qy, q + (size_t)8 * n + i, n);
+    store_fe_ws(qz, q + (size_t)16 * n + i, n);
   }
 }
 
@@ -242,8 +253,8 @@ uint64_t recover_work_words(uint64_t n) {
 
 uint64_t recover_grid_lanes() {
   int dev = 0, cus = 256, per_cu = 0;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rec_main, REC_TPB, 0) != hipSuccess || per_cu < 1)
     per_cu = 2;
   return (uint64_t)cus * (uint64_t)per_cu * REC_TPB;

@@ -40,6 +40,7 @@
 #pragma once
 #include "hlc_hash.hpp"
 #include "hlc_point.hpp"
+#include "hlc_point29.hpp"
 
 namespace hlc {
 
@@ -57,9 +58,10 @@ constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
 //    each access is one coalesced 256-B row per wave): the z-ratios of the table build;
 //  * per-lane contiguous R table (RTAB_WORDS words, 64-B entries read by 16-B vector loads):
 //    entries are gathered at lane-dependent indices, so each lane's entry must be one block.
-constexpr int RTAB_WORDS = RTAB_N * 16;         // per lane (affine, common-Z frame)
-constexpr int ZR_OFF = 0;                       // z-ratios of the table build
-constexpr int IL_WORDS = ZR_OFF + 8 * (RTAB_N - 1);       // interleaved words per lane
+constexpr int RTAB_ENTRY = 20;                  // words per entry: x, y in 9 x 29-bit limbs + 2 pad (80 B)
+constexpr int RTAB_WORDS = RTAB_N * RTAB_ENTRY; // per lane (affine, common-Z frame)
+constexpr int ZR_OFF = 0;                       // z-ratios of the table build (9 limbs each)
+constexpr int IL_WORDS = ZR_OFF + 9 * (RTAB_N - 1);       // interleaved words per lane
 constexpr int SCRATCH_WORDS = IL_WORDS + RTAB_WORDS;      // per lane workspace words
 
 // Per-vote records between the stages, word-major (word w of vote i at w * n + i: a wave's 64
@@ -387,6 +389,177 @@ HLC_DEV void rec_prep_scalars(const fe& zraw, const fe& s, const fe& rinv, int p
   const uint32_t s3 = recode_regular<W_R, M_R>(b2, rec + (size_t)(REC_DIG + DIG_R_WORDS) * stride, stride);
   rec[(size_t)REC_FLAGS * stride] = (nb1 ? 1u : 0u) | (nb2 ? 2u : 0u) | (s2 << 2) | (s3 << 3) | (neg_g ? 16u : 0u) |
                                     ((uint32_t)parity << 5);
+}
+
+// ---- main stage helpers over the 29-bit field layer ----
+HLC_DEV void store_ge29_tab(const fe29& x, const fe29& y, uint32_t* t) {
+  uint4* p = reinterpret_cast<uint4*>(t);
+  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  p[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+  p[2] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
+  p[3] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
+  p[4] = make_uint4(y.v[7], y.v[8], 0u, 0u);
+}
+HLC_DEV void load_ge29_tab(ge29& g, const uint32_t* t) {
+  const uint4* p = reinterpret_cast<const uint4*>(t);
+  const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+  g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
+  g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
+  g.x.v[8] = c.x; g.y.v[0] = c.y; g.y.v[1] = c.z; g.y.v[2] = c.w;
+  g.y.v[3] = d.x; g.y.v[4] = d.y; g.y.v[5] = d.z; g.y.v[6] = d.w;
+  g.y.v[7] = e.x; g.y.v[8] = e.y;
+}
+HLC_DEV void store_fe29_ws(const fe29& x, uint32_t* ws, size_t stride) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) ws[(size_t)i * stride] = x.v[i];
+}
+HLC_DEV void load_fe29_ws(fe29& x, const uint32_t* ws, size_t stride) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) x.v[i] = ws[(size_t)i * stride];
+}
+// comb entry (8 x 32 affine, global) -> 29-bit limbs
+HLC_DEV void load_ge_global29(ge29& g, const uint32_t* t) {
+  ge e;
+  load_ge_global(e, t);
+  fe29_from32(g.x, e.x.v);
+  fe29_from32(g.y, e.y.v);
+}
+
+// acc = k G for odd k < 2^256 (neg: acc = -k G), by the comb (see comb_mul_g), in 29-bit limbs.
+HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
+  ge29 e;
+  load_ge_global29(e, gcomb + GC_TOP_OFF);
+  if (neg) fe29_neg(e.y, e.y);
+  gej29_set_ge(acc, e);
+  int d = comb_digit(k);
+  load_ge_global29(e, comb_entry(gcomb, 0, d));
+#pragma unroll 1
+  for (int w = 0; w < GC_WINDOWS; ++w) {
+    ge29 cur = e;
+    const int dc = d;
+    if (w + 1 < GC_WINDOWS) {  // prefetch the next window's entry
+      d = comb_digit(k);
+      load_ge_global29(e, comb_entry(gcomb, w + 1, d));
+    }
+    if ((dc < 0) != neg) fe29_neg(cur.y, cur.y);
+    gej29_add_ge(acc, acc, cur);
+  }
+}
+
+// Main stage for one vote, over the 29-bit unsaturated field layer (hlc_fe29.hpp: ~25% fewer
+// issue cycles per multiplication than the saturated 8 x 32 layer, profiles/r02_ubench_field29.txt).
+// R = decompress(r, parity), Q = u1 G + u2 R, Q returned in 8 x 32 canonical limbs (x, y, z) for
+// the final stage.  Returns SCHEME_NONE, SCHEME_NO_POINT or SCHEME_INFINITY.
+HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz,
+                       const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab) {
+  const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
+  const int parity = (int)((flags >> 5) & 1u);
+  ge29 R;
+  fe29_from32(R.x, r32.v);
+  {
+    fe29 x3, alpha, seven;
+    fe29_sqr(x3, R.x);
+    fe29_mul(x3, x3, R.x);
+    fe29_set(seven, 7);
+    fe29_add(alpha, x3, seven);
+    if (!fe29_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
+    if ((int)(R.y.v[0] & 1u) != parity) fe29_neg(R.y, R.y);
+  }
+  const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
+  const bool neg_g = (flags & 16u) != 0;
+  fe29 zg;
+  {
+    gej29 d;
+    gej29_set_ge(d, R);
+    gej29_double(d, d);  // 2R = (X, Y, C); on the iso curve it is the affine point (X, Y)
+    ge29 dp;
+    dp.x = d.x;
+    dp.y = d.y;
+    fe29 c2, c3;
+    fe29_sqr(c2, d.z);
+    fe29_mul(c3, c2, d.z);
+    gej29 a;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve
+    fe29_mul(a.x, R.x, c2);
+    fe29_mul(a.y, R.y, c3);
+    fe29_set(a.z, 1);
+    store_ge29_tab(a.x, a.y, tab);
+    uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
+    for (int i = 1; i < RTAB_N; ++i) {
+      fe29 zr;
+      gej29_madd_zr(a, dp, zr);
+      store_ge29_tab(a.x, a.y, tab + RTAB_ENTRY * i);
+      store_fe29_ws(zr, zrws + (size_t)(9 * (i - 1)) * ws_stride, ws_stride);
+    }
+    fe29 sc;
+    fe29_set(sc, 1);
+    for (int i = RTAB_N - 2; i >= 0; --i) {
+      fe29 zr, s2, s3;
+      load_fe29_ws(zr, zrws + (size_t)(9 * i) * ws_stride, ws_stride);
+      fe29_mul(sc, sc, zr);
+      fe29_sqr(s2, sc);
+      fe29_mul(s3, s2, sc);
+      ge29 e;
+      load_ge29_tab(e, tab + RTAB_ENTRY * i);
+      fe29_mul(e.x, e.x, s2);
+      fe29_mul(e.y, e.y, s3);
+      store_ge29_tab(e.x, e.y, tab + RTAB_ENTRY * i);
+    }
+    fe29_mul(zg, a.z, d.z);
+  }
+  fe29 beta;
+  fe29_beta(beta);  // wave-uniform: multiplied from SGPRs (fe29_mul_uniform)
+  const uint32_t* dws = rec + (size_t)REC_DIG * stride;
+  gej29 acc;
+  gej29_set_inf(acc);
+  // Additions in order (window 25, b1), (25, b2), 5 doublings, (24, b1), ... -- the two halves add
+  // at the same positions (uniform across the wave).  Register pressure, not load latency, bounds
+  // this loop: the b1 entry is loaded before the last doubling of its window (one point operation
+  // ahead) and the b2 entry right after the b1 addition (its latency hidden by the other waves).
+  auto digit_at = [&](int win, int k) {
+    return digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
+  };
+  auto entry_of = [&](int d) { return tab + RTAB_ENTRY * (((d < 0 ? -d : d) - 1) >> 1); };
+#pragma unroll 1
+  for (int win = M_R - 1; win >= 0; --win) {
+    ge29 g;
+    int d = digit_at(win, 0);
+    if (win != M_R - 1) {
+#pragma unroll 1
+      for (int q = 0; q < W_R - 1; ++q) gej29_double(acc, acc);
+      load_ge29_tab(g, entry_of(d));
+      gej29_double(acc, acc);
+    } else {
+      load_ge29_tab(g, entry_of(d));
+    }
+    if ((d < 0) != ((negs & 1) != 0)) fe29_neg(g.y, g.y);
+    gej29_add_ge(acc, acc, g);
+    d = digit_at(win, 1);
+    load_ge29_tab(g, entry_of(d));
+    fe29_mul_uniform(g.x, g.x, beta);
+    if ((d < 0) != ((negs & 2) != 0)) fe29_neg(g.y, g.y);
+    gej29_add_ge(acc, acc, g);
+  }
+#pragma unroll 1
+  for (int k = 0; k < 2; ++k) {
+    if (((skews >> k) & 1) == 0) continue;
+    ge29 g;
+    load_ge29_tab(g, tab);
+    if (k == 1) fe29_mul_uniform(g.x, g.x, beta);
+    if (((negs >> k) & 1) == 0) fe29_neg(g.y, g.y);
+    gej29_add_ge(acc, acc, g);
+  }
+  if (!acc.inf) fe29_mul(acc.z, acc.z, zg);
+  fe u1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u1.v[i] = rec[(size_t)(REC_U1 + i) * stride];
+  gej29 ag;
+  comb_mul_g29(ag, u1, neg_g, gcomb);
+  gej29_add(acc, acc, ag);
+  if (acc.inf) return SCHEME_INFINITY;
+  fe29_to32(qx.v, acc.x);
+  fe29_to32(qy.v, acc.y);
+  fe29_to32(qz.v, acc.z);
+  return SCHEME_NONE;
 }
 
 // Main stage for one vote: R = decompress(r, parity), Q = u1 G + u2 R (Jacobian, not normalised).

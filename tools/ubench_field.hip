@@ -12,6 +12,8 @@
 #include <cstdlib>
 
 #include "../hashgraph-like-consensus_amd/csrc/hlc_point.hpp"
+#include "../hashgraph-like-consensus_amd/csrc/hlc_fe29.hpp"
+#include "../hashgraph-like-consensus_amd/csrc/hlc_point29.hpp"
 
 using namespace hlc;
 
@@ -135,6 +137,170 @@ __global__ void __launch_bounds__(TPB, 4) k_mul_x2(uint32_t* out, int iters) {
   sink(out, x);
 }
 
+// ---- 29-bit unsaturated layer (hlc_fe29.hpp) ----
+__device__ void seed29(fe29& a, uint32_t s) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a.v[i] = (((s + 0x9E3779B9u * (i + 1)) * 0x85EBCA6Bu) ^ (s >> 3)) & M29;
+}
+template <int W>
+__global__ void __launch_bounds__(TPB, W) k_mul29(uint32_t* out, int iters) {
+  fe29 a, b;
+  seed29(a, threadIdx.x + blockIdx.x * TPB);
+  seed29(b, 7 * threadIdx.x + 1);
+  for (int k = 0; k < iters; ++k) fe29_mul(a, a, b);
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= a.v[i];
+  sink(out, x);
+}
+template <int W>
+__global__ void __launch_bounds__(TPB, W) k_sqr29(uint32_t* out, int iters) {
+  fe29 a;
+  seed29(a, threadIdx.x + blockIdx.x * TPB);
+  for (int k = 0; k < iters; ++k) fe29_sqr(a, a);
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= a.v[i];
+  sink(out, x);
+}
+__global__ void __launch_bounds__(TPB, 4) k_subsub29(uint32_t* out, int iters) {
+  fe29 a, b;
+  seed29(a, threadIdx.x + blockIdx.x * TPB);
+  seed29(b, 7 * threadIdx.x + 1);
+  for (int k = 0; k < iters; ++k) {
+    fe29_sub(a, a, b);
+    fe29_sub(b, b, a);
+  }
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= a.v[i] ^ b.v[i];
+  sink(out, x);
+}
+__global__ void __launch_bounds__(TPB, 4) k_subsub(uint32_t* out, int iters) {
+  fe a, b;
+  seed_fe(a, threadIdx.x + blockIdx.x * TPB);
+  seed_fe(b, 7 * threadIdx.x + 1);
+  for (int k = 0; k < iters; ++k) {
+    fe_sub(a, a, b);
+    fe_sub(b, b, a);
+  }
+  uint32_t x = 0;
+  for (int i = 0; i < 8; ++i) x ^= a.v[i] ^ b.v[i];
+  sink(out, x);
+}
+
+template <int W>
+__global__ void __launch_bounds__(TPB, W) k_mul29ref(uint32_t* out, int iters) {
+  fe29 a, b;
+  seed29(a, threadIdx.x + blockIdx.x * TPB);
+  seed29(b, 7 * threadIdx.x + 1);
+  for (int k = 0; k < iters; ++k) fe29_mul_ref(a, a, b);
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= a.v[i];
+  sink(out, x);
+}
+
+// two independent product chains: separate calls vs one interleaved dual schedule (fe29_mul2)
+template <int DUAL>
+__global__ void __launch_bounds__(TPB, 4) k_mul29x2(uint32_t* out, int iters) {
+  fe29 a, b, c, e;
+  seed29(a, threadIdx.x + blockIdx.x * TPB);
+  seed29(b, 7 * threadIdx.x + 1);
+  seed29(c, 5 * threadIdx.x + 3);
+  seed29(e, 9 * threadIdx.x + 4);
+  for (int k = 0; k < iters; ++k) {
+    if (DUAL) {
+      fe29_mul2(a, a, b, c, c, e);
+    } else {
+      fe29_mul(a, a, b);
+      fe29_mul(c, c, e);
+    }
+  }
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= a.v[i] ^ c.v[i];
+  sink(out, x);
+}
+template <int DUAL>
+__global__ void __launch_bounds__(TPB, 4) k_sqr29x2(uint32_t* out, int iters) {
+  fe29 a, c;
+  seed29(a, threadIdx.x + blockIdx.x * TPB);
+  seed29(c, 5 * threadIdx.x + 3);
+  for (int k = 0; k < iters; ++k) {
+    if (DUAL) {
+      fe29_sqr2(a, a, c, c);
+    } else {
+      fe29_sqr(a, a);
+      fe29_sqr(c, c);
+    }
+  }
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= a.v[i] ^ c.v[i];
+  sink(out, x);
+}
+
+__global__ void __launch_bounds__(TPB, 4) k_dbl29(uint32_t* out, int iters) {
+  gej29 p;
+  seed29(p.x, threadIdx.x + blockIdx.x * TPB);
+  seed29(p.y, 3 * threadIdx.x + 5);
+  seed29(p.z, 11 * threadIdx.x + 2);
+  p.inf = 0;
+  for (int k = 0; k < iters; ++k) gej29_double(p, p);
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= p.x.v[i] ^ p.y.v[i] ^ p.z.v[i];
+  sink(out, x);
+}
+__global__ void __launch_bounds__(TPB, 4) k_madd29(uint32_t* out, int iters) {
+  gej29 p;
+  ge29 q;
+  seed29(p.x, threadIdx.x + blockIdx.x * TPB);
+  seed29(p.y, 3 * threadIdx.x + 5);
+  seed29(p.z, 11 * threadIdx.x + 2);
+  seed29(q.x, 13 * threadIdx.x + 7);
+  seed29(q.y, 17 * threadIdx.x + 9);
+  p.inf = 0;
+  for (int k = 0; k < iters; ++k) gej29_add_ge(p, p, q);
+  uint32_t x = 0;
+  for (int i = 0; i < 9; ++i) x ^= p.x.v[i] ^ p.y.v[i] ^ p.z.v[i];
+  sink(out, x);
+}
+
+// asm schedule == C++ reference on random and extreme inputs (limbs < 2^30.35)
+__device__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+__global__ void k_check29(uint32_t* bad, int rounds) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t MAXIN = 1367130551u;  // floor(2^30.35)
+  for (int r = 0; r < rounds; ++r) {
+    fe29 a, b, x, y;
+    const uint32_t mode = hash32(t * 977u + r) & 7u;
+    for (int i = 0; i < 9; ++i) {
+      uint32_t ha = hash32(t * 131u + r * 7919u + i), hb = hash32(t * 337u + r * 104729u + i + 100);
+      a.v[i] = mode == 0 ? MAXIN - (ha & 3u) : ha % MAXIN;
+      b.v[i] = mode <= 1 ? MAXIN - (hb & 3u) : hb % MAXIN;
+      if (mode == 2) a.v[i] = ha & M29;
+    }
+    fe29_mul(x, a, b);
+    fe29_mul_ref(y, a, b);
+    uint32_t d = 0;
+    for (int i = 0; i < 9; ++i) d |= x.v[i] ^ y.v[i];
+    fe29_sqr(x, a);
+    fe29_sqr_ref(y, a);
+    for (int i = 0; i < 9; ++i) d |= x.v[i] ^ y.v[i];
+    // dual schedules: x = a b, y = b^2 (and a^2, b^2; a b, b a)
+    fe29 x2, y2, xr, yr;
+    fe29_mulsqr(x2, a, b, y2, b);
+    fe29_mul_ref(xr, a, b);
+    fe29_sqr_ref(yr, b);
+    for (int i = 0; i < 9; ++i) d |= (x2.v[i] ^ xr.v[i]) | (y2.v[i] ^ yr.v[i]);
+    fe29_sqr2(x2, a, y2, b);
+    fe29_sqr_ref(xr, a);
+    for (int i = 0; i < 9; ++i) d |= (x2.v[i] ^ xr.v[i]) | (y2.v[i] ^ yr.v[i]);
+    fe29_mul2(x2, a, b, y2, b, a);
+    fe29_mul_ref(xr, a, b);
+    for (int i = 0; i < 9; ++i) d |= (x2.v[i] ^ xr.v[i]) | (y2.v[i] ^ xr.v[i]);
+    if (d) atomicAdd(bad, 1u);
+  }
+}
+
 template <typename K>
 float run(K kern, uint32_t* d, int blocks, int iters) {
   hipEvent_t a, b;
@@ -162,16 +328,27 @@ int main(int argc, char** argv) {
   struct R {
     const char* name;
     float ms;
-    int div;
+    double div;
   } r[] = {{"fe_mul", run(k_mul, d, blocks, iters), 1},
            {"fe_sqr", run(k_sqr, d, blocks, iters), 1},
            {"fe_add+fe_sub", run(k_addsub, d, blocks, iters), 1},
            {"gej_double", run(k_dbl, d, blocks, iters), 1},
            {"gej_add_ge", run(k_madd, d, blocks, iters), 1},
-           {"fe_inv", run(k_inv, d, blocks, iters / 20), 20},
-           {"fe_mul x2 ILP", run(k_mul_x2, d, blocks, iters), 1}};
+           {"fe_inv", run(k_inv, d, blocks, iters / 20), 0.05},
+           {"fe_mul x2 ILP", run(k_mul_x2, d, blocks, iters), 1},
+           {"fe_sub x2", run(k_subsub, d, blocks, iters), 1},
+           {"fe29_mul", run(k_mul29<4>, d, blocks, iters), 1},
+           {"fe29_sqr", run(k_sqr29<4>, d, blocks, iters), 1},
+           {"fe29_sub x2", run(k_subsub29, d, blocks, iters), 1},
+           {"fe29_mul (C++)", run(k_mul29ref<4>, d, blocks, iters), 1},
+           {"fe29_mul x2 sep", run(k_mul29x2<0>, d, blocks, iters), 2},
+           {"fe29_mul2 dual", run(k_mul29x2<1>, d, blocks, iters), 2},
+           {"fe29_sqr x2 sep", run(k_sqr29x2<0>, d, blocks, iters), 2},
+           {"fe29_sqr2 dual", run(k_sqr29x2<1>, d, blocks, iters), 2},
+           {"gej29_double", run(k_dbl29, d, blocks, iters), 1},
+           {"gej29_add_ge", run(k_madd29, d, blocks, iters), 1}};
   for (auto& x : r) {
-    const double ns = x.ms * 1e6 / (iters / x.div);  // per op, 4 waves per SIMD in parallel
+    const double ns = x.ms * 1e6 / iters / x.div;  // per op (div ops per iteration), 4 waves per SIMD
     printf("%-14s %8.3f ms  %8.1f ns/op  %8.1f SIMD-cycles/wave-op @%.2f GHz\n", x.name, x.ms, ns,
            ns * ghz / 4.0, ghz);
   }
@@ -179,6 +356,18 @@ int main(int argc, char** argv) {
   const float m8 = run(k_mul8, d, 2 * blocks, iters), s8 = run(k_sqr8, d, 2 * blocks, iters);
   printf("fe_mul @8w     %8.3f ms  %8.1f SIMD-cycles/wave-op\n", m8, m8 * 1e6 / iters * ghz / 8.0);
   printf("fe_sqr @8w     %8.3f ms  %8.1f SIMD-cycles/wave-op\n", s8, s8 * 1e6 / iters * ghz / 8.0);
+  const float m29 = run(k_mul29<8>, d, 2 * blocks, iters), s29 = run(k_sqr29<8>, d, 2 * blocks, iters);
+  printf("fe29_mul @8w   %8.3f ms  %8.1f SIMD-cycles/wave-op\n", m29, m29 * 1e6 / iters * ghz / 8.0);
+  printf("fe29_sqr @8w   %8.3f ms  %8.1f SIMD-cycles/wave-op\n", s29, s29 * 1e6 / iters * ghz / 8.0);
+  // one wave per SIMD (one 256-thread block per CU): how much a lone wave loses to latency
+  const float d1 = run(k_dbl29, d, cus, iters), d4 = run(k_dbl29, d, blocks, iters);
+  printf("gej29_double: 1 wave/SIMD %.3f ms, 4 waves/SIMD %.3f ms (lone-wave speed = %.2f of the 4-wave share)\n",
+         d1, d4, d4 / 4.0 / d1);
+  CHECK(hipMemset(d, 0, 4));
+  hipLaunchKernelGGL(k_check29, dim3(blocks), dim3(TPB), 0, 0, d, 64);
+  uint32_t bad = 0;
+  CHECK(hipMemcpy(&bad, d, 4, hipMemcpyDeviceToHost));
+  printf("fe29 asm vs C++ reference: %u mismatching lanes of %d (x64 rounds, mul + sqr)\n", bad, blocks * TPB);
   CHECK(hipFree(d));
-  return 0;
+  return bad ? 1 : 0;
 }

@@ -54,6 +54,9 @@ constexpr int ITERS = 2048;
 #define I_MOV(k) "v_mov_b32 %" S(k) ", %8\n"
 #define I_XOR(k) "v_xor_b32 %" S(k) ", %" S(k) ", %8\n"
 #define I_PERM(k) "v_perm_b32 %" S(k) ", %" S(k) ", %8, %9\n"
+#define I_ANDLIT(k) "v_and_b32 %" S(k) ", 0x1fffffff, %" S(k) "\n"
+#define I_ADDE64(k) "v_add_u32_e64 %" S(k) ", %" S(k) ", %8\n"
+#define I_ANDSG(k) "v_and_b32 %" S(k) ", s2, %" S(k) "\n"
 #define I_SUB(k) "v_sub_u32 %" S(k) ", %" S(k) ", %8\n"
 
 K32(k_add, I_ADD)
@@ -75,6 +78,9 @@ K32(k_mov, I_MOV)
 K32(k_xor, I_XOR)
 K32(k_perm, I_PERM)
 K32(k_sub, I_SUB)
+K32(k_andlit, I_ANDLIT)
+K32(k_adde64, I_ADDE64)
+K32(k_andsg, I_ANDSG)
 
 // 64-bit ops on 8 accumulators
 #define K64(NAME, INS)                                                                              \
@@ -177,6 +183,9 @@ int main() {
   rc |= run("add3_u32", k_add3, d);
   rc |= run("and_b32", k_and, d);
   rc |= run("xor_b32", k_xor, d);
+  rc |= run("and_b32 literal", k_andlit, d);
+  rc |= run("and_b32 sgpr", k_andsg, d);
+  rc |= run("add_u32_e64 (VOP3 enc)", k_adde64, d);
   rc |= run("mov_b32", k_mov, d);
   rc |= run("lshrrev_b32", k_lshr, d);
   rc |= run("alignbit", k_align, d);
