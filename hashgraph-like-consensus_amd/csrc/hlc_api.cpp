@@ -125,9 +125,9 @@ int upload(DBuf& b, const T* host, size_t count, hipStream_t s) {
 // Prefix sums of message sizes + device->host read of the totals (one sync).
 int scan_sizes(hlc_ctx* c, uint64_t n, const uint64_t* sz, uint64_t* off, uint64_t* total, hipStream_t s) {
   size_t tb = 0;
-  hlc::launch_exclusive_scan(sz, off, n, nullptr, tb, s);
+  HIPCHK(hlc::launch_exclusive_scan(sz, off, n, nullptr, tb, s));
   CHK(c->scan_tmp.ensure(tb + 16));
-  hlc::launch_exclusive_scan(sz, off, n, c->scan_tmp.p, tb, s);
+  HIPCHK(hlc::launch_exclusive_scan(sz, off, n, c->scan_tmp.p, tb, s));
   HIPCHK(hipGetLastError());
   CHK(c->totals.ensure(4 * sizeof(uint64_t)));
   uint64_t* t = c->totals.as<uint64_t>();
@@ -236,7 +236,7 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   CHK(c->vote_prop.ensure(n * 4 + 4));
   CHK(c->flag.ensure(16));
   HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(uint32_t), s));
-  hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s);
+  HIPCHK(hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s));
   uint8_t* status = dstatus;
   uint8_t* reason = dreason;
   if (!status) {
@@ -303,9 +303,9 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
     // parallel path (skipped by the walker, vote_count 0 so far) is there a second round trip.
     auto scan_totals = [&](uint64_t* h) -> int {
       size_t tb = 0;
-      hlc::launch_exclusive_scan(vcount, vbegin, nm, nullptr, tb, s);
+      HIPCHK(hlc::launch_exclusive_scan(vcount, vbegin, nm, nullptr, tb, s));
       CHK(c->scan_tmp.ensure(tb + 16));
-      hlc::launch_exclusive_scan(vcount, vbegin, nm, c->scan_tmp.p, tb, s);
+      HIPCHK(hlc::launch_exclusive_scan(vcount, vbegin, nm, c->scan_tmp.p, tb, s));
       HIPCHK(hipMemcpyAsync(h, vbegin + (nm - 1), 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipMemcpyAsync(h + 1, vcount + (nm - 1), 8, hipMemcpyDeviceToHost, s));
       HIPCHK(hipMemcpyAsync(h + 2, c->w_big.p, 4, hipMemcpyDeviceToHost, s));
@@ -735,11 +735,11 @@ int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vses
   CHK(ctx->s_iota.ensure(n * 4 + 4));
   CHK(ctx->s_order.ensure(n * 4 + 4));
   size_t tb = 0;
-  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
-                              ctx->s_order.as<uint32_t>(), nullptr, tb, s);
+  HIPCHK(hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
+                              ctx->s_order.as<uint32_t>(), nullptr, tb, s));
   CHK(ctx->s_sort_tmp.ensure(tb + 16));
-  hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
-                              ctx->s_order.as<uint32_t>(), ctx->s_sort_tmp.p, tb, s);
+  HIPCHK(hlc::launch_sort_by_session(vsess, n, ctx->s_keys.as<uint32_t>(), ctx->s_iota.as<uint32_t>(),
+                              ctx->s_order.as<uint32_t>(), ctx->s_sort_tmp.p, tb, s));
   CHK(ctx->s_segb.ensure(n_sessions * 4 + 4));
   CHK(ctx->s_sege.ensure(n_sessions * 4 + 4));
   HIPCHK(hipMemsetAsync(ctx->s_segb.p, 0, n_sessions * 4 + 4, s));

@@ -34,6 +34,21 @@
 #define HLC_HD inline
 #endif
 
+// Host test build (-DHLC_FE29_CHECK, tests/test_fe29_host.py): every lazy operation and every
+// 64-bit column accumulation checks its magnitude contract in wider arithmetic and counts a
+// violation instead of silently wrapping.  Compiles to nothing elsewhere.
+#if defined(HLC_FE29_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+extern "C" unsigned long long hlc_fe29_violations;
+#define FE29_CHECK(c)                 \
+  do {                                \
+    if (!(c)) ++hlc_fe29_violations;  \
+  } while (0)
+#else
+#define FE29_CHECK(c) \
+  do {                \
+  } while (0)
+#endif
+
 namespace hlc {
 
 struct fe29 {
@@ -63,7 +78,20 @@ HLC_HD void fe29_set(fe29& r, uint32_t x) {
 // r = a + b (limbwise; see the contract)
 HLC_HD void fe29_add(fe29& r, const fe29& a, const fe29& b) {
 #pragma unroll
-  for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK((uint64_t)a.v[i] + b.v[i] <= 0xFFFFFFFFull);
+    r.v[i] = a.v[i] + b.v[i];
+  }
+}
+
+// r = a << s limbwise, NO carry (lazy 2a / 4a / 8a: a valid MUL operand beside a normalised one
+// while every limb stays < 2^31.8)
+HLC_HD void fe29_shl(fe29& r, const fe29& a, int s) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK(((uint64_t)a.v[i] << s) <= 0xFFFFFFFFull);
+    r.v[i] = a.v[i] << s;
+  }
 }
 
 // one parallel carry step over limbs < 2^32 (no serial chain: every limb at once) with the 2^261
@@ -92,7 +120,10 @@ HLC_HD uint32_t k64(int i) {
 // fe29_carry (-> normalised) and of mul_small(2) (2 r < 2^31.6).  NOT a valid sqr input or `b`.
 HLC_HD void fe29_sub_lazy(fe29& r, const fe29& a, const fe29& b) {
 #pragma unroll
-  for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + k64(i) - b.v[i];
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK((uint64_t)a.v[i] + k64(i) >= b.v[i] && (uint64_t)a.v[i] + k64(i) - b.v[i] <= 0xFFFFFFFFull);
+    r.v[i] = a.v[i] + k64(i) - b.v[i];
+  }
 }
 
 // in-place carry step of a lazy value (limbs < 2^32) -> normalised
@@ -102,7 +133,37 @@ HLC_HD void fe29_norm(fe29& r) { fe29_carry(r.v); }
 HLC_HD void fe29_sub(fe29& r, const fe29& a, const fe29& b) {
   uint32_t d[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) d[i] = a.v[i] + k29(i) - b.v[i];
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK((uint64_t)a.v[i] + k29(i) >= b.v[i] && (uint64_t)a.v[i] + k29(i) - b.v[i] <= 0xFFFFFFFFull);
+    d[i] = a.v[i] + k29(i) - b.v[i];
+  }
+  fe29_carry(d);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = d[i];
+}
+
+// r = a - b - c (mod p), normalised: a + 128 p - b - c, one carry step.  Needs b_i + c_i <= 128p's
+// limbs (>= 2^31 - 5: e.g. two normalised values, or three) and a_i < 2^30.58 (a + 128p < 2^32).
+HLC_HD void fe29_sub2(fe29& r, const fe29& a, const fe29& b, const fe29& c) {
+  uint32_t d[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK((uint64_t)a.v[i] + k29(i) <= 0xFFFFFFFFull && (uint64_t)b.v[i] + c.v[i] <= k29(i));
+    d[i] = a.v[i] + k29(i) - b.v[i] - c.v[i];
+  }
+  fe29_carry(d);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = d[i];
+}
+
+// r = a - b - 2 c (mod p), normalised (same conditions with b_i + 2 c_i <= 128p's limbs)
+HLC_HD void fe29_sub_b2c(fe29& r, const fe29& a, const fe29& b, const fe29& c) {
+  uint32_t d[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK((uint64_t)a.v[i] + k29(i) <= 0xFFFFFFFFull && (uint64_t)b.v[i] + 2ull * c.v[i] <= k29(i));
+    d[i] = a.v[i] + k29(i) - b.v[i] - c.v[i] - c.v[i];
+  }
   fe29_carry(d);
 #pragma unroll
   for (int i = 0; i < 9; ++i) r.v[i] = d[i];
@@ -111,7 +172,10 @@ HLC_HD void fe29_sub(fe29& r, const fe29& a, const fe29& b) {
 HLC_HD void fe29_neg(fe29& r, const fe29& a) {
   uint32_t d[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) d[i] = k29(i) - a.v[i];
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK(a.v[i] <= k29(i));
+    d[i] = k29(i) - a.v[i];
+  }
   fe29_carry(d);
 #pragma unroll
   for (int i = 0; i < 9; ++i) r.v[i] = d[i];
@@ -122,7 +186,10 @@ HLC_HD void fe29_neg(fe29& r, const fe29& a) {
 HLC_HD void fe29_mul_small(fe29& r, const fe29& a, uint32_t m) {
   uint32_t d[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) d[i] = a.v[i] * m;
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK((uint64_t)a.v[i] * m <= 0xFFFFFFFFull);
+    d[i] = a.v[i] * m;
+  }
   fe29_carry(d);
 #pragma unroll
   for (int i = 0; i < 9; ++i) r.v[i] = d[i];
@@ -130,7 +197,12 @@ HLC_HD void fe29_mul_small(fe29& r, const fe29& a, uint32_t m) {
 
 HLC_HD void fe29_dbl(fe29& r, const fe29& a) { fe29_mul_small(r, a, 2); }
 
-HLC_HD uint64_t mad29(uint32_t a, uint32_t b, uint64_t acc) { return (uint64_t)a * b + acc; }
+HLC_HD uint64_t mad29(uint32_t a, uint32_t b, uint64_t acc) {
+#if defined(HLC_FE29_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+  FE29_CHECK((unsigned __int128)a * b + acc <= (unsigned __int128)0xFFFFFFFFFFFFFFFFull);
+#endif
+  return (uint64_t)a * b + acc;
+}
 
 // Shared tail of mul/sqr: H[0..8] = the high columns 9..17 (29-bit, H[8] the final carry), acc the
 // running low column j (already holding the products of column j and the carry of j-1).
@@ -186,7 +258,10 @@ HLC_HD void fe29_mul_ref(fe29& r, const fe29& a, const fe29& b) {
 HLC_HD void fe29_sqr_ref(fe29& r, const fe29& a) {
   uint32_t d[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK(((uint64_t)a.v[i] << 1) <= 0xFFFFFFFFull);
+    d[i] = a.v[i] << 1;
+  }
   uint32_t H[9];
   uint64_t acc = 0;
 #pragma unroll

@@ -1,8 +1,16 @@
-// Host build of hlc_fe29.hpp for the CPU tests (tests/test_fe29_host.py): one C entry point per
-// operation over uint32[9] limb arrays.  Test infrastructure, not part of libhlc.so.
+// Host build of hlc_fe29.hpp / hlc_point29.hpp for the CPU tests (tests/test_fe29_host.py): one C
+// entry point per operation over uint32[9] limb arrays, built with HLC_FE29_CHECK so that every
+// magnitude-contract violation is counted.  Test infrastructure, not part of libhlc.so.
 #include "hlc_fe29.hpp"
+#include "hlc_point29.hpp"
 
 using hlc::fe29;
+using hlc::ge29;
+using hlc::gej29;
+
+extern "C" {
+unsigned long long hlc_fe29_violations = 0;
+}
 
 static fe29 ld(const uint32_t* p) {
   fe29 r;
@@ -35,7 +43,52 @@ void fe29_op(int op, uint64_t n, const uint32_t* a, const uint32_t* b, uint32_t*
       case 9: hlc::fe29_to32(o, u); break;
       case 10: hlc::fe29_sub_lazy(r, u, v); st(o, r); break;
       case 11: r = u; hlc::fe29_norm(r); st(o, r); break;
+      case 12: hlc::fe29_sub2(r, u, v, ld(y + 9 * n)); st(o, r); break;         // a - b - c
+      case 13: hlc::fe29_sub_b2c(r, u, v, ld(y + 9 * n)); st(o, r); break;      // a - b - 2c
     }
+  }
+}
+
+unsigned long long fe29_violations(int reset) {
+  const unsigned long long v = hlc_fe29_violations;
+  if (reset) hlc_fe29_violations = 0;
+  return v;
+}
+
+// Point operations over n items.  Jacobian points are 28 words (x 9, y 9, z 9, inf), affine 18.
+// op 0: r = 2a; 1: r = a + b unchecked (gej29_madd<false>); 2: r = a + b exact; 3: a += b with the
+// z-ratio (out: 28 + 9 words); 4: r = a + b, both Jacobian (b: 28 words).
+void gej29_op(int op, uint64_t n, const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint32_t* x = a + 28 * k;
+    const uint32_t* y = b + (op == 4 ? 28 : 18) * k;
+    uint32_t* o = out + (op == 3 ? 37 : 28) * k;
+    gej29 p, q, res;
+    p.x = ld(x);
+    p.y = ld(x + 9);
+    p.z = ld(x + 18);
+    p.inf = x[27];
+    ge29 g;
+    g.x = ld(y);
+    g.y = ld(y + 9);
+    fe29 zr;
+    switch (op) {
+      case 0: hlc::gej29_double(res, p); break;
+      case 1: hlc::gej29_madd<false>(res, p, g); break;
+      case 2: hlc::gej29_madd<true>(res, p, g); break;
+      case 3: res = p; hlc::gej29_madd_zr(res, g, zr); st(o + 28, zr); break;
+      case 4:
+        q.x = ld(y);
+        q.y = ld(y + 9);
+        q.z = ld(y + 18);
+        q.inf = y[27];
+        hlc::gej29_add(res, p, q);
+        break;
+    }
+    st(o, res.x);
+    st(o + 9, res.y);
+    st(o + 18, res.z);
+    o[27] = res.inf;
   }
 }
 }

@@ -24,7 +24,7 @@ struct Workspace;  // defined in hlc_api.cpp
 // call flags (one device word, cleared by the caller): set by the kernels, read once per call
 constexpr uint32_t FLAG_GENERAL_PATH = 1u;     // some vote exceeds the fused prehash LDS window
 constexpr uint32_t FLAG_LARGE_PROPOSAL = 2u;   // some proposal has > 512 votes (global chain tables)
-void launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv, uint32_t* flags,
+hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv, uint32_t* flags,
                          hipStream_t s);
 void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
                       int mode, uint64_t* sha_sz, uint64_t* kec_sz, hipStream_t s);
@@ -37,7 +37,7 @@ void launch_sha_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, cons
 void launch_keccak_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, const uint8_t* buf,
                           uint32_t* out_digest_words, hipStream_t s);
 // exclusive prefix sum of u64 sizes (hipcub); temp == nullptr queries temp_bytes
-void launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
+hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
                            hipStream_t s);
 // hlc_eth_verify_batch length checks (ethereum.rs:71-82): pre[i] = PRE_PENDING or verify_out set
 void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
@@ -133,7 +133,7 @@ void launch_wire_results(uint64_t nm, const hlc_wire_proposal* wout, hlc_result*
 // ---- streaming votes (hlc_stream.hip) ----
 void launch_sessions_to_props(const hlc_session* ss, uint64_t m, hlc_proposal* props, hipStream_t s);
 // stable sort of vote indices by session; temp == nullptr queries temp_bytes
-void launch_sort_by_session(const uint32_t* vote_session, uint64_t n, uint32_t* keys_out, uint32_t* iota,
+hipError_t launch_sort_by_session(const uint32_t* vote_session, uint64_t n, uint32_t* keys_out, uint32_t* iota,
                             uint32_t* order, void* temp, size_t& temp_bytes, hipStream_t s);
 void launch_segments(const uint32_t* keys, uint64_t n, uint32_t* seg_begin, uint32_t* seg_end, hipStream_t s);
 // duplicate flags: tab (pre-set to ~0), minv (pre-set to ~0) sized mask + 1; slot_of[n], dup[n]

@@ -6,7 +6,6 @@
 // P == Q, P == -Q) are exact, so adversarial signatures (a crafted Q = infinity) match k256.
 #pragma once
 #include "hlc_fe29.hpp"
-#include "hlc_field.hpp"
 
 namespace hlc {
 
@@ -20,72 +19,73 @@ struct ge29 {
 };
 
 // beta (cube root of unity mod p) in radix 2^29
-HLC_DEV void fe29_beta(fe29& r) {
+HLC_HD void fe29_beta(fe29& r) {
   const uint32_t b[9] = {0x119501EEu, 0x09CB6143u, 0x1D626570u, 0x0092EA25u, 0x034E99CFu,
                          0x03CF561Au, 0x1C41B991u, 0x056CAF80u, 0x007AE96Au};
 #pragma unroll
   for (int i = 0; i < 9; ++i) r.v[i] = b[i];
 }
 
-HLC_DEV void gej29_set_inf(gej29& r) {
+HLC_HD void gej29_set_inf(gej29& r) {
   fe29_set(r.x, 0);
   fe29_set(r.y, 1);
   fe29_set(r.z, 0);
   r.inf = 1;
 }
 
-HLC_DEV void gej29_set_ge(gej29& r, const ge29& a) {
+HLC_HD void gej29_set_ge(gej29& r, const ge29& a) {
   r.x = a.x;
   r.y = a.y;
   fe29_set(r.z, 1);
   r.inf = 0;
 }
 
-// dbl-2009-l: 2M + 5S.  (secp256k1 has prime order: no point with y = 0.)  Subtractions that only
-// feed a multiplication by a normalised value, or another subtraction, stay lazy (hlc_fe29.hpp):
-// six carry steps per doubling.
-HLC_DEV void gej29_double(gej29& r, const gej29& a) {
-  fe29 A, B, C, D, D2, E, F, t;
+// dbl-2009-l (a = 0) arranged for lazy reduction: 3M + 4S and three carry steps (one more
+// product than the textbook 2M + 5S, ~110 fewer instructions).  D = 4 X B is ONE product of the
+// doubled operands (2X)(2B), C4 = 4C = (2B)^2, so X3 = F - 2D and Y3 = E (D - X3) - 2 C4 are
+// each one 128p-offset subtraction of two normalised values.  (secp256k1 has prime order: no
+// point with y = 0.)  r may alias a.
+HLC_HD void gej29_double(gej29& r, const gej29& a) {
+  fe29 A, B, X2, B2, D, C4, E, F, Z2, t, M;
   fe29_sqr(A, a.x);
   fe29_sqr(B, a.y);
-  fe29_sqr(C, B);
-  fe29_add(t, a.x, B);
-  fe29_sqr(t, t);
-  fe29_sub_lazy(t, t, A);
-  fe29_sub_lazy(t, t, C);
-  fe29_norm(t);                 // t = 2 X B (normalised)
-  fe29_add(D, t, t);            // D = 2t, lazy (< 2^30.01)
-  fe29_mul_small(D2, t, 4);     // 2D, normalised
-  fe29_mul_small(E, A, 3);
+  fe29_add(X2, a.x, a.x);
+  fe29_add(B2, B, B);
+  fe29_mul(D, X2, B2);          // 4 X B            (2^30.01 x 2^30.01 operands)
+  fe29_sqr(C4, B2);             // 4 Y^4
+  fe29_mul_small(E, A, 3);      // 3 X^2, normalised: it is squared next
   fe29_sqr(F, E);
-  fe29 z2;
-  fe29_add(z2, a.z, a.z);       // 2 Z (< 2^30.01) times normalised Y
-  fe29_mul(r.z, a.y, z2);
-  fe29_sub(r.x, F, D2);
-  fe29_sub_lazy(t, D, r.x);     // D - X3, lazy; times normalised E
-  fe29_mul(r.y, E, t);
-  fe29_mul_small(C, C, 4);      // 4C normalised; Y3 = E (D - X3) - 4C - 4C
-  fe29_sub_lazy(r.y, r.y, C);
-  fe29_sub_lazy(r.y, r.y, C);
-  fe29_norm(r.y);
+  fe29_add(Z2, a.z, a.z);
+  fe29_mul(r.z, a.y, Z2);       // Z3 = 2 Y Z
+  fe29_sub2(r.x, F, D, D);      // X3 = F - 2D
+  fe29_sub_lazy(t, D, r.x);     // D - X3, lazy: multiplies the normalised E
+  fe29_mul(M, E, t);
+  fe29_sub2(r.y, M, C4, C4);    // Y3 = E (D - X3) - 8 Y^4
   r.inf = a.inf;
 }
 
-// r = a + b, b affine (madd-2007-bl: 7M + 4S).  r may alias a.  Eight carry steps (lazy
-// subtractions where the result only feeds a multiplication by a normalised value).
-HLC_DEV void gej29_add_ge(gej29& r, const gej29& a, const ge29& b) {
+// r = a + b, b affine (madd-2007-bl: 8M + 3S, four carry steps).  Z3 = 2 Z1 H as one product;
+// I = 4 HH stays lazy (it only multiplies normalised values); 2V and 2 Y1 J fold into 128p-offset
+// subtractions.  r may alias a.  With zr != nullptr, *zr = Z3 / Z1 = 2H (the R-table build).
+// EXACT = true handles the exceptional cases (a == b: doubling; a == -b: infinity) here.
+// EXACT = false (the hot chains) does NOT test for them: H == 0 gives Z3 == 0, every later Z
+// stays 0 (each step multiplies Z), and the caller tests the chain's final Z once per vote and
+// recomputes the vote with EXACT = true (rec_main29) -- bit-identical results either way.
+template <bool EXACT>
+HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullptr) {
   if (a.inf) {
     gej29_set_ge(r, b);
     return;
   }
-  fe29 z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+  fe29 z1z1, u2, s2, h, rr, hh, i4, j, v, h2, z3, x3, t, y3, y1j;
   fe29_sqr(z1z1, a.z);
   fe29_mul(u2, b.x, z1z1);
   fe29_mul(s2, b.y, a.z);
   fe29_mul(s2, s2, z1z1);
   fe29_sub(h, u2, a.x);
-  fe29_sub_lazy(rr, s2, a.y);
-  if (fe29_is_zero_modp(h)) {
+  fe29_sub_lazy(rr, s2, a.y);      // S2 - Y1, lazy
+  if (EXACT && fe29_is_zero_modp(h)) {
+    fe29_norm(rr);
     if (fe29_is_zero_modp(rr)) {
       gej29_double(r, a);
     } else {
@@ -93,72 +93,35 @@ HLC_DEV void gej29_add_ge(gej29& r, const gej29& a, const ge29& b) {
     }
     return;
   }
+  fe29_mul_small(rr, rr, 2);       // R = 2 (S2 - Y1), normalised: it is squared next
   fe29_sqr(hh, h);
-  fe29_mul_small(i4, hh, 4);
-  fe29_mul(j, h, i4);
-  fe29_mul_small(rr, rr, 2);  // lazy in, normalised out
-  fe29_mul(v, a.x, i4);
-  // z3 = (z1 + h)^2 - z1z1 - hh
-  fe29 z3;
-  fe29_add(z3, a.z, h);
-  fe29_sqr(z3, z3);
-  fe29_sub_lazy(z3, z3, z1z1);
-  fe29_sub_lazy(z3, z3, hh);
-  fe29_norm(z3);
-  // x3 = r^2 - j - 2v
-  fe29 x3;
+  fe29_shl(i4, hh, 2);             // I = 4 HH, lazy (< 2^31.01)
+  fe29_mul(j, h, i4);              // J = H I
+  fe29_mul(v, a.x, i4);            // V = X1 I
+  fe29_add(h2, h, h);
+  fe29_mul(z3, a.z, h2);           // Z3 = 2 Z1 H
+  if (zr) *zr = h2;
   fe29_sqr(x3, rr);
-  fe29_sub_lazy(x3, x3, j);
-  fe29_dbl(t, v);
-  fe29_sub_lazy(x3, x3, t);
-  fe29_norm(x3);
-  // y3 = r (v - x3) - 2 y1 j
-  fe29 y3;
-  fe29_sub_lazy(t, v, x3);
+  fe29_sub_b2c(x3, x3, j, v);      // X3 = R^2 - J - 2V
+  fe29_sub_lazy(t, v, x3);         // V - X3, lazy: multiplies the normalised R
   fe29_mul(y3, rr, t);
-  fe29_mul(t, a.y, j);
-  fe29_dbl(t, t);
-  fe29_sub(y3, y3, t);
+  fe29_add(t, a.y, a.y);
+  fe29_mul(y1j, t, j);             // 2 Y1 J
+  fe29_sub(y3, y3, y1j);           // Y3 = R (V - X3) - 2 Y1 J
   r.x = x3;
   r.y = y3;
   r.z = z3;
   r.inf = 0;
 }
 
+HLC_HD void gej29_add_ge(gej29& r, const gej29& a, const ge29& b) { gej29_madd<true>(r, a, b); }
+
 // a += b (b affine, a finite, a != +-b: the R-table build, where (2i-1)R and 2R are distinct,
 // non-opposite multiples of a point of prime order n); zr = Z(a') / Z(a) = 2H.
-HLC_DEV void gej29_madd_zr(gej29& a, const ge29& b, fe29& zr) {
-  fe29 z1z1, u2, s2, h, hh, i4, j, rr, v, t;
-  fe29_sqr(z1z1, a.z);
-  fe29_mul(u2, b.x, z1z1);
-  fe29_mul(s2, b.y, a.z);
-  fe29_mul(s2, s2, z1z1);
-  fe29_sub(h, u2, a.x);
-  fe29_sub(rr, s2, a.y);
-  fe29_sqr(hh, h);
-  fe29_mul_small(i4, hh, 4);
-  fe29_mul(j, h, i4);
-  fe29_dbl(rr, rr);
-  fe29_mul(v, a.x, i4);
-  fe29_dbl(zr, h);
-  fe29_mul(a.z, a.z, zr);
-  fe29 x3;
-  fe29_sqr(x3, rr);
-  fe29_sub(x3, x3, j);
-  fe29_dbl(t, v);
-  fe29_sub(x3, x3, t);
-  fe29_sub(t, v, x3);
-  fe29 y3;
-  fe29_mul(y3, rr, t);
-  fe29_mul(t, a.y, j);
-  fe29_dbl(t, t);
-  fe29_sub(a.y, y3, t);
-  a.x = x3;
-  a.inf = 0;
-}
+HLC_HD void gej29_madd_zr(gej29& a, const ge29& b, fe29& zr) { gej29_madd<false>(a, a, b, &zr); }
 
 // r = a + b, both Jacobian (add-2007-bl: 11M + 5S).  r may alias a.
-HLC_DEV void gej29_add(gej29& r, const gej29& a, const gej29& b) {
+HLC_HD void gej29_add(gej29& r, const gej29& a, const gej29& b) {
   if (b.inf) {
     r = a;
     return;
@@ -214,14 +177,14 @@ HLC_DEV void gej29_add(gej29& r, const gej29& a, const gej29& b) {
   r.inf = 0;
 }
 
-HLC_DEV void fe29_sqr_n(fe29& r, const fe29& a, int n) {
+HLC_HD void fe29_sqr_n(fe29& r, const fe29& a, int n) {
   r = a;
   for (int i = 0; i < n; ++i) fe29_sqr(r, r);
 }
 
 // r = a^((p+1)/4) (canonical); returns whether r^2 == a (a quadratic residue).  The addition
 // chain of hlc_field.hpp's fe_sqrt (253 S + 13 M).
-HLC_DEV bool fe29_sqrt(fe29& r, const fe29& a) {
+HLC_HD bool fe29_sqrt(fe29& r, const fe29& a) {
   fe29 x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
   fe29_sqr(t, a);
   fe29_mul(x2, t, a);

@@ -963,9 +963,9 @@ inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB);
 
 }  // namespace
 
-void launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
-                           hipStream_t s) {
-  hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
+hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
+                                 hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n, s);
 }
 
 void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
@@ -980,10 +980,14 @@ void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_l
   if (n) hipLaunchKernelGGL(k_verify_pre, dim3(blocks_for(n)), dim3(TPB), 0, s, n, sig_len, id_len, pre, verify_out);
 }
 
-void launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv,
-                         uint32_t* flags, hipStream_t s) {
-  if (nv) hipMemsetAsync(vote_prop, 0xFF, nv * sizeof(uint32_t), s);
+hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv,
+                               uint32_t* flags, hipStream_t s) {
+  if (nv) {
+    const hipError_t e = hipMemsetAsync(vote_prop, 0xFF, nv * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+  }
   if (np) hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np), dim3(TPB), 0, s, props, vote_prop, flags);
+  return hipSuccess;
 }
 
 void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,

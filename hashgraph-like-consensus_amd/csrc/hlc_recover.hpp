@@ -426,6 +426,8 @@ HLC_DEV void load_ge_global29(ge29& g, const uint32_t* t) {
 }
 
 // acc = k G for odd k < 2^256 (neg: acc = -k G), by the comb (see comb_mul_g), in 29-bit limbs.
+// EXACT: see gej29_madd (the fast form leaves exceptional steps to the caller's final-Z test).
+template <bool EXACT>
 HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
   ge29 e;
   load_ge_global29(e, gcomb + GC_TOP_OFF);
@@ -442,14 +444,68 @@ HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
       load_ge_global29(e, comb_entry(gcomb, w + 1, d));
     }
     if ((dc < 0) != neg) fe29_neg(cur.y, cur.y);
-    gej29_add_ge(acc, acc, cur);
+    gej29_madd<EXACT>(acc, acc, cur);
   }
 }
 
-// Main stage for one vote, over the 29-bit unsaturated field layer (hlc_fe29.hpp: ~25% fewer
+// u2 R over the lane's R table (odd multiples 1..31 of R in one common-Z frame, zg = that Z):
+// regular signed digits of the GLV halves b1, b2 (b2 against lambda R = (beta x, y)).
+template <bool EXACT>
+HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const uint32_t* tab, const fe29& zg) {
+  const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
+  const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
+  fe29 beta;
+  fe29_beta(beta);  // wave-uniform: multiplied from SGPRs (fe29_mul_uniform)
+  const uint32_t* dws = rec + (size_t)REC_DIG * stride;
+  gej29_set_inf(acc);
+  // Additions in order (window 25, b1), (25, b2), 5 doublings, (24, b1), ... -- the two halves add
+  // at the same positions (uniform across the wave).  Register pressure, not load latency, bounds
+  // this loop: the b1 entry is loaded before the last doubling of its window (one point operation
+  // ahead) and the b2 entry right after the b1 addition (its latency hidden by the other waves).
+  auto digit_at = [&](int win, int k) {
+    return digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
+  };
+  auto entry_of = [&](int d) { return tab + RTAB_ENTRY * (((d < 0 ? -d : d) - 1) >> 1); };
+#pragma unroll 1
+  for (int win = M_R - 1; win >= 0; --win) {
+    ge29 g;
+    int d = digit_at(win, 0);
+    if (win != M_R - 1) {
+#pragma unroll 1
+      for (int q = 0; q < W_R - 1; ++q) gej29_double(acc, acc);
+      load_ge29_tab(g, entry_of(d));
+      gej29_double(acc, acc);
+    } else {
+      load_ge29_tab(g, entry_of(d));
+    }
+    if ((d < 0) != ((negs & 1) != 0)) fe29_neg(g.y, g.y);
+    gej29_madd<EXACT>(acc, acc, g);
+    d = digit_at(win, 1);
+    load_ge29_tab(g, entry_of(d));
+    fe29_mul_uniform(g.x, g.x, beta);
+    if ((d < 0) != ((negs & 2) != 0)) fe29_neg(g.y, g.y);
+    gej29_madd<EXACT>(acc, acc, g);
+  }
+#pragma unroll 1
+  for (int k = 0; k < 2; ++k) {
+    if (((skews >> k) & 1) == 0) continue;
+    ge29 g;
+    load_ge29_tab(g, tab);
+    if (k == 1) fe29_mul_uniform(g.x, g.x, beta);
+    if (((negs >> k) & 1) == 0) fe29_neg(g.y, g.y);
+    gej29_madd<EXACT>(acc, acc, g);
+  }
+  if (!acc.inf) fe29_mul(acc.z, acc.z, zg);
+}
+
+// Main stage for one vote, over the 29-bit unsaturated field layer (hlc_fe29.hpp: ~24% fewer
 // issue cycles per multiplication than the saturated 8 x 32 layer, profiles/r02_ubench_field29.txt).
 // R = decompress(r, parity), Q = u1 G + u2 R, Q returned in 8 x 32 canonical limbs (x, y, z) for
 // the final stage.  Returns SCHEME_NONE, SCHEME_NO_POINT or SCHEME_INFINITY.
+// The two chains run with the unchecked addition (gej29_madd<false>); an exceptional step (an
+// accumulator equal to +- the added point: never for honest signatures, constructible for crafted
+// ones) leaves a zero Z behind, so one test of both final Z values per vote routes such a vote
+// through the same chains with every step checked.
 HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz,
                        const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
@@ -465,7 +521,6 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
     if (!fe29_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
     if ((int)(R.y.v[0] & 1u) != parity) fe29_neg(R.y, R.y);
   }
-  const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
   const bool neg_g = (flags & 16u) != 0;
   fe29 zg;
   {
@@ -482,6 +537,7 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
     fe29_mul(a.x, R.x, c2);
     fe29_mul(a.y, R.y, c3);
     fe29_set(a.z, 1);
+    a.inf = 0;
     store_ge29_tab(a.x, a.y, tab);
     uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
     for (int i = 1; i < RTAB_N; ++i) {
@@ -506,54 +562,16 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
     }
     fe29_mul(zg, a.z, d.z);
   }
-  fe29 beta;
-  fe29_beta(beta);  // wave-uniform: multiplied from SGPRs (fe29_mul_uniform)
-  const uint32_t* dws = rec + (size_t)REC_DIG * stride;
-  gej29 acc;
-  gej29_set_inf(acc);
-  // Additions in order (window 25, b1), (25, b2), 5 doublings, (24, b1), ... -- the two halves add
-  // at the same positions (uniform across the wave).  Register pressure, not load latency, bounds
-  // this loop: the b1 entry is loaded before the last doubling of its window (one point operation
-  // ahead) and the b2 entry right after the b1 addition (its latency hidden by the other waves).
-  auto digit_at = [&](int win, int k) {
-    return digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
-  };
-  auto entry_of = [&](int d) { return tab + RTAB_ENTRY * (((d < 0 ? -d : d) - 1) >> 1); };
-#pragma unroll 1
-  for (int win = M_R - 1; win >= 0; --win) {
-    ge29 g;
-    int d = digit_at(win, 0);
-    if (win != M_R - 1) {
-#pragma unroll 1
-      for (int q = 0; q < W_R - 1; ++q) gej29_double(acc, acc);
-      load_ge29_tab(g, entry_of(d));
-      gej29_double(acc, acc);
-    } else {
-      load_ge29_tab(g, entry_of(d));
-    }
-    if ((d < 0) != ((negs & 1) != 0)) fe29_neg(g.y, g.y);
-    gej29_add_ge(acc, acc, g);
-    d = digit_at(win, 1);
-    load_ge29_tab(g, entry_of(d));
-    fe29_mul_uniform(g.x, g.x, beta);
-    if ((d < 0) != ((negs & 2) != 0)) fe29_neg(g.y, g.y);
-    gej29_add_ge(acc, acc, g);
-  }
-#pragma unroll 1
-  for (int k = 0; k < 2; ++k) {
-    if (((skews >> k) & 1) == 0) continue;
-    ge29 g;
-    load_ge29_tab(g, tab);
-    if (k == 1) fe29_mul_uniform(g.x, g.x, beta);
-    if (((negs >> k) & 1) == 0) fe29_neg(g.y, g.y);
-    gej29_add_ge(acc, acc, g);
-  }
-  if (!acc.inf) fe29_mul(acc.z, acc.z, zg);
   fe u1;
 #pragma unroll
   for (int i = 0; i < 8; ++i) u1.v[i] = rec[(size_t)(REC_U1 + i) * stride];
-  gej29 ag;
-  comb_mul_g29(ag, u1, neg_g, gcomb);
+  gej29 acc, ag;
+  chain_u2r29<false>(acc, rec, stride, tab, zg);
+  comb_mul_g29<false>(ag, u1, neg_g, gcomb);
+  if ((!acc.inf && fe29_is_zero_modp(acc.z)) || fe29_is_zero_modp(ag.z)) {
+    chain_u2r29<true>(acc, rec, stride, tab, zg);
+    comb_mul_g29<true>(ag, u1, neg_g, gcomb);
+  }
   gej29_add(acc, acc, ag);
   if (acc.inf) return SCHEME_INFINITY;
   fe29_to32(qx.v, acc.x);

@@ -241,15 +241,14 @@ void launch_sessions_to_props(const hlc_session* ss, uint64_t m, hlc_proposal* p
   hipLaunchKernelGGL(k_sessions_to_props, dim3(blocks_for(m)), dim3(TPB), 0, s, ss, m, props);
 }
 
-void launch_sort_by_session(const uint32_t* vote_session, uint64_t n, uint32_t* keys_out, uint32_t* iota,
-                            uint32_t* order, void* temp, size_t& temp_bytes, hipStream_t s) {
-  if (!temp) {
-    hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, vote_session, keys_out, iota, order, (int)n, 0, 32, s);
-    return;
-  }
-  if (!n) return;
+hipError_t launch_sort_by_session(const uint32_t* vote_session, uint64_t n, uint32_t* keys_out, uint32_t* iota,
+                                  uint32_t* order, void* temp, size_t& temp_bytes, hipStream_t s) {
+  if (!temp)
+    return hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, vote_session, keys_out, iota, order, (int)n, 0, 32,
+                                              s);
+  if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_iota, dim3(blocks_for(n)), dim3(TPB), 0, s, iota, n);
-  hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, vote_session, keys_out, iota, order, (int)n, 0, 32, s);
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, vote_session, keys_out, iota, order, (int)n, 0, 32, s);
 }
 
 void launch_segments(const uint32_t* keys, uint64_t n, uint32_t* seg_begin, uint32_t* seg_end, hipStream_t s) {

@@ -167,3 +167,208 @@ def test_lazy_subtraction_chains(lib):
         assert val(m[k]) % P == (va - vb) * ve % P
         assert val(z[k]) % P == (va - vb - vc) % P
         assert val(d[k]) % P == 2 * (va - vb) % P
+
+
+# ---- three-operand subtractions and the point formulas (hlc_point29.hpp) ----
+# Largest limbs of a normalised value: mul/sqr outputs (limb 2 < 2^29 + 2^19) and carry-step
+# outputs (limb 0 < 2^29 + 2^18, limb 1 < 2^29 + 2^12 + 8, others < 2^29 + 8).
+NB = [2**29 + 2**18 - 1, 2**29 + 2**12 + 7, 2**29 + 2**19 - 1] + [2**29 + 7] * 6
+GX = 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798
+GY = 0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8
+
+
+def to_limbs(v):
+    return [(v >> (29 * i)) & M for i in range(8)] + [v >> 232]
+
+
+def nrm_limbs(rnd, n, mode=None):
+    """n limb vectors within the normalised bounds NB: random, all-max, or near-max."""
+    out = np.zeros((n, 9), np.uint32)
+    for k in range(n):
+        m = rnd.random() if mode is None else mode
+        for i in range(9):
+            if m < 0.15:
+                out[k, i] = NB[i]
+            elif m < 0.4:
+                out[k, i] = NB[i] - rnd.randrange(2**12)
+            else:
+                out[k, i] = rnd.randrange(NB[i] + 1)
+    return out
+
+
+@pytest.fixture()
+def checked(lib):
+    lib.fe29_violations.restype = ctypes.c_ulonglong
+    lib.fe29_violations.argtypes = [ctypes.c_int]
+    lib.gej29_op.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.fe29_violations(1)
+    yield lib
+    assert lib.fe29_violations(1) == 0, "magnitude-contract violation in the checked host build"
+
+
+def test_sub2_sub_b2c(checked):
+    rnd = random.Random(6)
+    n = 3000
+    a = nrm_limbs(rnd, n)
+    a[: n // 3] = limbs(rnd, n // 3, int(2**30.58))        # a up to the 128p headroom
+    b, c = nrm_limbs(rnd, n), nrm_limbs(rnd, n)
+    bc = np.concatenate([b, c])
+    o2 = run(checked, 12, a, bc)
+    c3 = nrm_limbs(rnd, n)
+    c3[: n // 2] = nrm_limbs(rnd, n // 2, 0.0)
+    o3 = run(checked, 13, a, np.concatenate([b, c3]))
+    check_normalised(o2)
+    check_normalised(o3)
+    for k in range(n):
+        va, vb, vc, v3 = val(a[k]), val(b[k]), val(c[k]), val(c3[k])
+        assert val(o2[k]) % P == (va - vb - vc) % P
+        assert val(o3[k]) % P == (va - vb - 2 * v3) % P
+
+
+def jac(x, y, z, inf=0):
+    w = np.zeros(28, np.uint32)
+    w[0:9], w[9:18], w[18:27], w[27] = x, y, z, inf
+    return w
+
+
+def runp(lib, op, A, B):
+    A = np.ascontiguousarray(A, np.uint32)
+    B = np.ascontiguousarray(B, np.uint32)
+    out = np.zeros((A.shape[0], 37 if op == 3 else 28), np.uint32)
+    lib.gej29_op(op, A.shape[0], A.ctypes.data, B.ctypes.data, out.ctypes.data)
+    return out
+
+
+def dbl_textbook(X, Y, Z):
+    """dbl-2009-l as polynomials mod p."""
+    A, B = X * X % P, Y * Y % P
+    C = B * B % P
+    D = 2 * ((X + B) ** 2 - A - C) % P
+    E = 3 * A % P
+    F = E * E % P
+    X3 = (F - 2 * D) % P
+    return X3, (E * (D - X3) - 8 * C) % P, 2 * Y * Z % P
+
+
+def madd_textbook(X1, Y1, Z1, x2, y2):
+    """madd-2007-bl as polynomials mod p."""
+    Z1Z1 = Z1 * Z1 % P
+    U2, S2 = x2 * Z1Z1 % P, y2 * Z1 * Z1Z1 % P
+    H = (U2 - X1) % P
+    HH = H * H % P
+    I = 4 * HH % P
+    J, r, V = H * I % P, 2 * (S2 - Y1) % P, X1 * I % P
+    X3 = (r * r - J - 2 * V) % P
+    Y3 = (r * (V - X3) - 2 * Y1 * J) % P
+    Z3 = ((Z1 + H) ** 2 - Z1Z1 - HH) % P
+    return X3, Y3, Z3
+
+
+def test_point_formulas_at_limb_bounds(checked):
+    """Doubling and mixed addition on arbitrary limb vectors at the normalised bounds (the
+    formulas are polynomial maps, so any input tests the arithmetic): values mod p equal the
+    textbook formulas, outputs are normalised, and no intermediate breaks the magnitude contract."""
+    rnd = random.Random(7)
+    n = 1500
+    X, Y, Z = nrm_limbs(rnd, n), nrm_limbs(rnd, n), nrm_limbs(rnd, n)
+    x2, y2 = nrm_limbs(rnd, n), nrm_limbs(rnd, n)
+    A = np.array([jac(X[k], Y[k], Z[k]) for k in range(n)])
+    B = np.concatenate([x2, y2], axis=1)
+    d = runp(checked, 0, A, B)
+    m = runp(checked, 1, A, B)
+    mz = runp(checked, 3, A, B)
+    for o in (d, m, mz):
+        for q in range(3):
+            check_normalised(o[:, 9 * q: 9 * q + 9])
+    for k in range(n):
+        vx, vy, vz = val(X[k]) % P, val(Y[k]) % P, val(Z[k]) % P
+        assert tuple(val(d[k, 9 * q: 9 * q + 9]) % P for q in range(3)) == dbl_textbook(vx, vy, vz), k
+        want = madd_textbook(vx, vy, vz, val(x2[k]) % P, val(y2[k]) % P)
+        assert tuple(val(m[k, 9 * q: 9 * q + 9]) % P for q in range(3)) == want, k
+        assert tuple(val(mz[k, 9 * q: 9 * q + 9]) % P for q in range(3)) == want, k
+        assert val(mz[k, 28:37]) % P == 2 * ((val(x2[k]) * vz * vz - vx) % P) % P  # zr = 2H
+
+
+def ec_add(p1, p2):
+    if p1 is None:
+        return p2
+    if p2 is None:
+        return p1
+    (x1, y1), (x2, y2) = p1, p2
+    if x1 == x2:
+        if (y1 + y2) % P == 0:
+            return None
+        lam = 3 * x1 * x1 * pow(2 * y1, -1, P) % P
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, P) % P
+    x3 = (lam * lam - x1 - x2) % P
+    return x3, (lam * (x1 - x3) - y1) % P
+
+
+def ec_mul(k, pt=(GX, GY)):
+    acc = None
+    while k:
+        if k & 1:
+            acc = ec_add(acc, pt)
+        pt = ec_add(pt, pt)
+        k >>= 1
+    return acc
+
+
+def affine(o):
+    if o[27]:
+        return None
+    z = val(o[18:27]) % P
+    if z == 0:
+        return "Z=0"
+    zi = pow(z, -1, P)
+    return val(o[0:9]) * zi * zi % P, val(o[9:18]) * zi * zi * zi % P
+
+
+def test_point_ops_on_curve_and_exceptional(checked):
+    """Group law on real points (random Jacobian Z), the exceptional cases of the exact addition
+    (a == b: doubling, a == -b: infinity, a = infinity), and the unchecked addition's zero Z."""
+    rnd = random.Random(8)
+    rows_a, rows_b, want_d, want_m, kinds = [], [], [], [], []
+    for k in range(120):
+        p1 = ec_mul(rnd.getrandbits(40) + 1)
+        kind = k % 4          # 0: generic, 1: b == a, 2: b == -a, 3: a = infinity
+        p2 = ec_mul(rnd.getrandbits(40) + 1) if kind in (0, 3) else (p1 if kind == 1 else (p1[0], P - p1[1]))
+        z = rnd.randrange(1, P)
+        A = jac(to_limbs(p1[0] * z * z % P), to_limbs(p1[1] * z * z * z % P), to_limbs(z), 1 if kind == 3 else 0)
+        rows_a.append(A)
+        rows_b.append(np.concatenate([to_limbs(p2[0]), to_limbs(p2[1])]).astype(np.uint32))
+        want_d.append(ec_add(p1, p1))
+        want_m.append(p2 if kind == 3 else ec_add(p1, p2))
+        kinds.append(kind)
+    A, B = np.array(rows_a), np.array(rows_b)
+    d, me, mf = runp(checked, 0, A, B), runp(checked, 2, A, B), runp(checked, 1, A, B)
+    for k in range(len(kinds)):
+        if kinds[k] != 3:
+            assert affine(d[k]) == want_d[k]
+        assert affine(me[k]) == want_m[k], (k, kinds[k])
+        if kinds[k] in (1, 2):
+            assert affine(mf[k]) == "Z=0"   # unchecked form: the exceptional step leaves Z = 0
+        else:
+            assert affine(mf[k]) == want_m[k]
+
+
+def test_point_chains(checked):
+    """Natural magnitudes: 40 rounds of (5 doublings, 2 additions) from random points, the shape
+    of the u2 R chain, stay within the contract and match the affine group law."""
+    rnd = random.Random(9)
+    n = 24
+    pts = [ec_mul(rnd.getrandbits(32) + 1) for _ in range(n)]
+    adds = [ec_mul(rnd.getrandbits(32) + 1) for _ in range(n)]
+    A = np.array([jac(to_limbs(p[0]), to_limbs(p[1]), to_limbs(1)) for p in pts])
+    B = np.array([np.concatenate([to_limbs(q[0]), to_limbs(q[1])]) for q in adds], np.uint32)
+    cur = list(pts)
+    for _ in range(40):
+        for _ in range(5):
+            A = runp(checked, 0, A, B)
+            cur = [ec_add(p, p) for p in cur]
+        for _ in range(2):
+            A = runp(checked, 1, A, B)
+            cur = [ec_add(p, q) for p, q in zip(cur, adds)]
+    for k in range(n):
+        assert affine(A[k]) == cur[k]

@@ -1,21 +1,36 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 PMC CSVs of tools/profile.sh per kernel (sum over dispatches, per dispatch)."""
-import csv, collections, glob, sys
+"""Per-kernel averages of rocprofv3 PMC passes (tools/profile.sh output): one line per kernel and
+counter, averaged over its launches.  Usage: pmc_summary.py <prof dir> [kernel-substring ...]"""
+import collections
+import csv
+import os
+import re
+import sys
 
-root = sys.argv[1]
-for f in sorted(glob.glob(f"{root}/pmc_*/run_counter_collection.csv")):
-    agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
-    meta = {}
-    for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].replace("hlc::(anonymous namespace)::", "").split("(")[0]
-        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        disp[k].add(r["Dispatch_Id"])
-        meta[k] = f"vgpr={r['VGPR_Count']} sgpr={r['SGPR_Count']} scratch={r['Scratch_Size']} lds={r['LDS_Block_Size']} grid={r['Grid_Size']}"
-    print("==", f.split("/")[-2])
-    for k in sorted(agg, key=lambda k: -sum(agg[k].values())):
-        if not any(x in k for x in ("recover", "prehash", "chain", "tables")):
+
+def kernel_short(name: str) -> str:
+    m = re.search(r"::(k_\w+)\(", name)
+    return m.group(1) if m else name.split("(")[0][-40:]
+
+
+def summarize(d: str, only=()):
+    out = collections.defaultdict(dict)
+    for sub in sorted(os.listdir(d)):
+        f = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(f):
             continue
-        nd = len(disp[k])
-        vals = " ".join(f"{c}={v / nd:.4g}" for c, v in sorted(agg[k].items()))
-        print(f"  {k} [{nd} dispatches, {meta[k]}] per dispatch: {vals}")
+        acc = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(f)):
+            acc[kernel_short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, cs in acc.items():
+            if only and not any(o in k for o in only):
+                continue
+            for c, v in cs.items():
+                out[k][c] = (sum(v) / len(v), len(v))
+    return out
+
+
+if __name__ == "__main__":
+    res = summarize(sys.argv[1], sys.argv[2:])
+    for k in sorted(res):
+        print(k, " ".join(f"{c}={v:.4g}(x{n})" for c, (v, n) in sorted(res[k].items())))

@@ -246,6 +246,7 @@ __global__ void __launch_bounds__(TPB, 4) k_dbl29(uint32_t* out, int iters) {
   for (int i = 0; i < 9; ++i) x ^= p.x.v[i] ^ p.y.v[i] ^ p.z.v[i];
   sink(out, x);
 }
+template <bool EXACT>
 __global__ void __launch_bounds__(TPB, 4) k_madd29(uint32_t* out, int iters) {
   gej29 p;
   ge29 q;
@@ -255,7 +256,7 @@ __global__ void __launch_bounds__(TPB, 4) k_madd29(uint32_t* out, int iters) {
   seed29(q.x, 13 * threadIdx.x + 7);
   seed29(q.y, 17 * threadIdx.x + 9);
   p.inf = 0;
-  for (int k = 0; k < iters; ++k) gej29_add_ge(p, p, q);
+  for (int k = 0; k < iters; ++k) gej29_madd<EXACT>(p, p, q);
   uint32_t x = 0;
   for (int i = 0; i < 9; ++i) x ^= p.x.v[i] ^ p.y.v[i] ^ p.z.v[i];
   sink(out, x);
@@ -346,7 +347,8 @@ int main(int argc, char** argv) {
            {"fe29_sqr x2 sep", run(k_sqr29x2<0>, d, blocks, iters), 2},
            {"fe29_sqr2 dual", run(k_sqr29x2<1>, d, blocks, iters), 2},
            {"gej29_double", run(k_dbl29, d, blocks, iters), 1},
-           {"gej29_add_ge", run(k_madd29, d, blocks, iters), 1}};
+           {"gej29_madd exact", run(k_madd29<true>, d, blocks, iters), 1},
+           {"gej29_madd fast", run(k_madd29<false>, d, blocks, iters), 1}};
   for (auto& x : r) {
     const double ns = x.ms * 1e6 / iters / x.div;  // per op (div ops per iteration), 4 waves per SIMD
     printf("%-14s %8.3f ms  %8.1f ns/op  %8.1f SIMD-cycles/wave-op @%.2f GHz\n", x.name, x.ms, ns,
