@@ -17,7 +17,8 @@ import numpy as np
 import coracle
 import pyoracle as po
 
-KINDS = ["valid", "flip_rs", "bad_v", "eip155_v", "high_s", "r_range", "s_range", "no_point", "infinity"]
+KINDS = ["valid", "flip_rs", "bad_v", "eip155_v", "high_s", "r_range", "s_range", "no_point", "infinity",
+         "comb_collision"]
 
 
 @dataclass
@@ -51,6 +52,52 @@ def _kg(k: int):
     except OSError:
         pass
     return po.point_mul(k, po.G)
+
+
+def _comb_recode(k: int):
+    """The u1 G comb's regular recoding (hlc_recover.hpp comb_digit): 16 odd digits of 16 bits,
+    least significant first, and the top value (1)."""
+    ds = []
+    for _ in range(16):
+        d = (k & 0x1FFFF) - 0x10000
+        k = (k - d) >> 16
+        ds.append(d)
+    return ds, k
+
+
+def comb_exceptional_window(k: int):
+    """First comb window whose addition is exceptional (accumulator == +- the added multiple of
+    G), or None.  The comb starts from 2^256 G and adds d_w 2^(16 w) G, w = 0..15."""
+    ds, top = _comb_recode(k)
+    acc = top << 256
+    for w, d in enumerate(ds):
+        e = d << (16 * w)
+        if (acc - e) % po.N == 0 or (acc + e) % po.N == 0:
+            return w
+        acc += e
+    return None
+
+
+def _comb_collision_sig(z: int, rnd: random.Random) -> bytes:
+    """A crafted signature whose u1 = -z/r makes the device's u1 G comb hit an exceptional
+    addition (the accumulator equals the added point: a doubling inside the chain).  The
+    partial sum before window w is 2^256 + L_w = (2^256 - n) + L_w (mod n); choosing the low
+    digits L_w = 2^(16 w) - (2^256 - n) and d_w = 1 makes it equal d_w 2^(16 w).  r = -z / u1
+    follows (retried until r is an x-coordinate).  The result is whatever the exact group law
+    gives -- the point is that every implementation must agree on it."""
+    delta = (1 << 256) - po.N
+    while True:
+        w = rnd.randrange(9, 16)
+        hb = 256 - 16 * (w + 1) - 1
+        k = (1 << (16 * w)) - delta + (1 << (16 * w)) + ((rnd.getrandbits(hb) if hb > 0 else 0) << (16 * (w + 1)))
+        if not k & 1 or k >= po.N or comb_exceptional_window(k) is None:
+            continue
+        r = (-z * pow(k, -1, po.N)) % po.N  # u1 = k (odd: the comb's own representative)
+        parity = rnd.randrange(2)
+        if r == 0 or po.decompress(r, bool(parity)) is None:
+            continue
+        s = rnd.randrange(1, po.N // 2)
+        return r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([27 + parity])
 
 
 def make_items(n: int, seed: int) -> List[Item]:
@@ -88,5 +135,7 @@ def make_items(n: int, seed: int) -> List[Item]:
             r = rx % po.N
             s = z * pow(k, -1, po.N) % po.N or 1
             sig = bytearray(r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([27 + (ry & 1)]))
+        elif kind == "comb_collision":
+            sig = bytearray(_comb_collision_sig(z, rnd))
         items.append(Item(privs[i], pays[i], pre[i].tobytes(), bytes(sig), kind))
     return items
