@@ -32,44 +32,108 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
 
 METRIC = "verified votes/sec (ecrecover+chain check) at 1/2/4/8 MI355X vs host CPU"
-# Roofline of the dominant kernel (k_recover, integer-VALU bound, no MFMA): its arithmetic is
-# 32x32->64-bit limb products (v_mad_u64_u32).  Algorithmic work per vote, frozen in SURVEY.md
-# §8(d) before tuning: 2,480 modmul x 136 limb products (canonical 8x32 Montgomery CIOS).
-W_LIMB_PRODUCTS_PER_VOTE = 2480 * 136
-# The implemented algorithm needs fewer (GLV + regular windows, 16-bit G comb, pseudo-Mersenne
-# fold): DESIGN.md §5 counts its field operations -> reported beside, never as `achieved`.
-W_IMPL_LIMB_PRODUCTS_PER_VOTE = 129_328
-# Peak: v_mad_u64_u32 is quarter rate -- 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz
-# (profiles/r01_ubench_int.txt measures 35.6 T/s).
-MAD_PEAK_T_PER_S = 256 * 4 * 16 * 2.4e9 / 1e12
-# rocprofv3 PMC passes of this same bench command (tools/profile.sh), committed under profiles/:
-# `traffic` = memory-side bytes per k_recover launch from FETCH_SIZE / WRITE_SIZE (KiB), with the
-# gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes).
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r01_rocprof_v13_s7")
+# Roofline constants frozen in roofline.json: the recovery is
+# integer-VALU bound (no MFMA); W = 337,280 limb products per vote (canonical 8x32 CIOS
+# ecrecover), peak = 39.3 T limb products/s (v_mad_u64_u32 at quarter rate, 2.4 GHz).
+with open(os.path.join(ROOT, "roofline.json")) as _f:
+    ROOFLINE = json.load(_f)
+W_LIMB_PRODUCTS_PER_VOTE = ROOFLINE["W"]["limb_products_per_vote"]
+MAD_PEAK_T_PER_S = ROOFLINE["peak"]["limb_products_T_per_s"]
+W_IMPL_LIMB_PRODUCTS_PER_VOTE = ROOFLINE["implementation"]["limb_products_per_vote"]
+# rocprofv3 passes of this bench (tools/profile.sh), committed under profiles/: kernel-trace
+# summary, FETCH_SIZE / WRITE_SIZE and the VALU / wave counters of the recovery kernels.
+PMC_PROFILE = os.path.join(ROOT, ROOFLINE["profile"])
+REC_KERNELS = ("k_rec_prep", "k_rec_main", "k_rec_final")
 
 
-def pmc_traffic(kernel: str = "k_recover"):
-    """Per-launch (fetch, write, total) bytes of `kernel` from the committed PMC passes, or None."""
+def _pmc_rows(name: str):
     import csv
-
-    def per_launch(name: str, counter: str):
-        path = os.path.join(PMC_PROFILE, name)
+    path = os.path.join(PMC_PROFILE, name, "run_counter_collection.csv")
+    if not os.path.exists(path):
+        path = os.path.join(PMC_PROFILE, name + ".csv")
         if not os.path.exists(path):
-            return None
-        vals = []
-        with open(path, newline="") as f:
-            for row in csv.DictReader(f):
-                if f"::{kernel}(" in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                    vals.append(float(row["Counter_Value"]))
-        return sum(vals) / len(vals) * 1024.0 if vals else None
+            return []
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
 
-    fetch = per_launch("pmc_fetch.csv", "FETCH_SIZE")
-    write = per_launch("pmc_write.csv", "WRITE_SIZE")
-    if fetch is None or write is None:
+
+def pmc_per_launch(name: str, counter: str, kernel: str):
+    """Average per launch of `counter` for `kernel` in the committed PMC pass `name`, or None."""
+    vals = [float(r["Counter_Value"]) for r in _pmc_rows(name)
+            if f"::{kernel}(" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    return sum(vals) / len(vals) if vals else None
+
+
+def pmc_duration_ms(name: str, kernel: str):
+    """Average duration of `kernel` during the PMC pass `name` (its own dispatch timestamps)."""
+    seen, durs = set(), []
+    for r in _pmc_rows(name):
+        if f"::{kernel}(" in r["Kernel_Name"] and r["Dispatch_Id"] not in seen:
+            seen.add(r["Dispatch_Id"])
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    return sum(durs) / len(durs) if durs else None
+
+
+def pmc_traffic():
+    """Per-launch memory-side bytes of the recovery kernels from the committed FETCH_SIZE /
+    WRITE_SIZE passes (KiB), FETCH doubled per the gfx950 note of MI355X_MICROARCH.md (exact for
+    16-B-per-lane streams; the per-lane table gathers are uncalibrated, so `fetch_raw_bytes` is
+    given beside it), or None."""
+    out = {}
+    for k in REC_KERNELS:
+        f = pmc_per_launch("pmc_fetch", "FETCH_SIZE", k)
+        w = pmc_per_launch("pmc_write", "WRITE_SIZE", k)
+        if f is None or w is None:
+            return None
+        out[k] = {"fetch_raw_bytes": f * 1024.0, "fetch_bytes": 2.0 * f * 1024.0, "write_bytes": w * 1024.0}
+    tot = {key: sum(v[key] for v in out.values()) for key in ("fetch_raw_bytes", "fetch_bytes", "write_bytes")}
+    tot["bytes"] = tot["fetch_bytes"] + tot["write_bytes"]
+    tot["per_kernel"] = out
+    tot["source"] = os.path.relpath(PMC_PROFILE, ROOT)
+    return tot
+
+
+def valu_figures(votes: int):
+    """Measured VALU figures of k_rec_main from the committed PMC pass: lane-instructions per vote,
+    and the issue fraction = SQ_INSTS_VALU per SIMD x the hot point operations' measured issue
+    cycles per instruction (tools/ubench_field.hip, roofline.json) / the kernel's own cycles
+    (GRBM_GUI_ACTIVE per XCD) -- clock-independent; the kernel's sustained clock is given beside."""
+    insts = {k: pmc_per_launch("pmc_valu", "SQ_INSTS_VALU", k) for k in REC_KERNELS}
+    grbm = pmc_per_launch("pmc_valu", "GRBM_GUI_ACTIVE", "k_rec_main")
+    dur = pmc_duration_ms("pmc_valu", "k_rec_main")
+    if insts["k_rec_main"] is None or not grbm or not dur:
         return None
-    fetch *= 2.0  # gfx950: FETCH_SIZE reports half the bytes of 128-B requests
-    return {"fetch_bytes": fetch, "write_bytes": write, "bytes": fetch + write,
-            "source": os.path.relpath(PMC_PROFILE, ROOT)}
+    hot = ROOFLINE["implementation"]["hot_op_issue"]
+    simds, xcds = 256 * 4, 8
+    cycles = grbm / xcds
+    issue = insts["k_rec_main"] / simds * hot["cycles_per_wave_instruction"]
+    pv = ROOFLINE["profile_votes_per_launch"]
+    return {
+        "valu_instr_per_vote": {k: v * 64.0 / pv for k, v in insts.items() if v is not None},
+        "valu_issue_frac": issue / cycles,
+        "kernel_sclk_GHz": cycles / (dur * 1e6),
+        "valu_issue_basis": (f"k_rec_main: SQ_INSTS_VALU {insts['k_rec_main']:.4g}/launch / {simds} SIMDs x "
+                             f"{hot['cycles_per_wave_instruction']} cycles/instruction ({hot['source']}) / "
+                             f"{cycles:.4g} cycles (GRBM_GUI_ACTIVE per XCD, {dur:.3f} ms under PMC, "
+                             f"{os.path.relpath(PMC_PROFILE, ROOT)})"),
+    }
+
+
+def rocprof_kernel_ms():
+    """Average durations (ms) of the recovery kernels in the committed kernel-trace summary."""
+    import csv
+    path = os.path.join(PMC_PROFILE, "trace", "run_kernel_stats.csv")
+    if not os.path.exists(path):
+        return None
+    out = {}
+    with open(path, newline="") as f:
+        for r in csv.DictReader(f):
+            for k in REC_KERNELS:
+                if f"::{k}(" in r["Name"]:
+                    out[k] = float(r["AverageNs"]) / 1e6
+    if len(out) == len(REC_KERNELS):
+        out["sum"] = sum(out[k] for k in REC_KERNELS)
+    return out
 
 
 def cpu_model() -> str:
@@ -264,6 +328,28 @@ def stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, Device
     }
 
 
+def e2e_leg(eng, w, args, np):
+    """Secondary line: the same workload through the host-buffer entry hlc_validate_proposals
+    (inputs copied host -> HBM over PCIe, results copied back, blocking): what a caller holding the
+    votes in host memory sees.  Never the headline value (inputs are not HBM-resident)."""
+    b, d = w.batch, w.desc
+    bytes_in = int(b.arena.nbytes + b.vote_id.nbytes + b.proposal_id.nbytes + b.timestamp.nbytes + b.vote.nbytes
+                   + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
+    eng.validate_proposals(b, d, w.now, want_votes=True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, vst, _, _ = eng.validate_proposals(b, d, w.now, want_votes=True)
+    el = time.perf_counter() - t0
+    assert (vst == 0).all() and (res["status"] == 0).all()
+    return {
+        "metric": "verified votes/s, host buffers in and out (PCIe-inclusive hlc_validate_proposals)",
+        "value": b.n * args.steps / el,
+        "unit": "votes/s",
+        "ms_per_call": el / args.steps * 1e3,
+        "bytes_in_per_call": bytes_in,
+    }
+
+
 CONFIG4_PROPOSALS = 1_562_500   # SURVEY.md §8d config 4: 100,000,000 votes = 1,562,500 x 64
 CONFIG4_SHARDS = 8               # sharded by proposal over one 8-GPU node
 
@@ -290,6 +376,7 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-bytes leg (device protobuf decode)")
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming process_incoming_vote leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     args = ap.parse_args()
 
     import numpy as np
@@ -353,6 +440,7 @@ def main() -> int:
 
     eng.set_kernel_timing(True)
     eng.take_kernel_time()
+    eng.take_chain_time()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -364,6 +452,7 @@ def main() -> int:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     rec_ms, rec_n, call_ms, calls = eng.take_kernel_time()
+    chain_ms, chain_n = eng.take_chain_time()
     eng.set_kernel_timing(False)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -384,7 +473,11 @@ def main() -> int:
     value = votes_per_step * args.steps / elapsed
     rec_avg_s = rec_ms / max(rec_n, 1) / 1e3
     achieved = W_LIMB_PRODUCTS_PER_VOTE * db.n / rec_avg_s / 1e12
-    traffic = pmc_traffic("k_recover")
+    traffic = pmc_traffic()
+    valu = valu_figures(db.n)
+    chain_avg_s = chain_ms / max(chain_n, 1) / 1e3
+    ct = ROOFLINE["chain_tally"]
+    chain_bytes = ct["bytes_per_vote"] * db.n + ct["bytes_per_proposal"] * P
     if config == 2:
         workload = (f"config2: {P} proposals x {V} voters (Gossipsub, n={V}) per GPU, full from_proposal validation"
                     if (P, V) == (10_000, 64) else
@@ -418,25 +511,40 @@ def main() -> int:
         "counters_per_step": counters,
         "roofline": {
             "bound": "valu",
-            "kernel": "k_recover",
+            "kernel": "recovery: k_rec_prep + k_rec_main + k_rec_final (one HIP-event bracket on the launch stream)",
             "achieved": achieved,
             "peak": MAD_PEAK_T_PER_S,
             "unit": "T limb-products/s (32x32->64, v_mad_u64_u32)",
             "frac": achieved / MAD_PEAK_T_PER_S,
             "traffic": traffic["bytes"] if traffic else None,
+            "traffic_per_vote": traffic["bytes"] / ROOFLINE["profile_votes_per_launch"] if traffic else None,
             "traffic_detail": traffic,
             "work_per_vote": W_LIMB_PRODUCTS_PER_VOTE,
-            "work_source": "SURVEY.md 8(d): 2,480 modmul x 136 limb products (canonical algorithm)",
+            "work_source": "roofline.json W (SURVEY.md 8(d): 2,480 modmul x 136 limb products, canonical algorithm)",
             "impl_work_per_vote": W_IMPL_LIMB_PRODUCTS_PER_VOTE,
             "impl_mad_pipe_frac": W_IMPL_LIMB_PRODUCTS_PER_VOTE * db.n / rec_avg_s / 1e12 / MAD_PEAK_T_PER_S,
+            "valu_instr_per_vote": valu["valu_instr_per_vote"] if valu else None,
+            "valu_issue_frac": valu["valu_issue_frac"] if valu else None,
+            "valu_issue_basis": valu["valu_issue_basis"] if valu else None,
+            "kernel_sclk_GHz": valu["kernel_sclk_GHz"] if valu else None,
             "kernel_ms_avg": rec_avg_s * 1e3,
             "kernel_launches": rec_n,
+            "rocprof_kernel_ms": rocprof_kernel_ms(),
             "call_ms_avg": call_ms / max(calls, 1),
             "kernel_share_of_step": rec_ms / max(call_ms, 1e-9),
         },
+        "chain_tally": {
+            "what": "chain check + duplicate detection + tally kernels (utils.rs:175-286, session.rs:253-298), "
+                    "HIP-event bracket per call",
+            "ms_per_call": chain_avg_s * 1e3,
+            "bytes_per_call": chain_bytes,
+            "GBps": chain_bytes / max(chain_avg_s, 1e-12) / 1e9,
+            "bytes_model": ct["source"],
+        },
         "gen_seconds": t_gen,
     }
-    need_host = world == 1 and ((not args.no_wire) or (not args.no_stream) or (rank == 0 and not args.no_cpu_baseline))
+    need_host = world == 1 and ((not args.no_wire) or (not args.no_stream) or (not args.no_e2e) or
+                                (rank == 0 and not args.no_cpu_baseline))
     w = None
     if need_host:
         hb, hd, _ = db.to_host()
@@ -444,6 +552,8 @@ def main() -> int:
     if w is not None and not args.no_wire:
         out["wire"] = wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire,
                                elapsed / args.steps)
+    if w is not None and not args.no_e2e:
+        out["end_to_end"] = e2e_leg(eng, w, args, np)
     if w is not None and not args.no_stream:
         out["stream"] = stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -80,7 +80,7 @@ struct hlc_ctx {
   // measurement hooks
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, call_ev;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, call_ev, chain_ev;
   hipEvent_t take_event() {
     if (ev_pool.empty()) {
       hipEvent_t e = nullptr;
@@ -95,6 +95,7 @@ struct hlc_ctx {
     for (auto e : ev_pool) (void)hipEventDestroy(e);
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : chain_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   }
   DBuf vote_prop, sha_sz, sha_off, kec_sz, kec_off, sha_buf, kec_buf, sha_dig, kec_dig, pre, pre_reason,
       verify, status, reason, chain_code, chain_tab, dup_tab, red, scan_tmp, totals, flag;
@@ -256,6 +257,12 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   while (cap < 2 * n) cap <<= 1;
   CHK(c->chain_tab.ensure(cap * 4));
   CHK(c->dup_tab.ensure(cap * 4));
+  hipEvent_t ch0 = nullptr, ch1 = nullptr;
+  if (c->timing) {  // chain check + duplicate detection + tally bracket
+    ch0 = c->take_event();
+    ch1 = c->take_event();
+    HIPCHK(hipEventRecord(ch0, s));
+  }
   hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
                      c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->flag.as<uint32_t>(), s);
   hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
@@ -265,6 +272,8 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
   HIPCHK(hipGetLastError());
   if (c->timing) {
+    HIPCHK(hipEventRecord(ch1, s));
+    c->chain_ev.emplace_back(ch0, ch1);
     HIPCHK(hipEventRecord(call1, s));
     c->call_ev.emplace_back(call0, call1);
   }
@@ -561,6 +570,27 @@ int hlc_ctx_take_kernel_time(hlc_ctx* ctx, double* recover_ms, uint64_t* recover
     }
     vec->clear();
   }
+  return 0;
+}
+
+int hlc_ctx_take_chain_time(hlc_ctx* ctx, double* chain_ms, uint64_t* launches) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  double sum = 0;
+  for (auto& pr : ctx->chain_ev) {
+    HIPCHK(hipEventSynchronize(pr.second));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+    sum += ms;
+  }
+  if (chain_ms) *chain_ms = sum;
+  if (launches) *launches = ctx->chain_ev.size();
+  for (auto& pr : ctx->chain_ev) {
+    ctx->ev_pool.push_back(pr.first);
+    ctx->ev_pool.push_back(pr.second);
+  }
+  ctx->chain_ev.clear();
   return 0;
 }
 

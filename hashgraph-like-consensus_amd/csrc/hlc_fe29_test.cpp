@@ -57,12 +57,13 @@ unsigned long long fe29_violations(int reset) {
 
 // Point operations over n items.  Jacobian points are 28 words (x 9, y 9, z 9, inf), affine 18.
 // op 0: r = 2a; 1: r = a + b unchecked (gej29_madd<false>); 2: r = a + b exact; 3: a += b with the
-// z-ratio (out: 28 + 9 words); 4: r = a + b, both Jacobian (b: 28 words).
+// z-ratio (out: 28 + 9 words); 4: r = a + b, both Jacobian (b: 28 words); 5: co-Z a += b with
+// b updated (a, b share an implicit Z; out: a.x, a.y, zr, then b.x, b.y: 46 words).
 void gej29_op(int op, uint64_t n, const uint32_t* a, const uint32_t* b, uint32_t* out) {
   for (uint64_t k = 0; k < n; ++k) {
     const uint32_t* x = a + 28 * k;
     const uint32_t* y = b + (op == 4 ? 28 : 18) * k;
-    uint32_t* o = out + (op == 3 ? 37 : 28) * k;
+    uint32_t* o = out + (op == 3 ? 37 : op == 5 ? 46 : 28) * k;
     gej29 p, q, res;
     p.x = ld(x);
     p.y = ld(x + 9);
@@ -77,6 +78,20 @@ void gej29_op(int op, uint64_t n, const uint32_t* a, const uint32_t* b, uint32_t
       case 1: hlc::gej29_madd<false>(res, p, g); break;
       case 2: hlc::gej29_madd<true>(res, p, g); break;
       case 3: res = p; hlc::gej29_madd_zr(res, g, zr); st(o + 28, zr); break;
+      case 5:  // co-Z addition: a (affine words of p, same implicit Z as b) += b, b rescaled
+        res = p;
+        {
+          ge29 a2;
+          a2.x = p.x;
+          a2.y = p.y;
+          hlc::gej29_zaddu(a2, g, zr);
+          res.x = a2.x;
+          res.y = a2.y;
+          res.z = zr;
+          st(o + 28, g.x);
+          st(o + 37, g.y);
+        }
+        break;
       case 4:
         q.x = ld(y);
         q.y = ld(y + 9);

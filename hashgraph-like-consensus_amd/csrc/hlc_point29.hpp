@@ -120,6 +120,31 @@ HLC_HD void gej29_add_ge(gej29& r, const gej29& a, const ge29& b) { gej29_madd<t
 // non-opposite multiples of a point of prime order n); zr = Z(a') / Z(a) = 2H.
 HLC_HD void gej29_madd_zr(gej29& a, const ge29& b, fe29& zr) { gej29_madd<false>(a, a, b, &zr); }
 
+// Co-Z addition with update (Meloni's ZADDU; 4M + 2S, four carry steps): a and b share one
+// Jacobian Z (not stored).  a <- a + b and b <- b rescaled, both again sharing the new
+// Z' = Z (a.x - b.x); zr = Z' / Z = a.x - b.x.  Builds the R table's odd multiples
+// (2i+1) R = (2i-1) R + 2R with b = 2R; needs a != +-b (distinct, non-opposite multiples of a
+// point of prime order).
+HLC_HD void gej29_zaddu(ge29& a, ge29& b, fe29& zr) {
+  fe29 A, B, C, u, D, t, E, X3, Y3;
+  fe29_sub(zr, a.x, b.x);          // X2 - X1 (normalised: squared next)
+  fe29_sqr(A, zr);
+  fe29_mul(B, b.x, A);             // b.x in the new frame
+  fe29_mul(C, a.x, A);
+  fe29_sub(u, a.y, b.y);           // Y2 - Y1
+  fe29_sqr(D, u);
+  fe29_sub_lazy(t, C, B);
+  fe29_mul(E, b.y, t);             // b.y in the new frame
+  fe29_sub2(X3, D, B, C);          // X3 = (Y2 - Y1)^2 - B - C
+  fe29_sub_lazy(t, B, X3);
+  fe29_mul(Y3, u, t);
+  fe29_sub(Y3, Y3, E);             // Y3 = (Y2 - Y1)(B - X3) - E
+  a.x = X3;
+  a.y = Y3;
+  b.x = B;
+  b.y = E;
+}
+
 // r = a + b, both Jacobian (add-2007-bl: 11M + 5S).  r may alias a.
 HLC_HD void gej29_add(gej29& r, const gej29& a, const gej29& b) {
   if (b.inf) {

@@ -478,10 +478,21 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
     } else {
       load_ge29_tab(g, entry_of(d));
     }
+#ifdef HLC_B2_LATE
     if ((d < 0) != ((negs & 1) != 0)) fe29_neg(g.y, g.y);
     gej29_madd<EXACT>(acc, acc, g);
     d = digit_at(win, 1);
     load_ge29_tab(g, entry_of(d));
+#else
+    // the b2 entry is loaded before the b1 addition: its gather latency hides behind that addition
+    const int d2 = digit_at(win, 1);
+    ge29 g2;
+    load_ge29_tab(g2, entry_of(d2));
+    if ((d < 0) != ((negs & 1) != 0)) fe29_neg(g.y, g.y);
+    gej29_madd<EXACT>(acc, acc, g);
+    g = g2;
+    d = d2;
+#endif
     fe29_mul_uniform(g.x, g.x, beta);
     if ((d < 0) != ((negs & 2) != 0)) fe29_neg(g.y, g.y);
     gej29_madd<EXACT>(acc, acc, g);
@@ -533,19 +544,21 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
     fe29 c2, c3;
     fe29_sqr(c2, d.z);
     fe29_mul(c3, c2, d.z);
-    gej29 a;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve
+    ge29 a;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve (co-Z with dp: Z = 1)
     fe29_mul(a.x, R.x, c2);
     fe29_mul(a.y, R.y, c3);
-    fe29_set(a.z, 1);
-    a.inf = 0;
     store_ge29_tab(a.x, a.y, tab);
     uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
+    // (2i+1) R = (2i-1) R + 2R by co-Z additions (gej29_zaddu: 4M + 2S, 2R rescaled alongside);
+    // entry i lives in frame Z_i = prod_{j <= i} zr_j.
     for (int i = 1; i < RTAB_N; ++i) {
       fe29 zr;
-      gej29_madd_zr(a, dp, zr);
+      gej29_zaddu(a, dp, zr);
       store_ge29_tab(a.x, a.y, tab + RTAB_ENTRY * i);
       store_fe29_ws(zr, zrws + (size_t)(9 * (i - 1)) * ws_stride, ws_stride);
     }
+    // every entry into the last frame (libsecp256k1's ge_table_set_globalz): entry i times
+    // (prod_{j > i} zr_j)^(2, 3); sc ends as prod of all zr = the common Z relative to the iso frame
     fe29 sc;
     fe29_set(sc, 1);
     for (int i = RTAB_N - 2; i >= 0; --i) {
@@ -560,7 +573,7 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
       fe29_mul(e.y, e.y, s3);
       store_ge29_tab(e.x, e.y, tab + RTAB_ENTRY * i);
     }
-    fe29_mul(zg, a.z, d.z);
+    fe29_mul(zg, sc, d.z);
   }
   fe u1;
 #pragma unroll

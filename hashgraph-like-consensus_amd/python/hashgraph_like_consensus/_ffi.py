@@ -130,7 +130,7 @@ EXPORTED_SYMBOLS = (
     "hlc_ctx_create", "hlc_ctx_destroy", "hlc_ctx_reserve", "hlc_last_error", "hlc_abi_version",
     "hlc_compute_vote_hashes", "hlc_eth_verify_batch", "hlc_validate_proposals",
     "hlc_validate_proposals_device", "hlc_eth_address_batch", "hlc_eth_sign_batch",
-    "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_consensus_timeout_batch",
+    "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_ctx_take_chain_time", "hlc_consensus_timeout_batch",
     "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
     "hlc_process_votes", "hlc_process_votes_device", "hlc_synth_arena_bytes", "hlc_synth_votes_device",
 )
@@ -204,6 +204,8 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_ctx_set_kernel_timing.restype = c_int
     lib.hlc_ctx_take_kernel_time.argtypes = [vp, POINTER(ctypes.c_double), u64p, POINTER(ctypes.c_double), u64p]
     lib.hlc_ctx_take_kernel_time.restype = c_int
+    lib.hlc_ctx_take_chain_time.argtypes = [vp, POINTER(ctypes.c_double), u64p]
+    lib.hlc_ctx_take_chain_time.restype = c_int
     _lib = lib
     return lib
 

@@ -258,3 +258,9 @@ class Engine:
         _ffi.check(self.lib.hlc_ctx_take_kernel_time(self.ctx, ctypes.byref(rms), ctypes.byref(rl),
                                                      ctypes.byref(cms), ctypes.byref(cl)))
         return rms.value, rl.value, cms.value, cl.value
+
+    def take_chain_time(self):
+        """-> (chain_ms, launches): chain-check + duplicate + tally kernels since the previous take."""
+        ms, n = ctypes.c_double(), c_uint64()
+        _ffi.check(self.lib.hlc_ctx_take_chain_time(self.ctx, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value

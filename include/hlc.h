@@ -210,12 +210,16 @@ int hlc_abi_version(void);
 
 /* ---- Measurement hooks (bench.py roofline): HIP events on the launch stream ------ */
 /* enable != 0: every validate-many call records hipEvents around the signature-recovery
- * kernel (k_recover) and around the whole call, on the stream the kernels run on. */
+ * kernels (k_rec_prep + k_rec_main + k_rec_final), around the chain/tally kernels and around the
+ * whole call, on the stream the kernels run on. */
 int hlc_ctx_set_kernel_timing(hlc_ctx* ctx, int enable);
 /* Waits for the recorded events, returns the summed device time (ms) and launch count of
- * k_recover and of whole validate-many calls since the previous take, then resets them. */
+ * the recovery and of whole validate-many calls since the previous take, then resets them. */
 int hlc_ctx_take_kernel_time(hlc_ctx* ctx, double* recover_ms, uint64_t* recover_launches,
                              double* call_ms, uint64_t* calls);
+/* The same for the chain-check + duplicate + tally kernels of each validate-many call
+ * (validate_vote_chain, initialize_with_votes and the tally: utils.rs:175-286, session.rs:253-298). */
+int hlc_ctx_take_chain_time(hlc_ctx* ctx, double* chain_ms, uint64_t* launches);
 
 /* ---- Hot-path entry points (host buffers, blocking) ----------------------------- */
 

@@ -372,3 +372,54 @@ def test_point_chains(checked):
             cur = [ec_add(p, q) for p, q in zip(cur, adds)]
     for k in range(n):
         assert affine(A[k]) == cur[k]
+
+
+def test_coz_addition(checked):
+    """gej29_zaddu: (a, b) sharing one Jacobian Z -> (a + b, b) sharing Z (a.x - b.x), the
+    R-table build's step (b = 2R, a = (2i-1)R)."""
+    rnd = random.Random(10)
+    rows_a, rows_b, want = [], [], []
+    for _ in range(100):
+        k = rnd.getrandbits(40) + 3
+        a, b = ec_mul(2 * k - 1), ec_mul(2)
+        z = rnd.randrange(1, P)
+        z2, z3 = z * z % P, z * z * z % P
+        rows_a.append(jac(to_limbs(a[0] * z2 % P), to_limbs(a[1] * z3 % P), to_limbs(0)))
+        rows_b.append(np.concatenate([to_limbs(b[0] * z2 % P), to_limbs(b[1] * z3 % P)]).astype(np.uint32))
+        want.append((ec_add(a, b), b, z))
+    out = runp_coz(checked, np.array(rows_a), np.array(rows_b))
+    for k, (s, b, z) in enumerate(want):
+        zr = val(out[k, 18:27]) % P
+        zn = z * zr % P
+        zi = pow(zn, -1, P)
+        assert (val(out[k, 0:9]) * zi * zi % P, val(out[k, 9:18]) * zi * zi * zi % P) == s
+        assert (val(out[k, 28:37]) * zi * zi % P, val(out[k, 37:46]) * zi * zi * zi % P) == b
+        for q in (0, 9, 18, 28, 37):
+            check_normalised(out[k:k + 1, q:q + 9])
+
+
+def runp_coz(lib, A, B):
+    out = np.zeros((A.shape[0], 46), np.uint32)
+    lib.gej29_op(5, A.shape[0], np.ascontiguousarray(A, np.uint32).ctypes.data,
+                 np.ascontiguousarray(B, np.uint32).ctypes.data, out.ctypes.data)
+    return out
+
+
+def test_coz_addition_at_limb_bounds(checked):
+    rnd = random.Random(11)
+    n = 1500
+    ax, ay, bx, by = (nrm_limbs(rnd, n) for _ in range(4))
+    A = np.array([jac(ax[k], ay[k], np.zeros(9, np.uint32)) for k in range(n)])
+    out = runp_coz(checked, A, np.concatenate([bx, by], axis=1))
+    for q in (0, 9, 18, 28, 37):
+        check_normalised(out[:, q:q + 9])
+    for k in range(n):
+        x1, y1, x2, y2 = val(bx[k]), val(by[k]), val(ax[k]), val(ay[k])
+        zr = (x2 - x1) % P
+        AA = zr * zr % P
+        B, C, D = x1 * AA % P, x2 * AA % P, (y2 - y1) ** 2 % P
+        E = y1 * (C - B) % P
+        X3 = (D - B - C) % P
+        Y3 = ((y2 - y1) * (B - X3) - E) % P
+        got = [val(out[k, q:q + 9]) % P for q in (0, 9, 18, 28, 37)]
+        assert got == [X3, Y3, zr, B, E], k

@@ -35,6 +35,15 @@ __device__ void seed_fe(fe& a, uint32_t s) {
 }
 
 __device__ void sink(uint32_t* out, uint32_t x) { out[blockIdx.x * TPB + threadIdx.x] = x; }
+// shader clock during a kernel: block 0, lane 0 brackets its loop with clock64 (shader clock) and
+// wall_clock64 (100 MHz)
+__device__ unsigned long long g_clk[4];
+__device__ void clk_mark(int k) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    g_clk[2 * k] = clock64();
+    g_clk[2 * k + 1] = wall_clock64();
+  }
+}
 
 __global__ void __launch_bounds__(TPB, 4) k_mul(uint32_t* out, int iters) {
   fe a, b;
@@ -241,7 +250,9 @@ __global__ void __launch_bounds__(TPB, 4) k_dbl29(uint32_t* out, int iters) {
   seed29(p.y, 3 * threadIdx.x + 5);
   seed29(p.z, 11 * threadIdx.x + 2);
   p.inf = 0;
+  clk_mark(0);
   for (int k = 0; k < iters; ++k) gej29_double(p, p);
+  clk_mark(1);
   uint32_t x = 0;
   for (int i = 0; i < 9; ++i) x ^= p.x.v[i] ^ p.y.v[i] ^ p.z.v[i];
   sink(out, x);
@@ -256,7 +267,9 @@ __global__ void __launch_bounds__(TPB, 4) k_madd29(uint32_t* out, int iters) {
   seed29(q.x, 13 * threadIdx.x + 7);
   seed29(q.y, 17 * threadIdx.x + 9);
   p.inf = 0;
+  clk_mark(0);
   for (int k = 0; k < iters; ++k) gej29_madd<EXACT>(p, p, q);
+  clk_mark(1);
   uint32_t x = 0;
   for (int i = 0; i < 9; ++i) x ^= p.x.v[i] ^ p.y.v[i] ^ p.z.v[i];
   sink(out, x);
@@ -361,6 +374,18 @@ int main(int argc, char** argv) {
   const float m29 = run(k_mul29<8>, d, 2 * blocks, iters), s29 = run(k_sqr29<8>, d, 2 * blocks, iters);
   printf("fe29_mul @8w   %8.3f ms  %8.1f SIMD-cycles/wave-op\n", m29, m29 * 1e6 / iters * ghz / 8.0);
   printf("fe29_sqr @8w   %8.3f ms  %8.1f SIMD-cycles/wave-op\n", s29, s29 * 1e6 / iters * ghz / 8.0);
+  // shader clock under the full-chip point-operation loops (the sustained, power-limited clock)
+  for (int which = 0; which < 2; ++which) {
+    if (which == 0) {
+      (void)run(k_dbl29, d, blocks, iters);
+    } else {
+      (void)run(k_madd29<false>, d, blocks, iters);
+    }
+    unsigned long long h[4];
+    CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_clk), sizeof h));
+    printf("%s: sustained shader clock %.3f GHz\n", which ? "gej29_madd fast" : "gej29_double",
+           (double)(h[2] - h[0]) / ((double)(h[3] - h[1]) / 100e6) / 1e9);
+  }
   // one wave per SIMD (one 256-thread block per CU): how much a lone wave loses to latency
   const float d1 = run(k_dbl29, d, cus, iters), d4 = run(k_dbl29, d, blocks, iters);
   printf("gej29_double: 1 wave/SIMD %.3f ms, 4 waves/SIMD %.3f ms (lone-wave speed = %.2f of the 4-wave share)\n",
