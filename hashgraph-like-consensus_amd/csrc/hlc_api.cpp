@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -71,6 +72,7 @@ struct hlc_ctx {
   std::mutex mu;
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
+  int rec_force_exact = 0;  // HLC_REC_FORCE_EXACT=1: every vote through the checked chains (tests)
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
   DBuf in_off2, in_len2, in_off3, in_len3, in_priv;
@@ -212,7 +214,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   }
   hlc::launch_recover(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_SIGNATURE,
                       dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(),
-                      c->rec_lanes, c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s);
+                      c->rec_lanes, c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact);
   if (c->timing) {
     HIPCHK(hipEventRecord(r1, s));
     c->rec_ev.emplace_back(r0, r1);
@@ -486,6 +488,7 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
     return set_err(HLC_ENODEV, std::string("libhlc is built for gfx950, device is ") + prop.gcnArchName);
   hlc_ctx* c = new hlc_ctx();
   c->device = device;
+  if (const char* fx = std::getenv("HLC_REC_FORCE_EXACT")) c->rec_force_exact = std::atoi(fx) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return set_err(HLC_EDEVICE, "stream creation failed");
@@ -910,7 +913,8 @@ int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_
   CHK(ctx->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   hlc::launch_recover(n, ctx->pre.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), dbytes, ctx->in_off3.as<uint64_t>(),
                       ctx->in_off.as<uint64_t>(), 1, ctx->gtab.as<uint32_t>(), ctx->rec_scratch.as<uint32_t>(),
-                      ctx->rec_lanes, ctx->rec_work.as<uint32_t>(), ctx->verify.as<uint8_t>(), drec, s);
+                      ctx->rec_lanes, ctx->rec_work.as<uint32_t>(), ctx->verify.as<uint8_t>(), drec, s,
+                      ctx->rec_force_exact);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_status, ctx->verify.p, n, hipMemcpyDeviceToHost, s));
   if (out_addr) HIPCHK(hipMemcpyAsync(out_addr, drec, n * 20, hipMemcpyDeviceToHost, s));

@@ -63,7 +63,7 @@ void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                     const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride,
                     const uint32_t* gtab, uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work,
-                    uint8_t* verify_out, uint8_t* addr_out, hipStream_t s);
+                    uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0);
 uint64_t recover_grid_lanes();
 uint64_t recover_scratch_words();  // per-lane workspace words of k_rec_main
 uint64_t recover_work_words(uint64_t n);

@@ -72,7 +72,8 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
                                                                      const uint64_t* sig_off, size_t off_stride,
                                                                      const uint32_t* gcomb, uint32_t* scratch,
                                                                      uint64_t lanes, uint8_t* state,
-                                                                     const uint32_t* rec, uint32_t* q) {
+                                                                     const uint32_t* rec, uint32_t* q,
+                                                                     int force_exact) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
   uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tid * RTAB_WORDS;
@@ -91,7 +92,7 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
       qz = acc.z;
     }
 #else
-    const int code = rec_main29(r, rec + i, n, qx, qy, qz, gcomb, ws, lanes, tab);
+    const int code = rec_main29(r, rec + i, n, qx, qy, qz, gcomb, ws, lanes, tab, force_exact != 0);
 #endif
     if (code != SCHEME_NONE) {
       state[i] = (uint8_t)(1 + code);
@@ -182,25 +183,36 @@ __global__ void k_build_fbtab(uint32_t* fb) {
   }
 }
 
-// The u1 G comb of the recovery (hlc_recover.hpp): T[w][j] = (2j+1) 2^(16w) G, affine, and the
-// constant top point 2^256 G.  One thread per entry, from the signing comb fbtab.
+// The u1 G comb of the recovery (hlc_recover.hpp): T[w][j] = (2j+1) 2^(W w) G, affine, and the
+// constant top point 2^(W windows) G.  One thread per entry, from the signing comb fbtab.  A scalar
+// that reaches past 2^256 (the top window, the top point) is reduced mod n first:
+// 2^bit mod n by modular doublings, then m * that by two Montgomery products.
 __global__ void k_build_gcomb(uint32_t* gcomb, const uint32_t* fb) {
   const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t total = (uint64_t)GC_WINDOWS * GC_ENTRIES + 1;
   if (e >= total) return;
+  uint32_t m;
+  int bit;
+  if (e == total - 1) {
+    m = 1u;
+    bit = GC_W * GC_WINDOWS;
+  } else {
+    m = 2u * (uint32_t)(e % GC_ENTRIES) + 1u;  // < 2^W
+    bit = GC_W * (int)(e / GC_ENTRIES);
+  }
   fe k;
   fe_set(k, 0);
-  if (e == total - 1) {
-    // 2^256 mod n = 2^256 - n
-    uint32_t bw = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) k.v[q] = sub_cc(0u, n_limb(q), bw);
-  } else {
-    const int w = (int)(e / GC_ENTRIES), j = (int)(e % GC_ENTRIES);
-    const uint32_t m = 2u * (uint32_t)j + 1u;  // < 2^16
-    const int bit = GC_W * w;
+  if (bit + GC_W <= 256) {
     k.v[bit >> 5] = m << (bit & 31);
-    if ((bit & 31) > 16 && (bit >> 5) < 7) k.v[(bit >> 5) + 1] = m >> (32 - (bit & 31));
+    if ((bit & 31) + GC_W > 32 && (bit >> 5) < 7) k.v[(bit >> 5) + 1] = m >> (32 - (bit & 31));
+  } else {
+    fe s, r2, mm;
+    fe_set(s, 1);
+    for (int i = 0; i < bit; ++i) sc_add(s, s, s);  // 2^bit mod n
+    sc_r2(r2);
+    fe_set(mm, m);
+    sc_mont_mul(mm, mm, r2);  // m R
+    sc_mont_mul(k, mm, s);    // m 2^bit mod n
   }
   gej p;
   fixed_base_mul(p, k, fb);
@@ -263,7 +275,7 @@ uint64_t recover_grid_lanes() {
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                     const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb,
                     uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, uint8_t* verify_out, uint8_t* addr_out,
-                    hipStream_t s) {
+                    hipStream_t s, int force_exact) {
   if (!n) return;
   uint32_t* rec = work;
   uint32_t* q = rec + n * (uint64_t)REC_WORDS;
@@ -276,7 +288,7 @@ void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, co
   uint64_t need = (n + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
   hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, bytes, sig_off, off_stride, gcomb,
-                     scratch, (uint64_t)blocks * REC_TPB, verify_out, rec, q);
+                     scratch, (uint64_t)blocks * REC_TPB, verify_out, rec, q, force_exact);
   hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, L, pre, bytes, id_off, off_stride, verify_out, q, pfx,
                      addr_out);
 }

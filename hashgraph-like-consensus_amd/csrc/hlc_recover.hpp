@@ -31,11 +31,11 @@
 //       table is built on the isomorphic curve y^2 = x^3 + 7 C^6 (C = Z(2R)) and brought to one
 //       common Z ("effective affine", as libsecp256k1's ecmult_odd_multiples_table +
 //       ge_table_set_globalz), so every chain addition is one mixed Jacobian+affine add.
-//   u1 G: a fixed-base comb with NO doublings over a 32 MiB table resident in HBM/MALL:
-//       16 windows of 16 bits, T[w][j] = (2j+1) 2^(16w) G (affine), regular signed digits of
-//       the odd representative of u1 (u1 or n - u1, the sign folded into the digits); the
-//       recoding's top digit is provably 1, so window 16 is the constant start point 2^256 G.
-//       16 mixed additions, each table entry prefetched one window ahead.
+//   u1 G: a fixed-base comb with NO doublings over a table resident in HBM: GC_WINDOWS windows of
+//       GC_W bits (12 x 22), T[w][j] = (2j+1) 2^(W w) G (affine), regular signed digits of the odd
+//       representative of u1 (u1 or n - u1, the sign folded into the digits); the recoding's
+//       top digit is provably 1, so the last window is the constant start point 2^(W windows) G.
+//       GC_WINDOWS mixed additions, each table entry prefetched one window ahead.
 //   Q = (u2 R) + (u1 G) with one Jacobian addition (exceptional cases exact).
 #pragma once
 #include "hlc_hash.hpp"
@@ -71,14 +71,23 @@ constexpr int REC_DIG = 8;                      // 2 x DIG_R_WORDS: int16 digit 
 constexpr int REC_FLAGS = REC_DIG + 2 * DIG_R_WORDS;  // bit 0-1 negs, 2-3 skews, 4 neg_g, 5 parity
 constexpr int REC_WORDS = REC_FLAGS + 1;
 constexpr int Q_WORDS = 24;                     // main -> final: Jacobian X, Y, Z
-constexpr int REC_BATCH = 8;                    // votes per lane (one inversion) in prep / final
+#ifndef HLC_REC_BATCH
+#define HLC_REC_BATCH 8
+#endif
+constexpr int REC_BATCH = HLC_REC_BATCH;        // votes per lane (one inversion) in prep / final
 constexpr uint8_t REC_PENDING = 0xFF;           // verify_out state between the stages
 
-// fixed-base comb for u1 G (global memory, built once per context by k_build_gcomb)
-constexpr int GC_W = 16;                        // bits per window
-constexpr int GC_WINDOWS = 16;                  // 16 x 16 = 256 bits; window 16 is constant
-constexpr int GC_ENTRIES = 1 << (GC_W - 1);     // odd multiples 1 .. 2^16 - 1
-constexpr size_t GC_TOP_OFF = (size_t)GC_WINDOWS * GC_ENTRIES * 16;  // 2^256 G
+// fixed-base comb for u1 G (global memory, built once per context by k_build_gcomb).  Wider
+// windows mean fewer additions per vote and a larger table: W = 22 -> 12 additions over
+// 12 x 2^21 affine points (1.5 GiB in HBM, out of the Infinity Cache; every entry is prefetched
+// one window ahead, so the gather latency hides behind an addition).
+#ifndef HLC_GC_W
+#define HLC_GC_W 22
+#endif
+constexpr int GC_W = HLC_GC_W;                  // bits per window
+constexpr int GC_WINDOWS = (255 + GC_W - 1) / GC_W;  // W * windows >= 255: the recoding's top is 1
+constexpr int GC_ENTRIES = 1 << (GC_W - 1);     // odd multiples 1 .. 2^W - 1
+constexpr size_t GC_TOP_OFF = (size_t)GC_WINDOWS * GC_ENTRIES * 16;  // 2^(W windows) G
 constexpr size_t GCOMB_WORDS = GC_TOP_OFF + 16;
 
 enum { SCHEME_NONE = 0, SCHEME_SIG_LEN = 1, SCHEME_ID_LEN = 2, SCHEME_BAD_PARITY = 3,
@@ -204,10 +213,11 @@ HLC_DEV void load_ge_global(ge& g, const uint32_t* t) {
   g.y.v[4] = d.x; g.y.v[5] = d.y; g.y.v[6] = d.z; g.y.v[7] = d.w;
 }
 
-// One step of the regular recoding of an odd 256-bit x with W = 16, least significant digit
-// first: d = (x mod 2^17) - 2^16 (odd, |d| < 2^16), x = (x - d) / 2^16 (stays odd).
+// One step of the regular recoding of an odd 256-bit x with W = GC_W, least significant digit
+// first: d = (x mod 2^(W+1)) - 2^W (odd, |d| < 2^W), x = (x - d) / 2^W (stays odd).  For
+// x < 2^256 the value left after GC_WINDOWS steps is 1 (W * GC_WINDOWS >= 255).
 HLC_DEV int comb_digit(fe& x) {
-  const int d = (int)(x.v[0] & 0x1FFFFu) - 0x10000;
+  const int d = (int)(x.v[0] & ((2u << GC_W) - 1u)) - (1 << GC_W);
   const uint32_t nd = (uint32_t)(-d);
   const uint32_t ext = d > 0 ? 0xFFFFFFFFu : 0u;
   uint32_t c = 0;
@@ -215,8 +225,8 @@ HLC_DEV int comb_digit(fe& x) {
 #pragma unroll
   for (int i = 1; i < 8; ++i) x.v[i] = adc(x.v[i], ext, c);
 #pragma unroll
-  for (int i = 0; i < 7; ++i) x.v[i] = __builtin_amdgcn_alignbit(x.v[i + 1], x.v[i], 16);
-  x.v[7] = x.v[7] >> 16;
+  for (int i = 0; i < 7; ++i) x.v[i] = __builtin_amdgcn_alignbit(x.v[i + 1], x.v[i], GC_W);
+  x.v[7] = x.v[7] >> GC_W;
   return d;
 }
 
@@ -516,9 +526,10 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
 // The two chains run with the unchecked addition (gej29_madd<false>); an exceptional step (an
 // accumulator equal to +- the added point: never for honest signatures, constructible for crafted
 // ones) leaves a zero Z behind, so one test of both final Z values per vote routes such a vote
-// through the same chains with every step checked.
+// through the same chains with every step checked.  (With the shipped 22-bit comb no such
+// collision exists at all: see DESIGN.md §4.1.  The test stays as the guard.)
 HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz,
-                       const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab) {
+                       const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int parity = (int)((flags >> 5) & 1u);
   ge29 R;
@@ -581,7 +592,9 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
   gej29 acc, ag;
   chain_u2r29<false>(acc, rec, stride, tab, zg);
   comb_mul_g29<false>(ag, u1, neg_g, gcomb);
-  if ((!acc.inf && fe29_is_zero_modp(acc.z)) || fe29_is_zero_modp(ag.z)) {
+  // force_exact (HLC_REC_FORCE_EXACT=1 at context creation): every vote takes the checked
+  // chains -- the GPU tests compare that path with the oracle too
+  if (force_exact || (!acc.inf && fe29_is_zero_modp(acc.z)) || fe29_is_zero_modp(ag.z)) {
     chain_u2r29<true>(acc, rec, stride, tab, zg);
     comb_mul_g29<true>(ag, u1, neg_g, gcomb);
   }

@@ -17,8 +17,7 @@ import numpy as np
 import coracle
 import pyoracle as po
 
-KINDS = ["valid", "flip_rs", "bad_v", "eip155_v", "high_s", "r_range", "s_range", "no_point", "infinity",
-         "comb_collision"]
+KINDS = ["valid", "flip_rs", "bad_v", "eip155_v", "high_s", "r_range", "s_range", "no_point", "infinity"]
 
 
 @dataclass
@@ -54,24 +53,40 @@ def _kg(k: int):
     return po.point_mul(k, po.G)
 
 
+COMB_W = 22                                  # HLC_GC_W of the default build (hlc_recover.hpp)
+COMB_N = (255 + COMB_W - 1) // COMB_W        # windows; the top value is 1 at 2^(W N)
+
+
+def comb_collisions_possible(w: int = COMB_W) -> bool:
+    """Whether any u1 can make the comb add a point equal to +- its accumulator.  Before window
+    j the accumulator is 2^(W N) + L_j (mod n) with L_j odd and |L_j| < 2^(W j); it would have
+    to equal +- d_j 2^(W j) (even, < 2^(W (j+1)) << n).  As integers that needs
+    (2^(W N) mod n) + L_j = d_j 2^(W j): odd + odd = even only when 2^(W N) mod n is odd.  For
+    W = 16 (2^256 mod n, odd) collisions are constructible (`_comb_collision_sig`); for the
+    shipped W = 22 (2^264 mod n, even) none exists, u1 = 0 aside (k = n: unreachable, it needs
+    a prehash == 0 mod n)."""
+    n_win = (255 + w - 1) // w
+    return pow(2, w * n_win, po.N) & 1 == 1
+
+
 def _comb_recode(k: int):
-    """The u1 G comb's regular recoding (hlc_recover.hpp comb_digit): 16 odd digits of 16 bits,
-    least significant first, and the top value (1)."""
+    """The u1 G comb's regular recoding (hlc_recover.hpp comb_digit): COMB_N odd digits of COMB_W
+    bits, least significant first, and the top value (1)."""
     ds = []
-    for _ in range(16):
-        d = (k & 0x1FFFF) - 0x10000
-        k = (k - d) >> 16
+    for _ in range(COMB_N):
+        d = (k & ((2 << COMB_W) - 1)) - (1 << COMB_W)
+        k = (k - d) >> COMB_W
         ds.append(d)
     return ds, k
 
 
 def comb_exceptional_window(k: int):
     """First comb window whose addition is exceptional (accumulator == +- the added multiple of
-    G), or None.  The comb starts from 2^256 G and adds d_w 2^(16 w) G, w = 0..15."""
+    G), or None.  The comb starts from 2^(W N) G and adds d_w 2^(W w) G, w = 0..N-1."""
     ds, top = _comb_recode(k)
-    acc = top << 256
+    acc = top << (COMB_W * COMB_N)
     for w, d in enumerate(ds):
-        e = d << (16 * w)
+        e = d << (COMB_W * w)
         if (acc - e) % po.N == 0 or (acc + e) % po.N == 0:
             return w
         acc += e
@@ -81,15 +96,17 @@ def comb_exceptional_window(k: int):
 def _comb_collision_sig(z: int, rnd: random.Random) -> bytes:
     """A crafted signature whose u1 = -z/r makes the device's u1 G comb hit an exceptional
     addition (the accumulator equals the added point: a doubling inside the chain).  The
-    partial sum before window w is 2^256 + L_w = (2^256 - n) + L_w (mod n); choosing the low
-    digits L_w = 2^(16 w) - (2^256 - n) and d_w = 1 makes it equal d_w 2^(16 w).  r = -z / u1
-    follows (retried until r is an x-coordinate).  The result is whatever the exact group law
-    gives -- the point is that every implementation must agree on it."""
-    delta = (1 << 256) - po.N
+    partial sum before window w is 2^(W N) + L_w = delta + L_w (mod n), delta = 2^(W N) mod n
+    (~2^137); choosing the low digits L_w = 2^(W w) - delta and d_w = 1 makes it equal
+    d_w 2^(W w).  r = -z / u1 follows (retried until r is an x-coordinate).  The result is
+    whatever the exact group law gives -- the point is that every implementation must agree."""
+    assert comb_collisions_possible(), "no comb collision exists for this window width"
+    delta = pow(2, COMB_W * COMB_N, po.N)
+    w_lo = (delta.bit_length() + COMB_W) // COMB_W
     while True:
-        w = rnd.randrange(9, 16)
-        hb = 256 - 16 * (w + 1) - 1
-        k = (1 << (16 * w)) - delta + (1 << (16 * w)) + ((rnd.getrandbits(hb) if hb > 0 else 0) << (16 * (w + 1)))
+        w = rnd.randrange(w_lo, COMB_N - 1)
+        hb = 256 - COMB_W * (w + 1) - 1
+        k = (1 << (COMB_W * w)) - delta + (1 << (COMB_W * w)) + ((rnd.getrandbits(hb) if hb > 0 else 0) << (COMB_W * (w + 1)))
         if not k & 1 or k >= po.N or comb_exceptional_window(k) is None:
             continue
         r = (-z * pow(k, -1, po.N)) % po.N  # u1 = k (odd: the comb's own representative)
@@ -135,7 +152,5 @@ def make_items(n: int, seed: int) -> List[Item]:
             r = rx % po.N
             s = z * pow(k, -1, po.N) % po.N or 1
             sig = bytearray(r.to_bytes(32, "big") + s.to_bytes(32, "big") + bytes([27 + (ry & 1)]))
-        elif kind == "comb_collision":
-            sig = bytearray(_comb_collision_sig(z, rnd))
         items.append(Item(privs[i], pays[i], pre[i].tobytes(), bytes(sig), kind))
     return items

@@ -423,3 +423,14 @@ def test_coz_addition_at_limb_bounds(checked):
         Y3 = ((y2 - y1) * (B - X3) - E) % P
         got = [val(out[k, q:q + 9]) % P for q in (0, 9, 18, 28, 37)]
         assert got == [X3, Y3, zr, B, E], k
+
+
+def test_comb_collision_parity_argument():
+    """tests/crypto_items.comb_collisions_possible: with 16-bit windows (2^256 mod n odd) the
+    crafted construction exists and its windows really collide; with the shipped 22-bit windows
+    (2^264 mod n even) it cannot (the parity argument in its docstring)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import crypto_items as ci
+    assert ci.COMB_W == 22 and not ci.comb_collisions_possible(22)
+    assert ci.comb_collisions_possible(16)
