@@ -113,6 +113,115 @@ __global__ void __launch_bounds__(TPB, 4) k_inv(uint32_t* out, int iters) {
   sink(out, x);
 }
 
+// ---- batch inversion in SIMT: three ways to invert 64 x B values per wave ----
+// (a) k_inv: one inversion per lane (B = 1).
+// (b) k_inv_wavescan: Montgomery's trick ACROSS the 64 lanes (B = 1): inclusive prefix and suffix
+//     products by __shfl_up / __shfl_down (6 steps each), ONE inversion of the wave's product
+//     (every lane runs the same instruction stream), a_i^-1 = P_(i-1) S_(i+1) / prod.
+// (c) k_inv_lanebatch: Montgomery's trick WITHIN each lane over B = 8 values (the recovery's
+//     k_rec_prep / k_rec_final).
+__device__ void shfl_up_fe(fe& r, const fe& a, int d) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = __shfl_up(a.v[i], d, 64);
+}
+__device__ void shfl_down_fe(fe& r, const fe& a, int d) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = __shfl_down(a.v[i], d, 64);
+}
+__device__ void shfl_fe(fe& r, const fe& a, int src) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = __shfl(a.v[i], src, 64);
+}
+__device__ void wave_batch_inv(fe& a) {
+  const int lane = threadIdx.x & 63;
+  fe P = a, S = a, t;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    shfl_up_fe(t, P, d);
+    if (lane >= d) fe_mul(P, P, t);
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    shfl_down_fe(t, S, d);
+    if (lane + d < 64) fe_mul(S, S, t);
+  }
+  fe tot, ti, pe, se;
+  shfl_fe(tot, P, 63);
+  fe_inv(ti, tot);
+  shfl_up_fe(pe, P, 1);
+  shfl_down_fe(se, S, 1);
+  if (lane == 0) fe_set(pe, 1);
+  if (lane == 63) fe_set(se, 1);
+  fe_mul(a, pe, se);
+  fe_mul(a, a, ti);
+}
+__device__ void lane_batch_inv8(fe* a) {
+  fe pre[8], acc;
+  fe_set(acc, 1);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    pre[j] = acc;
+    fe_mul(acc, acc, a[j]);
+  }
+  fe inv;
+  fe_inv(inv, acc);
+#pragma unroll
+  for (int j = 7; j >= 0; --j) {
+    fe t;
+    fe_mul(t, pre[j], inv);
+    fe_mul(inv, inv, a[j]);
+    a[j] = t;
+  }
+}
+__global__ void __launch_bounds__(TPB, 4) k_inv_wavescan(uint32_t* out, int iters) {
+  fe a;
+  seed_fe(a, threadIdx.x + blockIdx.x * TPB);
+  a.v[0] |= 1u;
+  for (int k = 0; k < iters; ++k) wave_batch_inv(a);
+  uint32_t x = 0;
+  for (int i = 0; i < 8; ++i) x ^= a.v[i];
+  sink(out, x);
+}
+__global__ void __launch_bounds__(TPB, 4) k_inv_lanebatch(uint32_t* out, int iters) {
+  fe a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    seed_fe(a[j], threadIdx.x + blockIdx.x * TPB + 977u * j);
+    a[j].v[0] |= 1u;
+  }
+  for (int k = 0; k < iters; ++k) lane_batch_inv8(a);
+  uint32_t x = 0;
+  for (int j = 0; j < 8; ++j)
+    for (int i = 0; i < 8; ++i) x ^= a[j].v[i];
+  sink(out, x);
+}
+// a * a^-1 == 1 for both batch forms (bad lanes counted)
+__global__ void k_check_inv(uint32_t* bad) {
+  fe a, b, one;
+  seed_fe(a, threadIdx.x + blockIdx.x * blockDim.x + 12345u);
+  a.v[0] |= 1u;
+  b = a;
+  wave_batch_inv(b);
+  fe_mul(one, a, b);
+  fe_normalize(one, one);
+  uint32_t d = one.v[0] ^ 1u;
+  for (int i = 1; i < 8; ++i) d |= one.v[i];
+  fe v[8], w[8];
+  for (int j = 0; j < 8; ++j) {
+    seed_fe(v[j], threadIdx.x * 8 + j + 777u);
+    v[j].v[0] |= 1u;
+    w[j] = v[j];
+  }
+  lane_batch_inv8(w);
+  for (int j = 0; j < 8; ++j) {
+    fe_mul(one, v[j], w[j]);
+    fe_normalize(one, one);
+    d |= one.v[0] ^ 1u;
+    for (int i = 1; i < 8; ++i) d |= one.v[i];
+  }
+  if (d) atomicAdd(bad, 1u);
+}
+
 // the same field ops at 8 waves per SIMD (latency vs throughput)
 __global__ void __launch_bounds__(TPB, 8) k_mul8(uint32_t* out, int iters) {
   fe a, b;
@@ -374,6 +483,22 @@ int main(int argc, char** argv) {
   const float m29 = run(k_mul29<8>, d, 2 * blocks, iters), s29 = run(k_sqr29<8>, d, 2 * blocks, iters);
   printf("fe29_mul @8w   %8.3f ms  %8.1f SIMD-cycles/wave-op\n", m29, m29 * 1e6 / iters * ghz / 8.0);
   printf("fe29_sqr @8w   %8.3f ms  %8.1f SIMD-cycles/wave-op\n", s29, s29 * 1e6 / iters * ghz / 8.0);
+  // batch inversion forms: ns per wave per 64 inverted values
+  {
+    const int it = iters / 20;
+    const float ta = run(k_inv, d, blocks, it), tb = run(k_inv_wavescan, d, blocks, it),
+                tc = run(k_inv_lanebatch, d, blocks, it);
+    // 4 waves per SIMD in parallel: SIMD-time per wave-iteration = ms / it / 4
+    printf("batch inversion, SIMD-ns per 64 values: per-lane fe_inv %.1f | wave scan (Montgomery across "
+           "64 lanes, shfl) %.1f | per-lane batch of 8 %.1f\n",
+           ta * 1e6 / it / 4.0, tb * 1e6 / it / 4.0, tc * 1e6 / it / 4.0 / 8.0);
+    CHECK(hipMemset(d, 0, 4));
+    hipLaunchKernelGGL(k_check_inv, dim3(blocks), dim3(TPB), 0, 0, d);
+    uint32_t badi = 0;
+    CHECK(hipMemcpy(&badi, d, 4, hipMemcpyDeviceToHost));
+    printf("batch inversion check: %u bad lanes\n", badi);
+    if (badi) return 1;
+  }
   // shader clock under the full-chip point-operation loops (the sustained, power-limited clock)
   for (int which = 0; which < 2; ++which) {
     if (which == 0) {
