@@ -389,15 +389,24 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # HLC_BENCH_BACKEND=gloo + HLC_BENCH_SAME_GPU=1: a dry run of the N > 1 path with every rank on
+    # GPU 0 and the exchange over gloo on host copies (RCCL refuses two ranks on one GPU); the
+    # driver's multi-GPU runs use the default, RCCL with one GPU per rank
+    backend = os.environ.get("HLC_BENCH_BACKEND", "nccl")
+    gpu = 0 if os.environ.get("HLC_BENCH_SAME_GPU") == "1" else local_rank
     dist = None
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(gpu)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    dev = f"cuda:{local_rank}"
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        else:
+            dist.init_process_group(backend)
+    dev = f"cuda:{gpu}"
+    coll_dev = dev if backend == "nccl" else "cpu"
     config = args.config or (2 if world == 1 else 4)
 
-    eng = Engine(local_rank)
+    eng = Engine(gpu)
     V = args.votes_per_proposal
     if config == 2:
         P = args.proposals or 10_000
@@ -421,13 +430,17 @@ def main() -> int:
     # results all-gathered over RCCL plus an all_reduce(sum) of the verified / rejected-by-code
     # counters; at N = 1 only the local counters
     from hashgraph_like_consensus.parallel import ShardExchange
-    ex = ShardExchange(max_p, world, dev)
+    ex = ShardExchange(max_p, world, coll_dev)
 
     def step():
         eng.validate_proposals_device(db, handle)
         if dist is not None:
-            with torch.cuda.stream(stream):
-                ex(db.results, db.status, P, db.n)
+            if backend == "nccl":
+                with torch.cuda.stream(stream):
+                    ex(db.results, db.status, P, db.n)
+            else:
+                torch.cuda.synchronize()
+                ex(db.results.cpu(), db.status.cpu(), P, db.n)
 
     for _ in range(args.warmup):
         step()
@@ -455,10 +468,10 @@ def main() -> int:
     chain_ms, chain_n = eng.take_chain_time()
     eng.set_kernel_timing(False)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        nt = torch.tensor([db.n], dtype=torch.int64, device=dev)
+        nt = torch.tensor([db.n], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(nt)
         votes_per_step = int(nt.item())
     else:
@@ -505,8 +518,9 @@ def main() -> int:
             "votes_per_proposal": V,
             "votes_per_step_per_gpu": db.n,
             "votes_per_step": votes_per_step,
-            "parallelism": f"proposal-sharded x{world}" + (", RCCL all_gather of results + all_reduce of counters"
-                                                          if world > 1 else ""),
+            "parallelism": f"proposal-sharded x{world}" + (
+                f", {'RCCL' if backend == 'nccl' else backend} all_gather of results + all_reduce of counters"
+                if world > 1 else ""),
         },
         "counters_per_step": counters,
         "roofline": {
@@ -516,7 +530,8 @@ def main() -> int:
             "peak": MAD_PEAK_T_PER_S,
             "unit": "T limb-products/s (32x32->64, v_mad_u64_u32)",
             "frac": achieved / MAD_PEAK_T_PER_S,
-            "traffic": traffic["bytes"] if traffic else None,
+            # per launch of THIS run: the profiled bytes per vote x this launch's votes
+            "traffic": traffic["bytes"] / ROOFLINE["profile_votes_per_launch"] * db.n if traffic else None,
             "traffic_per_vote": traffic["bytes"] / ROOFLINE["profile_votes_per_launch"] if traffic else None,
             "traffic_detail": traffic,
             "work_per_vote": W_LIMB_PRODUCTS_PER_VOTE,
