@@ -94,13 +94,15 @@ HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullp
     return;
   }
   fe29_mul_small(rr, rr, 2);       // R = 2 (S2 - Y1), normalised: it is squared next
+  // (operations ordered so that Z1, H, I die early: register pressure, not latency, bounds the
+  // chains' occupancy)
+  fe29_add(h2, h, h);
+  fe29_mul(z3, a.z, h2);           // Z3 = 2 Z1 H
+  if (zr) *zr = h2;
   fe29_sqr(hh, h);
   fe29_shl(i4, hh, 2);             // I = 4 HH, lazy (< 2^31.01)
   fe29_mul(j, h, i4);              // J = H I
   fe29_mul(v, a.x, i4);            // V = X1 I
-  fe29_add(h2, h, h);
-  fe29_mul(z3, a.z, h2);           // Z3 = 2 Z1 H
-  if (zr) *zr = h2;
   fe29_sqr(x3, rr);
   fe29_sub_b2c(x3, x3, j, v);      // X3 = R^2 - J - 2V
   fe29_sub_lazy(t, v, x3);         // V - X3, lazy: multiplies the normalised R
