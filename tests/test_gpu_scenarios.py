@@ -71,6 +71,36 @@ def test_gpu_config5_byzantine_full_640k(engine):
     res, vst = compare(engine, batch, desc, w.now, "config5-full")
     assert len(set(int(s) for s in vst)) >= 9
     assert (res["status"] != 0).sum() > 9_000
+    _byzantine_rate(engine, batch, desc, w.now, vst)
+
+
+def _byzantine_rate(engine, batch, desc, now, vst, steps=5):
+    """Throughput of the device entry on this Byzantine batch (inputs in HBM, like bench.py's
+    headline): written to $HLC_BYZ_RATE_OUT when set (profiles/r02_byzantine_rate.json).  Votes
+    that fail a check before the signature (empty fields, hash, pid) skip the recovery, as
+    validate_vote returns early (utils.rs:127-171): counted in `pre_signature_rejects`."""
+    import json
+    import time
+    import torch
+    from hashgraph_like_consensus.device import DeviceBatch
+    db = DeviceBatch(batch, desc, now, device="cuda:0")
+    stream = torch.cuda.Stream()
+    engine.validate_proposals_device(db, stream.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(db.status_numpy(), vst)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        engine.validate_proposals_device(db, stream.cuda_stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"metric": "verified votes/s, config 5 (config-2 shape, 1/3 Byzantine votes), inputs in HBM",
+           "value": batch.n * steps / el, "unit": "votes/s", "ms_per_step": el / steps * 1e3, "votes": int(batch.n),
+           "rejected_votes": int((vst != 0).sum()),
+           "pre_signature_rejects": int(np.isin(vst, [2, 3, 4, 5, 6]).sum()), "status_histogram": {int(k): int((vst == k).sum()) for k in set(vst.tolist())}}
+    path = os.environ.get("HLC_BYZ_RATE_OUT")
+    if path:
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
 
 
 def test_gpu_chain_and_duplicate_mutations(engine):
