@@ -169,6 +169,23 @@ HLC_HD void fe29_sub_b2c(fe29& r, const fe29& a, const fe29& b, const fe29& c) {
   for (int i = 0; i < 9; ++i) r.v[i] = d[i];
 }
 
+HLC_HD void fe29_neg(fe29& r, const fe29& a);
+// r = c ? 64p - a : a, branch-free and without a carry step (a limbs <= 64p's, e.g. normalised):
+// a lazy value < 2^30 -- the sign of a gathered table entry's y, which only enters products and
+// lazy subtractions (hlc_point29.hpp).  64p - a == 64p + ~a + 1 (mod 2^32).
+HLC_HD void fe29_cneg_lazy(fe29& r, const fe29& a, bool c) {
+#ifdef HLC_BRANCH_NEG  // A/B: the branchy, carried negation it replaced
+  if (c) fe29_neg(r, a); else r = a;
+  return;
+#endif
+  const uint32_t m = 0u - (uint32_t)c;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK(a.v[i] <= k64(i));
+    r.v[i] = (a.v[i] ^ m) + ((k64(i) + 1u) & m);
+  }
+}
+
 HLC_HD void fe29_neg(fe29& r, const fe29& a) {
   uint32_t d[9];
 #pragma unroll

@@ -45,6 +45,7 @@ void fe29_op(int op, uint64_t n, const uint32_t* a, const uint32_t* b, uint32_t*
       case 11: r = u; hlc::fe29_norm(r); st(o, r); break;
       case 12: hlc::fe29_sub2(r, u, v, ld(y + 9 * n)); st(o, r); break;         // a - b - c
       case 13: hlc::fe29_sub_b2c(r, u, v, ld(y + 9 * n)); st(o, r); break;      // a - b - 2c
+      case 14: hlc::fe29_cneg_lazy(r, u, y[0] != 0); st(o, r); break;            // b[0] ? -a : a
     }
   }
 }

@@ -441,7 +441,7 @@ template <bool EXACT>
 HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
   ge29 e;
   load_ge_global29(e, gcomb + GC_TOP_OFF);
-  if (neg) fe29_neg(e.y, e.y);
+  fe29_cneg_lazy(e.y, e.y, neg);
   gej29_set_ge(acc, e);
   int d = comb_digit(k);
   load_ge_global29(e, comb_entry(gcomb, 0, d));
@@ -453,7 +453,7 @@ HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
       d = comb_digit(k);
       load_ge_global29(e, comb_entry(gcomb, w + 1, d));
     }
-    if ((dc < 0) != neg) fe29_neg(cur.y, cur.y);
+    fe29_cneg_lazy(cur.y, cur.y, (dc < 0) != neg);
     gej29_madd<EXACT>(acc, acc, cur);
   }
 }
@@ -489,7 +489,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
       load_ge29_tab(g, entry_of(d));
     }
 #ifdef HLC_B2_LATE
-    if ((d < 0) != ((negs & 1) != 0)) fe29_neg(g.y, g.y);
+    fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 1) != 0));
     gej29_madd<EXACT>(acc, acc, g);
     d = digit_at(win, 1);
     load_ge29_tab(g, entry_of(d));
@@ -498,13 +498,13 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
     const int d2 = digit_at(win, 1);
     ge29 g2;
     load_ge29_tab(g2, entry_of(d2));
-    if ((d < 0) != ((negs & 1) != 0)) fe29_neg(g.y, g.y);
+    fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 1) != 0));
     gej29_madd<EXACT>(acc, acc, g);
     g = g2;
     d = d2;
 #endif
     fe29_mul_uniform(g.x, g.x, beta);
-    if ((d < 0) != ((negs & 2) != 0)) fe29_neg(g.y, g.y);
+    fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 2) != 0));
     gej29_madd<EXACT>(acc, acc, g);
   }
 #pragma unroll 1
@@ -513,7 +513,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
     ge29 g;
     load_ge29_tab(g, tab);
     if (k == 1) fe29_mul_uniform(g.x, g.x, beta);
-    if (((negs >> k) & 1) == 0) fe29_neg(g.y, g.y);
+    fe29_cneg_lazy(g.y, g.y, ((negs >> k) & 1) == 0);
     gej29_madd<EXACT>(acc, acc, g);
   }
   if (!acc.inf) fe29_mul(acc.z, acc.z, zg);

@@ -434,3 +434,54 @@ def test_comb_collision_parity_argument():
     import crypto_items as ci
     assert ci.COMB_W == 22 and not ci.comb_collisions_possible(22)
     assert ci.comb_collisions_possible(16)
+
+
+K64 = [0x3FFF0BC0, 0x3FFFFDFE] + [0x3FFFFFFE] * 7   # 64p's limbs: bound of a lazily negated y
+
+
+def lazy_limbs(rnd, n):
+    out = np.zeros((n, 9), np.uint32)
+    for k in range(n):
+        m = rnd.random()
+        for i in range(9):
+            out[k, i] = K64[i] if m < 0.2 else (K64[i] - rnd.randrange(2**12) if m < 0.4 else rnd.randrange(K64[i] + 1))
+    return out
+
+
+def test_cneg_lazy(checked):
+    rnd = random.Random(12)
+    a = nrm_limbs(rnd, 3000)
+    c = np.zeros((3000, 9), np.uint32)
+    c[:, 0] = [rnd.randrange(2) for _ in range(3000)]
+    o = run(checked, 14, a, c)
+    assert (o <= np.array(K64, np.uint32)).all()
+    for k in range(3000):
+        assert val(o[k]) % P == ((-val(a[k])) if c[k, 0] else val(a[k])) % P
+
+
+def test_point_formulas_with_lazy_y(checked):
+    """The chains add table entries whose y went through fe29_cneg_lazy (limbs up to 64p's), and
+    an accumulator started from such an entry carries a lazy y into the next doublings and
+    additions: doubling and both additions at those bounds."""
+    rnd = random.Random(13)
+    n = 1500
+    X, Z, x2 = nrm_limbs(rnd, n), nrm_limbs(rnd, n), nrm_limbs(rnd, n)
+    Y, y2 = lazy_limbs(rnd, n), lazy_limbs(rnd, n)
+    A = np.array([jac(X[k], Y[k], Z[k]) for k in range(n)])
+    B = np.concatenate([x2, y2], axis=1)
+    d, m, me = runp(checked, 0, A, B), runp(checked, 1, A, B), runp(checked, 2, A, B)
+    for o in (d, m):
+        for q in range(3):
+            check_normalised(o[:, 9 * q: 9 * q + 9])
+    for k in range(n):
+        vx, vy, vz = val(X[k]) % P, val(Y[k]) % P, val(Z[k]) % P
+        assert tuple(val(d[k, 9 * q: 9 * q + 9]) % P for q in range(3)) == dbl_textbook(vx, vy, vz), k
+        want = madd_textbook(vx, vy, vz, val(x2[k]) % P, val(y2[k]) % P)
+        assert tuple(val(m[k, 9 * q: 9 * q + 9]) % P for q in range(3)) == want, k
+        if want[2] % P:
+            assert tuple(val(me[k, 9 * q: 9 * q + 9]) % P for q in range(3)) == want, k
+    # infinity accumulator + lazy entry: the exact form copies the lazy y into the accumulator
+    Ai = A.copy()
+    Ai[:, 27] = 1
+    mi = runp(checked, 2, Ai, B)
+    assert (mi[:, 9:18] == y2).all() and (mi[:, 27] == 0).all()
