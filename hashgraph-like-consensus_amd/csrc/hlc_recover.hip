@@ -23,8 +23,9 @@ constexpr int PREP_TPB = 64;
 __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, const uint8_t* pre,
                                                        const uint32_t* z_digest, const uint8_t* bytes,
                                                        const uint64_t* sig_off, size_t off_stride, uint8_t* state,
-                                                       uint32_t* rec, uint32_t* pfx) {
+                                                       uint32_t* rec, uint32_t* pfx, unsigned long long* main_ctr) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) *main_ctr = 0;  // k_rec_main's work counter (the next kernel on the stream)
   if (t >= L) return;
   fe acc;
   fe_set(acc, 1);
@@ -68,16 +69,42 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
 }
 
 // ---- main: decompress + u1 G + u2 R, one vote per lane at a time (persistent grid) ----
+// Work is handed out dynamically, 64 consecutive votes per wave per grab (one atomic by lane 0).
+// The SIMD's arbiter favours its oldest wave, so with a static vote-per-lane stride the oldest of
+// the 3 resident waves finishes its share long before the youngest, which then runs alone at
+// lone-wave efficiency (measured with HLC_CLOCK_PROBE: 4-vote blocks done at 3.5 ms, the last
+// 3-vote blocks at 7.0 ms of one launch); grabbing keeps every wave busy until the work runs out.
 __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n, const uint8_t* pre, const uint8_t* bytes,
                                                                      const uint64_t* sig_off, size_t off_stride,
                                                                      const uint32_t* gcomb, uint32_t* scratch,
                                                                      uint64_t lanes, uint8_t* state,
                                                                      const uint32_t* rec, uint32_t* q,
-                                                                     int force_exact) {
+                                                                     int force_exact, unsigned long long* ctr) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
   uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tid * RTAB_WORDS;
+#ifdef HLC_CLOCK_PROBE
+  // A/B probe (make variant NAME=clk DEFS=-DHLC_CLOCK_PROBE): the shader clock a wave sees under
+  // the real kernel = core-clock ticks (clock64) over constant 100 MHz ticks (wall_clock64)
+  const uint64_t clk0 = clock64(), wall0 = wall_clock64();
+  uint32_t done = 0;
+#endif
+#ifdef HLC_STATIC_STRIDE
+  // A/B variant: the round-1 static assignment (vote tid + k * lanes)
   for (uint64_t i = tid; i < n; i += lanes) {
+#else
+  const unsigned lane = threadIdx.x & 63u;
+  for (;;) {
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(ctr, 64ull);
+    base = __shfl(base, 0);
+    if (base >= n) break;
+    const uint64_t i = base + lane;
+    if (i >= n) continue;  // the next grab is past n: the wave leaves together
+#endif
+#ifdef HLC_CLOCK_PROBE
+    ++done;
+#endif
     if ((pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
     fe r;
     fe_load_be(r, bytes + sig_off[i * off_stride]);
@@ -102,6 +129,13 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
     store_fe_ws(qy, q + (size_t)8 * n + i, n);
     store_fe_ws(qz, q + (size_t)16 * n + i, n);
   }
+#ifdef HLC_CLOCK_PROBE
+  if (threadIdx.x == 0 && blockIdx.x % 61 == 0) {
+    const uint64_t dc = clock64() - clk0, dw = wall_clock64() - wall0;
+    printf("HLC_CLOCK block %u votes %u clk %llu wall %llu GHz %.3f\n", blockIdx.x, done, (unsigned long long)dc,
+           (unsigned long long)dw, dw ? (double)dc / ((double)dw * 10.0) : 0.0);
+  }
+#endif
 }
 
 // ---- final: batched Z^-1 (one safegcd per REC_BATCH votes), affine, keccak, owner compare ----
@@ -281,14 +315,17 @@ void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, co
   uint32_t* q = rec + n * (uint64_t)REC_WORDS;
   uint32_t* pfx = q + n * (uint64_t)Q_WORDS;
   const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH;
+  // k_rec_main's work counter: 8-byte aligned inside the 64-word tail of recover_work_words(n)
+  unsigned long long* ctr =
+      reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(pfx + L * REC_BATCH * 8) + 7) & ~uintptr_t(7));
   const unsigned pb = (unsigned)((L + PREP_TPB - 1) / PREP_TPB);
   hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, L, pre, z_digest, bytes, sig_off, off_stride,
-                     verify_out, rec, pfx);
+                     verify_out, rec, pfx, ctr);
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (n + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
   hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, bytes, sig_off, off_stride, gcomb,
-                     scratch, (uint64_t)blocks * REC_TPB, verify_out, rec, q, force_exact);
+                     scratch, (uint64_t)blocks * REC_TPB, verify_out, rec, q, force_exact, ctr);
   hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, L, pre, bytes, id_off, off_stride, verify_out, q, pfx,
                      addr_out);
 }
