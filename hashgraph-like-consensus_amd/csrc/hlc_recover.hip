@@ -10,7 +10,8 @@ namespace {
 
 constexpr int REC_TPB = 256;
 #ifndef HLC_REC_WAVES
-#define HLC_REC_WAVES 3  // waves per SIMD the register allocator must admit for k_rec_main (best of 2/3/4, profiles/r02_variants.txt)
+#define HLC_REC_WAVES 2  // waves per SIMD the register allocator must admit for k_rec_main: with dynamic work
+                         // hand-out 2 (256 VGPRs, no spills) beats 3 and 4 by 2.5% (profiles/r02_ab_waves_dynamic.txt)
 #endif
 
 // ---- prep: parse + batched r^-1 + scalars (REC_BATCH votes per lane, one safegcd) ----
