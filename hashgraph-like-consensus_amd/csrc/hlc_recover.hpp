@@ -231,6 +231,9 @@ HLC_DEV int comb_digit(fe& x) {
 }
 
 HLC_DEV const uint32_t* comb_entry(const uint32_t* gcomb, int w, int d) {
+#ifdef HLC_PROBE_HOT_GATHER
+  d = 1;  // timing probe only (wrong results): every gather hits one hot entry per window
+#endif
   const int idx = ((d < 0 ? -d : d) - 1) >> 1;
   return gcomb + ((size_t)w * GC_ENTRIES + (size_t)idx) * 16;
 }
@@ -475,7 +478,11 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
   auto digit_at = [&](int win, int k) {
     return digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
   };
+#ifdef HLC_PROBE_HOT_GATHER
+  auto entry_of = [&](int d) { return tab; };  // timing probe only (wrong results): no table traffic
+#else
   auto entry_of = [&](int d) { return tab + RTAB_ENTRY * (((d < 0 ? -d : d) - 1) >> 1); };
+#endif
 #pragma unroll 1
   for (int win = M_R - 1; win >= 0; --win) {
     ge29 g;
