@@ -127,3 +127,14 @@ def test_gpu_validate_small_workload(engine):
     assert np.array_equal(rec, crec)
     assert np.array_equal(res, cres)
     assert (vst == 0).all()
+
+
+def test_gpu_verify_batch_sizes(engine):
+    """k_rec_main hands out 64 votes per wave per grab: batches that are not a multiple of 64,
+    smaller than one wave, or end in skipped (pre-rejected) votes must equal the oracle too."""
+    ids, pays, sigs = _mutated_items(300, 23)
+    exp_st, exp_addr = _oracle_verify(ids, pays, sigs)
+    for n in (1, 2, 63, 64, 65, 127, 129, 300):
+        st, addr = engine.eth_verify_batch(ids[:n], pays[:n], sigs[:n])
+        assert [int(x) for x in st] == exp_st[:n], n
+        assert [a.tobytes() for a in addr] == exp_addr[:n], n
