@@ -69,6 +69,8 @@ struct DBuf {
 struct hlc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t aux = nullptr;                        // the recovery prep stage, concurrent with the prehash
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // caller stream -> aux -> caller stream
   std::mutex mu;
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
@@ -82,7 +84,7 @@ struct hlc_ctx {
   // measurement hooks
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, call_ev, chain_ev;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, rec_prep_ev, call_ev, chain_ev;
   hipEvent_t take_event() {
     if (ev_pool.empty()) {
       hipEvent_t e = nullptr;
@@ -96,6 +98,9 @@ struct hlc_ctx {
   ~hlc_ctx() {
     for (auto e : ev_pool) (void)hipEventDestroy(e);
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : rec_prep_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   }
@@ -199,22 +204,38 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   CHK(c->pre_reason.ensure(n));
   CHK(c->verify.ensure(n));
   CHK(c->kec_dig.ensure(n * 32));
+  CHK(ensure_recover_scratch(c));
+  CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
+  // the recovery's prep stage (signature parse, batched r^-1, GLV digits) needs only the signatures:
+  // it runs on the context's aux stream while the prehash kernels run on `s`; `s` waits for it
+  // before the main stage.  Measured recovery time = prep bracket (aux) + main/final bracket (s).
+  HIPCHK(hipEventRecord(c->ev_fork, s));
+  HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  hipEvent_t p0 = nullptr, p1 = nullptr, r0 = nullptr, r1 = nullptr;
+  if (c->timing) {
+    p0 = c->take_event();
+    p1 = c->take_event();
+    r0 = c->take_event();
+    r1 = c->take_event();
+    HIPCHK(hipEventRecord(p0, c->aux));
+  }
+  hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
+                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), c->aux);
+  if (c->timing) {
+    HIPCHK(hipEventRecord(p1, c->aux));
+    c->rec_prep_ev.emplace_back(p0, p1);
+  }
+  HIPCHK(hipEventRecord(c->ev_join, c->aux));
   hlc::launch_prehash_fused(dv, n, vote_prop, dprops, c->kec_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
                             c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
   hlc::launch_prehash_stream(dv, n, vote_prop, dprops, c->flag.as<uint32_t>(), c->kec_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
-  CHK(ensure_recover_scratch(c));
-  CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
-  hipEvent_t r0 = nullptr, r1 = nullptr;
-  if (c->timing) {
-    r0 = c->take_event();
-    r1 = c->take_event();
-    HIPCHK(hipEventRecord(r0, s));
-  }
-  hlc::launch_recover(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_SIGNATURE,
-                      dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(),
-                      c->rec_lanes, c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact);
+  HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+  if (c->timing) HIPCHK(hipEventRecord(r0, s));
+  hlc::launch_recover_main(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_SIGNATURE,
+                           dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(),
+                           c->rec_lanes, c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact);
   if (c->timing) {
     HIPCHK(hipEventRecord(r1, s));
     c->rec_ev.emplace_back(r0, r1);
@@ -489,7 +510,12 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
   hlc_ctx* c = new hlc_ctx();
   c->device = device;
   if (const char* fx = std::getenv("HLC_REC_FORCE_EXACT")) c->rec_force_exact = std::atoi(fx) != 0;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     delete c;
     return set_err(HLC_EDEVICE, "stream creation failed");
   }
@@ -514,9 +540,11 @@ void hlc_ctx_destroy(hlc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  hipStream_t s = ctx->stream;
+  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
+  hipStream_t s = ctx->stream, a = ctx->aux;
   delete ctx;
   if (s) (void)hipStreamDestroy(s);
+  if (a) (void)hipStreamDestroy(a);
 }
 
 int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, uint64_t max_bytes) {
@@ -554,19 +582,19 @@ int hlc_ctx_take_kernel_time(hlc_ctx* ctx, double* recover_ms, uint64_t* recover
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
   double rsum = 0, csum = 0;
-  for (auto* vec : {&ctx->rec_ev, &ctx->call_ev}) {
+  for (auto* vec : {&ctx->rec_ev, &ctx->rec_prep_ev, &ctx->call_ev}) {
     for (auto& pr : *vec) {
       HIPCHK(hipEventSynchronize(pr.second));
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
-      (vec == &ctx->rec_ev ? rsum : csum) += ms;
+      (vec == &ctx->call_ev ? csum : rsum) += ms;
     }
   }
   if (recover_ms) *recover_ms = rsum;
   if (recover_launches) *recover_launches = ctx->rec_ev.size();
   if (call_ms) *call_ms = csum;
   if (calls) *calls = ctx->call_ev.size();
-  for (auto* vec : {&ctx->rec_ev, &ctx->call_ev}) {
+  for (auto* vec : {&ctx->rec_ev, &ctx->rec_prep_ev, &ctx->call_ev}) {
     for (auto& pr : *vec) {
       ctx->ev_pool.push_back(pr.first);
       ctx->ev_pool.push_back(pr.second);
@@ -912,7 +940,8 @@ int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_
   }
   CHK(ctx->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   hlc::launch_recover(n, ctx->pre.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), dbytes, ctx->in_off3.as<uint64_t>(),
-                      ctx->in_off.as<uint64_t>(), 1, ctx->gtab.as<uint32_t>(), ctx->rec_scratch.as<uint32_t>(),
+                      ctx->in_off.as<uint64_t>(), 1, ctx->in_len3.as<uint32_t>(), 1, ctx->gtab.as<uint32_t>(),
+                      ctx->rec_scratch.as<uint32_t>(),
                       ctx->rec_lanes, ctx->rec_work.as<uint32_t>(), ctx->verify.as<uint8_t>(), drec, s,
                       ctx->rec_force_exact);
   HIPCHK(hipGetLastError());

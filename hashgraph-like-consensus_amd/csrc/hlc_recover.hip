@@ -18,15 +18,28 @@ constexpr int REC_TPB = 256;
 // Lane t owns votes t + k * L (k < REC_BATCH): a wave reads 64 consecutive votes per k.
 // Forward: acc_k = mont(acc_{k-1}, r_k) = (prod r) R^-k over the lane's valid votes, each acc_{k-1}
 // kept in `pfx`; one inversion cur = acc^-1; backward: r_k^-1 = mont(acc_{k-1}, cur),
-// cur = mont(cur, r_k).  Invalid votes multiply nothing (their state is final already).
+// cur = mont(cur, r_k).  The stage reads only the signatures (every 65-byte one: which votes the
+// pre-checks reject is not known yet), so it runs on a second stream while the prehash kernels
+// run (hlc_api.cpp vote_stage); a vote's scheme error goes to bits 8-15 of its record flags and
+// the main stage turns it into the vote's state.
 constexpr int PREP_TPB = 64;
 
-__global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, const uint8_t* pre,
-                                                       const uint32_t* z_digest, const uint8_t* bytes,
-                                                       const uint64_t* sig_off, size_t off_stride, uint8_t* state,
-                                                       uint32_t* rec, uint32_t* pfx, unsigned long long* main_ctr) {
+HLC_DEV bool prep_sig(const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len,
+                      size_t len_stride, uint64_t i, fe& r, fe& s, int& parity, int& code) {
+  if (sig_len[i * len_stride] != 65u) return false;  // rejected by the pre-checks (length)
+  const uint8_t* sig = bytes + sig_off[i * off_stride];
+  fe_load_be(r, sig);
+  fe_load_be(s, sig + 32);
+  code = rec_parse(s, r, sig[64], parity);
+  return true;
+}
+
+__global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, const uint8_t* bytes,
+                                                       const uint64_t* sig_off, size_t off_stride,
+                                                       const uint32_t* sig_len, size_t len_stride, uint32_t* rec,
+                                                       uint32_t* pfx, unsigned long long* main_ctr) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t == 0) *main_ctr = 0;  // k_rec_main's work counter (the next kernel on the stream)
+  if (t == 0) *main_ctr = 0;  // k_rec_main's work counter (it runs after this kernel)
   if (t >= L) return;
   fe acc;
   fe_set(acc, 1);
@@ -34,18 +47,13 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
   for (int k = 0; k < REC_BATCH; ++k) {
     const uint64_t i = t + (uint64_t)k * L;
     if (i >= n) break;
-    if (pre && pre[i] != PRE_PENDING) continue;  // not recovered: state untouched (may hold a caller code)
-    const uint8_t* sig = bytes + sig_off[i * off_stride];
     fe r, s;
-    fe_load_be(r, sig);
-    fe_load_be(s, sig + 32);
-    int parity;
-    const int code = rec_parse(s, r, sig[64], parity);
+    int parity, code;
+    if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) continue;
     if (code != SCHEME_NONE) {
-      state[i] = (uint8_t)(1 + code);
+      rec[(size_t)REC_FLAGS * n + i] = (uint32_t)code << 8;
       continue;
     }
-    state[i] = REC_PENDING;
     store_fe_ws(acc, pfx + (size_t)k * 8 * L + t, L);
     sc_mont_mul(acc, acc, r);
   }
@@ -54,18 +62,15 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
 #pragma unroll 1
   for (int k = REC_BATCH - 1; k >= 0; --k) {
     const uint64_t i = t + (uint64_t)k * L;
-    if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
-    const uint8_t* sig = bytes + sig_off[i * off_stride];
-    fe r, s, z, prev, rinv;
-    fe_load_be(r, sig);
-    fe_load_be(s, sig + 32);
-    int parity;
-    (void)rec_parse(s, r, sig[64], parity);
+    if (i >= n) continue;
+    fe r, s, prev, rinv;
+    int parity, code;
+    if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code) || code != SCHEME_NONE)
+      continue;
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
     sc_mont_mul(rinv, prev, cur);  // r_k^-1
     sc_mont_mul(cur, cur, r);      // acc_{k-1}^-1
-    fe_from_digest(z, z_digest + 8 * i);
-    rec_prep_scalars(z, s, rinv, parity, rec + i, n);
+    rec_prep_scalars(s, rinv, parity, rec + i, n);
   }
 }
 
@@ -75,7 +80,8 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
 // the 3 resident waves finishes its share long before the youngest, which then runs alone at
 // lone-wave efficiency (measured with HLC_CLOCK_PROBE: 4-vote blocks done at 3.5 ms, the last
 // 3-vote blocks at 7.0 ms of one launch); grabbing keeps every wave busy until the work runs out.
-__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n, const uint8_t* pre, const uint8_t* bytes,
+__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n, const uint8_t* pre,
+                                                                     const uint32_t* z_digest, const uint8_t* bytes,
                                                                      const uint64_t* sig_off, size_t off_stride,
                                                                      const uint32_t* gcomb, uint32_t* scratch,
                                                                      uint64_t lanes, uint8_t* state,
@@ -106,26 +112,32 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
 #ifdef HLC_CLOCK_PROBE
     ++done;
 #endif
-    if ((pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
-    fe r;
+    if (pre && pre[i] != PRE_PENDING) continue;  // not recovered: state untouched (may hold a caller code)
+    const uint32_t prep_code = (rec[(size_t)REC_FLAGS * n + i] >> 8) & 0xFFu;
+    if (prep_code != SCHEME_NONE) {  // v / r / s rejected by the prep stage
+      state[i] = (uint8_t)(1 + prep_code);
+      continue;
+    }
+    fe r, z, u1;
+    bool neg_g;
     fe_load_be(r, bytes + sig_off[i * off_stride]);
+    fe_from_digest(z, z_digest + 8 * i);
+    rec_u1(z, rec + i, n, u1, neg_g);
     fe qx, qy, qz;
 #ifdef HLC_FIELD32
     // A/B variant (make variants): the saturated 8 x 32 field layer
     gej acc;
-    int code = rec_main(r, rec + i, n, acc, gcomb, ws, lanes, tab);
+    int code = rec_main(r, u1, neg_g, rec + i, n, acc, gcomb, ws, lanes, tab);
     if (code == SCHEME_NONE) {
       qx = acc.x;
       qy = acc.y;
       qz = acc.z;
     }
 #else
-    const int code = rec_main29(r, rec + i, n, qx, qy, qz, gcomb, ws, lanes, tab, force_exact != 0);
+    const int code = rec_main29(r, u1, neg_g, rec + i, n, qx, qy, qz, gcomb, ws, lanes, tab, force_exact != 0);
 #endif
-    if (code != SCHEME_NONE) {
-      state[i] = (uint8_t)(1 + code);
-      continue;
-    }
+    state[i] = code != SCHEME_NONE ? (uint8_t)(1 + code) : REC_PENDING;
+    if (code != SCHEME_NONE) continue;
     store_fe_ws(qx, q + i, n);
     store_fe_ws(qy, q + (size_t)8 * n + i, n);
     store_fe_ws(qz, q + (size_t)16 * n + i, n);
@@ -307,28 +319,57 @@ uint64_t recover_grid_lanes() {
   return (uint64_t)cus * (uint64_t)per_cu * REC_TPB;
 }
 
-void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
-                    const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb,
-                    uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, uint8_t* verify_out, uint8_t* addr_out,
-                    hipStream_t s, int force_exact) {
-  if (!n) return;
-  uint32_t* rec = work;
-  uint32_t* q = rec + n * (uint64_t)REC_WORDS;
-  uint32_t* pfx = q + n * (uint64_t)Q_WORDS;
-  const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH;
+namespace {
+struct RecBufs {
+  uint32_t *rec, *q, *pfx;
+  unsigned long long* ctr;
+  uint64_t L;
+};
+RecBufs rec_bufs(uint64_t n, uint32_t* work) {
+  RecBufs b;
+  b.rec = work;
+  b.q = b.rec + n * (uint64_t)REC_WORDS;
+  b.pfx = b.q + n * (uint64_t)Q_WORDS;
+  b.L = (n + REC_BATCH - 1) / REC_BATCH;
   // k_rec_main's work counter: 8-byte aligned inside the 64-word tail of recover_work_words(n)
-  unsigned long long* ctr =
-      reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(pfx + L * REC_BATCH * 8) + 7) & ~uintptr_t(7));
-  const unsigned pb = (unsigned)((L + PREP_TPB - 1) / PREP_TPB);
-  hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, L, pre, z_digest, bytes, sig_off, off_stride,
-                     verify_out, rec, pfx, ctr);
+  b.ctr = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(b.pfx + b.L * REC_BATCH * 8) + 7) &
+                                                ~uintptr_t(7));
+  return b;
+}
+}  // namespace
+
+void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
+                         const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s) {
+  if (!n) return;
+  const RecBufs b = rec_bufs(n, work);
+  const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
+  hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, bytes, sig_off, off_stride, sig_len,
+                     len_stride, b.rec, b.pfx, b.ctr);
+}
+
+void launch_recover_main(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
+                         const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb,
+                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, uint8_t* verify_out,
+                         uint8_t* addr_out, hipStream_t s, int force_exact) {
+  if (!n) return;
+  const RecBufs b = rec_bufs(n, work);
+  const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (n + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
-  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, bytes, sig_off, off_stride, gcomb,
-                     scratch, (uint64_t)blocks * REC_TPB, verify_out, rec, q, force_exact, ctr);
-  hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, L, pre, bytes, id_off, off_stride, verify_out, q, pfx,
-                     addr_out);
+  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, z_digest, bytes, sig_off,
+                     off_stride, gcomb, scratch, (uint64_t)blocks * REC_TPB, verify_out, b.rec, b.q, force_exact, b.ctr);
+  hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, pre, bytes, id_off, off_stride, verify_out,
+                     b.q, b.pfx, addr_out);
+}
+
+void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
+                    const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* sig_len,
+                    size_t len_stride, const uint32_t* gcomb, uint32_t* scratch, uint64_t scratch_lanes,
+                    uint32_t* work, uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact) {
+  launch_recover_prep(n, bytes, sig_off, off_stride, sig_len, len_stride, work, s);
+  launch_recover_main(n, pre, z_digest, bytes, sig_off, id_off, off_stride, gcomb, scratch, scratch_lanes, work,
+                      verify_out, addr_out, s, force_exact);
 }
 
 void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s) {

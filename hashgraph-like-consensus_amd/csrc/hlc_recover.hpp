@@ -66,9 +66,9 @@ constexpr int SCRATCH_WORDS = IL_WORDS + RTAB_WORDS;      // per lane workspace 
 
 // Per-vote records between the stages, word-major (word w of vote i at w * n + i: a wave's 64
 // consecutive votes read one coalesced 256-B row per word).
-constexpr int REC_U1 = 0;                       // 8 words: odd representative of u1
+constexpr int REC_RINV = 0;                     // 8 words: r^-1 R mod n (Montgomery form; u1 = -z/r in main)
 constexpr int REC_DIG = 8;                      // 2 x DIG_R_WORDS: int16 digit pairs of b1, b2
-constexpr int REC_FLAGS = REC_DIG + 2 * DIG_R_WORDS;  // bit 0-1 negs, 2-3 skews, 4 neg_g, 5 parity
+constexpr int REC_FLAGS = REC_DIG + 2 * DIG_R_WORDS;  // bit 0-1 negs, 2-3 skews, 5 parity, 8-15 prep code
 constexpr int REC_WORDS = REC_FLAGS + 1;
 constexpr int Q_WORDS = 24;                     // main -> final: Jacobian X, Y, Z
 #ifndef HLC_REC_BATCH
@@ -373,35 +373,43 @@ HLC_DEV int rec_parse(fe& s, const fe& r, uint32_t v, int& parity) {
   return SCHEME_NONE;
 }
 
-// Prep stage, after r^-1 is known: u1 = -z/r (odd representative), u2 = s/r split by GLV and
-// recoded; writes the vote's record (stride = n, vote-major words).
-HLC_DEV void rec_prep_scalars(const fe& zraw, const fe& s, const fe& rinv, int parity, uint32_t* rec, size_t stride) {
-  fe z;
-  sc_reduce(z, zraw);
-  fe u1, u2;
+// Prep stage, after r^-1 is known: u2 = s/r split by GLV and recoded, r^-1 kept (Montgomery form)
+// for u1 = -z/r, which the main stage forms once the prehash z exists: the prep stage needs only
+// the signature, so it runs concurrently with the prehash kernels.  Writes the vote's record
+// (stride = n, vote-major words).
+HLC_DEV void rec_prep_scalars(const fe& s, const fe& rinv, int parity, uint32_t* rec, size_t stride) {
+  fe u2, rinvR;
   {
-    fe r2c, rinvR;
+    fe r2c;
     sc_r2(r2c);
     sc_mont_mul(rinvR, rinv, r2c);  // r^-1 * R (Montgomery form)
     sc_mont_mul(u2, s, rinvR);      // s * r^-1
-    sc_mont_mul(u1, z, rinvR);      // z * r^-1
-    sc_neg(u1, u1);
-  }
-  const bool neg_g = (u1.v[0] & 1u) == 0u;
-  if (neg_g) {
-    uint32_t bw = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) u1.v[i] = sub_cc(n_limb(i), u1.v[i], bw);
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) rec[(size_t)(REC_U1 + i) * stride] = u1.v[i];
+  for (int i = 0; i < 8; ++i) rec[(size_t)(REC_RINV + i) * stride] = rinvR.v[i];
   fe b1, b2;
   bool nb1, nb2;
   glv_split(u2, b1, nb1, b2, nb2);
   const uint32_t s2 = recode_regular<W_R, M_R>(b1, rec + (size_t)REC_DIG * stride, stride);
   const uint32_t s3 = recode_regular<W_R, M_R>(b2, rec + (size_t)(REC_DIG + DIG_R_WORDS) * stride, stride);
-  rec[(size_t)REC_FLAGS * stride] = (nb1 ? 1u : 0u) | (nb2 ? 2u : 0u) | (s2 << 2) | (s3 << 3) | (neg_g ? 16u : 0u) |
-                                    ((uint32_t)parity << 5);
+  rec[(size_t)REC_FLAGS * stride] = (nb1 ? 1u : 0u) | (nb2 ? 2u : 0u) | (s2 << 2) | (s3 << 3) | ((uint32_t)parity << 5);
+}
+
+// Main stage: u1 = -z r^-1 mod n from the prehash and the record's r^-1, as its odd representative
+// (u1 or n - u1, neg_g set for the latter) -- the comb's recoding needs an odd scalar.
+HLC_DEV void rec_u1(const fe& zraw, const uint32_t* rec, size_t stride, fe& u1, bool& neg_g) {
+  fe z, rinvR;
+  sc_reduce(z, zraw);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rinvR.v[i] = rec[(size_t)(REC_RINV + i) * stride];
+  sc_mont_mul(u1, z, rinvR);  // z * r^-1
+  sc_neg(u1, u1);
+  neg_g = (u1.v[0] & 1u) == 0u;
+  if (neg_g) {
+    uint32_t bw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u1.v[i] = sub_cc(n_limb(i), u1.v[i], bw);
+  }
 }
 
 // ---- main stage helpers over the 29-bit field layer ----
@@ -535,8 +543,8 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
 // ones) leaves a zero Z behind, so one test of both final Z values per vote routes such a vote
 // through the same chains with every step checked.  (With the shipped 22-bit comb no such
 // collision exists at all: see DESIGN.md §4.1.  The test stays as the guard.)
-HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz,
-                       const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact) {
+HLC_DEV int rec_main29(const fe& r32, const fe& u1, bool neg_g, const uint32_t* rec, size_t stride, fe& qx, fe& qy,
+                       fe& qz, const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int parity = (int)((flags >> 5) & 1u);
   ge29 R;
@@ -550,7 +558,6 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
     if (!fe29_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
     if ((int)(R.y.v[0] & 1u) != parity) fe29_neg(R.y, R.y);
   }
-  const bool neg_g = (flags & 16u) != 0;
   fe29 zg;
   {
     gej29 d;
@@ -593,9 +600,6 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
     }
     fe29_mul(zg, sc, d.z);
   }
-  fe u1;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) u1.v[i] = rec[(size_t)(REC_U1 + i) * stride];
   gej29 acc, ag;
   chain_u2r29<false>(acc, rec, stride, tab, zg);
   comb_mul_g29<false>(ag, u1, neg_g, gcomb);
@@ -617,8 +621,8 @@ HLC_DEV int rec_main29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx
 // Returns SCHEME_NONE, SCHEME_NO_POINT or SCHEME_INFINITY.  rec: the vote's record (stride n);
 // gcomb: the fixed-base comb; ws: this lane's interleaved workspace column (stride = lanes);
 // tab: this lane's R table.
-HLC_DEV int rec_main(const fe& r, const uint32_t* rec, size_t stride, gej& acc, const uint32_t* gcomb, uint32_t* ws,
-                     size_t ws_stride, uint32_t* tab) {
+HLC_DEV int rec_main(const fe& r, const fe& u1, bool neg_g, const uint32_t* rec, size_t stride, gej& acc,
+                     const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int parity = (int)((flags >> 5) & 1u);
   // R = decompress(r, parity): y^2 = x^3 + 7 (x = r < n < p)
@@ -634,7 +638,6 @@ HLC_DEV int rec_main(const fe& r, const uint32_t* rec, size_t stride, gej& acc, 
     if ((int)(R.y.v[0] & 1u) != parity) fe_neg(R.y, R.y);
   }
   const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
-  const bool neg_g = (flags & 16u) != 0;
   // R table on the isomorphic curve with C = Z(2R): entries (2i+1)R, i < 16, common Z
   fe zg;  // real Z of the table frame
   {
@@ -719,9 +722,6 @@ HLC_DEV int rec_main(const fe& r, const uint32_t* rec, size_t stride, gej& acc, 
     gej_add_ge(acc, acc, g);
   }
   if (!acc.inf) fe_mul(acc.z, acc.z, zg);  // u2 R back on the real curve
-  fe u1;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) u1.v[i] = rec[(size_t)(REC_U1 + i) * stride];
   gej ag;
   comb_mul_g(ag, u1, neg_g, gcomb);
   gej_add(acc, acc, ag);
