@@ -255,7 +255,10 @@ int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_propo
 /* Same, but every pointer (inside `votes`, `proposals`, and the outputs) is DEVICE memory
  * of the context's device, and the work is enqueued on `stream` (a hipStream_t, or NULL for
  * the context's stream) without host synchronisation.  Used when inputs are already
- * resident in HBM (bench.py). */
+ * resident in HBM (bench.py).  The recovery's signature-only stage runs on a second stream the
+ * context owns, forked from and joined back into `stream` by events.  A context's workspace
+ * serves one call at a time: successive calls on one context must be ordered (the same stream,
+ * or the caller's own synchronisation between streams). */
 int hlc_validate_proposals_device(hlc_ctx* ctx, const hlc_votes* votes,
                                   const hlc_proposal* proposals, uint64_t n_proposals,
                                   uint64_t now, hlc_result* out_results,
