@@ -63,11 +63,15 @@ __device__ uint64_t vote_enc_len(const hlc_votes& v, uint64_t i) {
   return n;
 }
 
+// Block (p, y) of a (proposals x G) grid writes every G-th span of proposal p's vote range: G > 1
+// when the batch's proposals are large on average (config 3: one proposal of 1M votes).
 __global__ void k_assign_props(const hlc_proposal* props, uint32_t* vote_prop, uint32_t* flags) {
   const uint32_t p = blockIdx.x;
   const hlc_proposal d = props[p];
-  if (threadIdx.x == 0 && d.vote_count > SMALL_CAP) atomicOr(flags, FLAG_LARGE_PROPOSAL);
-  for (uint64_t j = threadIdx.x; j < d.vote_count; j += blockDim.x) vote_prop[d.vote_begin + j] = p;
+  if (threadIdx.x == 0 && blockIdx.y == 0 && d.vote_count > SMALL_CAP) atomicOr(flags, FLAG_LARGE_PROPOSAL);
+  const uint64_t step = (uint64_t)blockDim.x * gridDim.y;
+  for (uint64_t j = (uint64_t)blockIdx.y * blockDim.x + threadIdx.x; j < d.vote_count; j += step)
+    vote_prop[d.vote_begin + j] = p;
 }
 
 __global__ void k_msg_sizes(hlc_votes v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
@@ -282,17 +286,69 @@ __global__ void k_vote_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop
 }
 
 // ---------------- chain / duplicate tables ----------------
-__device__ __forceinline__ uint32_t key_hash(uint32_t p, const uint8_t* b, uint32_t len) {
-  uint32_t h = 2166136261u ^ (p * 0x9E3779B1u);
-  for (uint32_t k = 0; k < len; ++k) h = (h ^ b[k]) * 16777619u;
+// The N-byte field at any byte address as N/4 little-endian words: 4-byte-aligned dword loads
+// (only dwords that hold a byte of the field, so nothing past the field's last dword is read)
+// joined by funnel shifts -- N/4 + 1 loads instead of N byte loads.
+template <int N>
+__device__ __forceinline__ void load_words(const uint8_t* p, uint32_t w[N / 4]) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* b = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t sh = (uint32_t)(a & 3u) * 8u;
+  uint32_t r[N / 4 + 1];
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k) r[k] = b[k];
+  r[N / 4] = sh ? b[N / 4] : 0u;
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k) w[k] = __builtin_amdgcn_alignbit(r[k + 1], r[k], sh);
+}
+
+__device__ __forceinline__ uint32_t key_fin(uint32_t h) {
   h ^= h >> 15;
   h *= 0x2C1B3C6Du;
   h ^= h >> 12;
   return h;
 }
 
+template <int N>
+__device__ __forceinline__ uint32_t key_hash_w(uint32_t p, const uint32_t w[N / 4]) {
+  uint32_t h = 2166136261u ^ (p * 0x9E3779B1u) ^ (uint32_t)N;
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k) h = __builtin_amdgcn_alignbit(h, h, 19) ^ (w[k] * 16777619u);
+  return key_fin(h);
+}
+
+// hash of (proposal, field bytes): word-wise for the canonical lengths (address 20, hash 32), byte-
+// wise otherwise.  A key's length picks the form, so equal keys always hash alike.
+__device__ __forceinline__ uint32_t key_hash(uint32_t p, const uint8_t* b, uint32_t len) {
+  if (len == 32) {
+    uint32_t w[8];
+    load_words<32>(b, w);
+    return key_hash_w<32>(p, w);
+  }
+  if (len == 20) {
+    uint32_t w[5];
+    load_words<20>(b, w);
+    return key_hash_w<20>(p, w);
+  }
+  uint32_t h = 2166136261u ^ (p * 0x9E3779B1u);
+  for (uint32_t k = 0; k < len; ++k) h = (h ^ b[k]) * 16777619u;
+  return key_fin(h);
+}
+
+template <int N>
+__device__ __forceinline__ bool words_eq(const uint8_t* a, const uint8_t* b) {
+  uint32_t x[N / 4], y[N / 4], d = 0;
+  load_words<N>(a, x);
+  load_words<N>(b, y);
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k) d |= x[k] ^ y[k];
+  return d == 0;
+}
+
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
   if (al != bl) return false;
+  if (al == 32) return words_eq<32>(a, b);
+  if (al == 20) return words_eq<20>(a, b);
   for (uint32_t k = 0; k < al; ++k)
     if (a[k] != b[k]) return false;
   return true;
@@ -343,7 +399,8 @@ __device__ __forceinline__ uint32_t table_find(const uint32_t* tab, uint32_t mas
 }
 
 // red layout per proposal: [0] first bad vote (local idx), [1] first chain error, [2] first dup, [3] yes
-__global__ void k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
+constexpr int CHAIN_TPB = 1024;
+__global__ void __launch_bounds__(CHAIN_TPB) k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                               const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
                               uint32_t mask, uint8_t* chain_code, uint32_t* red, const uint32_t* flags) {
   if (flags && !(*flags & FLAG_LARGE_PROPOSAL)) return;  // every proposal is small: k_chain_small
@@ -382,12 +439,31 @@ __global__ void k_chain_check(hlc_votes v, uint64_t n, const uint32_t* vote_prop
     if (first != (uint32_t)i) atomicMin(&red[4 * p + 2], j);
     yes = v.vote[i] != 0;
   }
-  // YES count: one atomic per wave when the whole wave shares a proposal (large proposals)
+  // YES count of large proposals: one atomic per BLOCK when the whole block shares a proposal
+  // (config 3: one proposal of 1M votes -- same-address atomics serialise at the L2, so one per
+  // wave cost ~0.6 ms), one per wave when the wave does, else one per YES vote
+  __shared__ uint32_t s_p[CHAIN_TPB / 64], s_y[CHAIN_TPB / 64];
   const uint32_t p0 = __builtin_amdgcn_readfirstlane(p);
-  const uint64_t same = __ballot(p == p0);
-  if (same == ~0ull) {
-    const uint64_t y = __ballot(yes);
-    if (p0 != NO_PROP && (threadIdx.x & 63) == 0 && y) atomicAdd(&red[4 * p0 + 3], (uint32_t)__popcll(y));
+  const bool wave_same = __ballot(p == p0) == ~0ull;
+  const uint32_t wy = (uint32_t)__popcll(__ballot(yes));
+  const unsigned wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_p[wv] = wave_same ? p0 : NO_PROP;
+    s_y[wv] = wy;
+  }
+  __syncthreads();
+  bool block_same = true;
+#pragma unroll
+  for (int k = 0; k < CHAIN_TPB / 64; ++k) block_same &= s_p[k] == s_p[0];
+  if (block_same) {
+    if (threadIdx.x == 0 && s_p[0] != NO_PROP) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int k = 0; k < CHAIN_TPB / 64; ++k) t += s_y[k];
+      if (t) atomicAdd(&red[4 * s_p[0] + 3], t);
+    }
+  } else if (wave_same) {
+    if (p0 != NO_PROP && (threadIdx.x & 63) == 0 && wy) atomicAdd(&red[4 * p0 + 3], wy);
   } else if (yes) {
     atomicAdd(&red[4 * p + 3], 1u);
   }
@@ -986,7 +1062,9 @@ hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t*
     const hipError_t e = hipMemsetAsync(vote_prop, 0xFF, nv * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
   }
-  if (np) hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np), dim3(TPB), 0, s, props, vote_prop, flags);
+  // a second grid dimension when proposals are large on average (each block then covers ~4k votes)
+  const uint64_t g = np ? std::min<uint64_t>(std::max<uint64_t>((nv / np + 4095) / 4096, 1), 1024) : 1;
+  if (np) hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np, (unsigned)g), dim3(TPB), 0, s, props, vote_prop, flags);
   return hipSuccess;
 }
 
@@ -1059,7 +1137,8 @@ void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
   if (!np) return;
   hipLaunchKernelGGL(k_red_init, dim3((unsigned)((np + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np);
   if (n)
-    hipLaunchKernelGGL(k_chain_check, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, status,
+    hipLaunchKernelGGL(k_chain_check, dim3((unsigned)((n + CHAIN_TPB - 1) / CHAIN_TPB)), dim3(CHAIN_TPB), 0, s, *v, n,
+                       vote_prop, props, status,
                        chain_tab, dup_tab, mask, chain_code, red, flags);
 }
 

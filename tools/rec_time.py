@@ -4,7 +4,8 @@ Prints ms per call, recovery-bracket ms and the fraction of votes the build veri
 import sys
 import time
 
-sys.path.insert(0, "hashgraph-like-consensus_amd/python")
+import os  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "hashgraph-like-consensus_amd", "python"))
 import torch  # noqa: E402
 
 from hashgraph_like_consensus import synth  # noqa: E402
