@@ -111,36 +111,58 @@ __global__ void k_synth_keys(SynthArgs a, const uint32_t* fb) {
   fl[HLC_F_SIGNATURE] = 65;
 }
 
-// compute_vote_hash (utils.rs:37-47) along each proposal's chain
+// compute_vote_hash (utils.rs:37-47) along each proposal's chain.  The chain is sequential (each
+// vote's received_hash is the previous vote's hash), so one lane walks a proposal; the SHA-256
+// message words are assembled in registers from the fixed layout vote_id(4 LE) | owner(20) |
+// proposal_id(4 LE) | timestamp(8 LE) | vote(1) | received(0/32), no byte buffer.
 __global__ void k_synth_chain(SynthArgs a, hlc_proposal* props, uint32_t expected, int gossipsub) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.P) return;
-  uint8_t msg[69];
-  uint8_t prev[32];
+  uint32_t prev[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // previous vote hash, big-endian words
   for (uint64_t j = 0; j < a.V; ++j) {
     const uint64_t i = p * a.V + j;
     const uint64_t base = rec_base(p, j, a.V);
     uint8_t* o = a.bytes + base;
     const uint32_t vid = a.vote_id[i], pid = a.proposal_id[i];
     const uint64_t ts = a.timestamp[i];
-    for (int k = 0; k < 4; ++k) msg[k] = (uint8_t)(vid >> (8 * k));
-    for (int k = 0; k < 20; ++k) msg[4 + k] = o[k];
-    for (int k = 0; k < 4; ++k) msg[24 + k] = (uint8_t)(pid >> (8 * k));
-    for (int k = 0; k < 8; ++k) msg[28 + k] = (uint8_t)(ts >> (8 * k));
-    msg[36] = a.vote[i];
-    int len = 37;
-    if (j) {
-      for (int k = 0; k < 32; ++k) msg[37 + k] = prev[k];
-      for (int k = 0; k < 32; ++k) o[20 + k] = prev[k];  // received_hash
-      len = 69;
-    }
+    const uint32_t vote = a.vote[i];
+    uint32_t w[16];
+    w[0] = bswap32(vid);
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      w[1 + k] = (uint32_t)o[4 * k] << 24 | (uint32_t)o[4 * k + 1] << 16 | (uint32_t)o[4 * k + 2] << 8 |
+                 (uint32_t)o[4 * k + 3];
+    w[6] = bswap32(pid);
+    w[7] = bswap32((uint32_t)ts);
+    w[8] = bswap32((uint32_t)(ts >> 32));
     uint32_t h[8];
-    sha256_bytes(nullptr, msg, len, h);
-    uint8_t* vh = o + 20 + (j ? 32 : 0);
-    for (int k = 0; k < 8; ++k) {
-      for (int b = 0; b < 4; ++b) prev[4 * k + b] = (uint8_t)(h[k] >> (24 - 8 * b));
+    sha256_init(h);
+    if (j == 0) {  // 37 bytes: one block
+      w[9] = vote << 24 | 0x00800000u;
+#pragma unroll
+      for (int k = 10; k < 15; ++k) w[k] = 0;
+      w[15] = 37u * 8u;
+      sha256_compress(h, w);
+    } else {       // 69 bytes: received = prev (bytes 37..68), two blocks
+      w[9] = vote << 24 | prev[0] >> 8;
+#pragma unroll
+      for (int k = 1; k < 7; ++k) w[9 + k] = prev[k - 1] << 24 | prev[k] >> 8;
+      uint32_t w2[16];
+      w2[0] = prev[6] << 24 | prev[7] >> 8;
+      w2[1] = prev[7] << 24 | 0x00800000u;
+#pragma unroll
+      for (int k = 2; k < 15; ++k) w2[k] = 0;
+      w2[15] = 69u * 8u;
+      sha256_compress(h, w);
+      sha256_compress(h, w2);
+#pragma unroll
+      for (int k = 0; k < 32; ++k) o[20 + k] = (uint8_t)(prev[k >> 2] >> (24 - 8 * (k & 3)));  // received_hash
     }
-    for (int k = 0; k < 32; ++k) vh[k] = prev[k];
+    uint8_t* vh = o + 20 + (j ? 32 : 0);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) vh[k] = (uint8_t)(h[k >> 2] >> (24 - 8 * (k & 3)));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) prev[k] = h[k];
   }
   hlc_proposal d;
   d.vote_begin = p * a.V;
