@@ -350,6 +350,45 @@ def e2e_leg(eng, w, args, np):
     }
 
 
+def config3_leg(eng, args, torch, synth, DeviceBatch, dev, ct):
+    """Secondary line, SURVEY.md §8(d) config 3: one P2P proposal of 1,000,000 chained votes
+    (n = 1.5M, so the ceil(2n/3) round cap is exactly 1M), generated on the device: the global
+    chain / duplicate hash tables and the tally at scale.  Inputs resident in HBM, outcome asserted
+    (every vote valid, the proposal OK with 1M votes) before the timed calls."""
+    V = 1_000_000
+    t = time.perf_counter()
+    db = DeviceBatch.synthetic(eng, 1, V, 1_500_000, False, synth.config_seed(3), device=dev)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t
+    eng.reserve(db.n, 1, db.bytes_len)
+    s = torch.cuda.Stream(device=dev)
+    eng.validate_proposals_device(db, s.cuda_stream)
+    torch.cuda.synchronize()
+    res = db.results_numpy()
+    assert int(res["status"][0]) == 0 and int(res["total"][0]) == V and (db.status_numpy() == 0).all()
+    eng.take_kernel_time()
+    eng.take_chain_time()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        eng.validate_proposals_device(db, s.cuda_stream)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t) / args.steps
+    rec_ms, rec_n, _, _ = eng.take_kernel_time()
+    ch_ms, ch_n = eng.take_chain_time()
+    ch_s = ch_ms / max(ch_n, 1) / 1e3
+    ch_bytes = ct["bytes_per_vote"] * V + ct["bytes_per_proposal"]
+    return {
+        "metric": "verified votes/s, config 3 (1 P2P proposal, 1,000,000 chained votes, n = 1,500,000)",
+        "value": V / el,
+        "unit": "votes/s",
+        "ms_per_call": el * 1e3,
+        "recovery_ms": rec_ms / max(rec_n, 1),
+        "chain_tally_ms": ch_s * 1e3,
+        "chain_tally_GBps": ch_bytes / max(ch_s, 1e-12) / 1e9,
+        "gen_seconds": gen_s,
+    }
+
+
 CONFIG4_PROPOSALS = 1_562_500   # SURVEY.md §8d config 4: 100,000,000 votes = 1,562,500 x 64
 CONFIG4_SHARDS = 8               # sharded by proposal over one 8-GPU node
 
@@ -377,6 +416,7 @@ def main() -> int:
     ap.add_argument("--no-wire", action="store_true", help="skip the wire-bytes leg (device protobuf decode)")
     ap.add_argument("--no-stream", action="store_true", help="skip the streaming process_incoming_vote leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
+    ap.add_argument("--no-config3", action="store_true", help="skip the config-3 leg (1M-vote chain, ~10 s to generate)")
     args = ap.parse_args()
 
     import numpy as np
@@ -571,6 +611,10 @@ def main() -> int:
         out["end_to_end"] = e2e_leg(eng, w, args, np)
     if w is not None and not args.no_stream:
         out["stream"] = stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch)
+    if world == 1 and not args.no_config3:
+        eng.set_kernel_timing(True)
+        out["config3"] = config3_leg(eng, args, torch, synth, DeviceBatch, dev, ct)
+        eng.set_kernel_timing(False)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w.batch, w.desc, w.now, min(args.cpu_sample_proposals, P),
                                            min(args.cpu_single_proposals, P))

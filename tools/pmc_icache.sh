@@ -6,7 +6,7 @@ for v in ${@:-default}; do
   mkdir -p $OUT
   LIB=""
   [ $v != default ] && LIB=$PWD/hashgraph-like-consensus_amd/lib/variants/libhlc_$v.so
-  BENCH="$PWD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-wire --no-stream"
+  BENCH="$PWD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config3 --no-wire --no-stream"
   ( cd /tmp && export TMPDIR=/tmp && HLC_LIB=$LIB timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --output-format csv -d $OUT -o run -- python3 $BENCH > $OUT/pmc.log 2>&1 ) || { tail -20 $OUT/pmc.log; exit 1; }
   f=$(find $OUT -name "*counter_collection.csv" | head -1)
   python3 - "$f" "$v" <<'PY'

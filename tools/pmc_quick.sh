@@ -4,7 +4,7 @@ set -o pipefail
 TAG=${1:-q}
 OUT=$PWD/gpurun_out/pmc_$TAG
 mkdir -p $OUT
-BENCH="$PWD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-wire --no-stream"
+BENCH="$PWD/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config3 --no-wire --no-stream"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT -o run -- python3 $BENCH > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
 f=$(find $OUT -name "*counter_collection.csv" | head -1)

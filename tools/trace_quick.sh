@@ -4,7 +4,7 @@ set -o pipefail
 TAG=${1:-q}
 OUT=$PWD/gpurun_out/trace_$TAG
 mkdir -p $OUT
-BENCH="$PWD/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-wire --no-stream"
+BENCH="$PWD/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-config3 --no-wire --no-stream"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- python3 $BENCH > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
 f=$(find $OUT -name "*kernel_stats.csv" | head -1)
