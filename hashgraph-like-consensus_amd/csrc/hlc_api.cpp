@@ -260,7 +260,7 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   CHK(c->vote_prop.ensure(n * 4 + 4));
   CHK(c->flag.ensure(16));
   HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(uint32_t), s));
-  HIPCHK(hlc::launch_assign_props(dprops, np, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s));
+  HIPCHK(hlc::launch_assign_props(dprops, np, dv->field_len, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s));
   uint8_t* status = dstatus;
   uint8_t* reason = dreason;
   if (!status) {
@@ -287,7 +287,7 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     HIPCHK(hipEventRecord(ch0, s));
   }
   hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
-                     c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->flag.as<uint32_t>(), s);
+                     c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
   hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
                           c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
                           c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);

@@ -24,7 +24,9 @@ struct Workspace;  // defined in hlc_api.cpp
 // call flags (one device word, cleared by the caller): set by the kernels, read once per call
 constexpr uint32_t FLAG_GENERAL_PATH = 1u;     // some vote exceeds the fused prehash LDS window
 constexpr uint32_t FLAG_LARGE_PROPOSAL = 2u;   // some proposal has > 512 votes (global chain tables)
-hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv, uint32_t* flags,
+constexpr uint32_t FLAG_LARGE_PARENTS = 4u;    // some vote of such a proposal has a parent_hash (the chain table is needed)
+hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, const uint32_t* field_len, uint32_t* vote_prop,
+                               uint64_t nv, uint32_t* flags,
                          hipStream_t s);
 void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
                       int mode, uint64_t* sha_sz, uint64_t* kec_sz, hipStream_t s);
@@ -85,8 +87,10 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
                         uint8_t* status, uint8_t* reason, hipStream_t s);
 // large-proposal chain / duplicate tables: always enqueued, skipped on the device unless the call's
 // flag word has FLAG_LARGE_PROPOSAL (flags == nullptr: always run)
+// (also initialises the per-proposal reduction records `red`: the duplicate test reports from k_tables)
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, const uint32_t* flags, hipStream_t s);
+                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, uint64_t np,
+                   const uint32_t* flags, hipStream_t s);
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
                         uint32_t mask, uint8_t* chain_code, uint32_t* red, uint64_t np, const uint32_t* flags,

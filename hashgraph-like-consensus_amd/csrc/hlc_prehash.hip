@@ -65,13 +65,21 @@ __device__ uint64_t vote_enc_len(const hlc_votes& v, uint64_t i) {
 
 // Block (p, y) of a (proposals x G) grid writes every G-th span of proposal p's vote range: G > 1
 // when the batch's proposals are large on average (config 3: one proposal of 1M votes).
-__global__ void k_assign_props(const hlc_proposal* props, uint32_t* vote_prop, uint32_t* flags) {
+// A large proposal also raises FLAG_LARGE_PARENTS when any of its votes has a parent_hash: only
+// then does k_tables build the vote_hash table the parent lookups need.
+__global__ void k_assign_props(const hlc_proposal* props, const uint32_t* field_len, uint32_t* vote_prop,
+                               uint32_t* flags) {
   const uint32_t p = blockIdx.x;
   const hlc_proposal d = props[p];
-  if (threadIdx.x == 0 && blockIdx.y == 0 && d.vote_count > SMALL_CAP) atomicOr(flags, FLAG_LARGE_PROPOSAL);
+  const bool large = d.vote_count > SMALL_CAP;
+  if (threadIdx.x == 0 && blockIdx.y == 0 && large) atomicOr(flags, FLAG_LARGE_PROPOSAL);
   const uint64_t step = (uint64_t)blockDim.x * gridDim.y;
-  for (uint64_t j = (uint64_t)blockIdx.y * blockDim.x + threadIdx.x; j < d.vote_count; j += step)
+  bool parent = false;
+  for (uint64_t j = (uint64_t)blockIdx.y * blockDim.x + threadIdx.x; j < d.vote_count; j += step) {
     vote_prop[d.vote_begin + j] = p;
+    if (large) parent |= field_len[(d.vote_begin + j) * HLC_NFIELDS + HLC_F_PARENT] != 0;
+  }
+  if (large && __ballot(parent) && (threadIdx.x & 63) == 0) atomicOr(flags, FLAG_LARGE_PARENTS);
 }
 
 __global__ void k_msg_sizes(hlc_votes v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
@@ -354,36 +362,41 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* a, uint32_t al, const ui
   return true;
 }
 
+// Returns EMPTY_SLOT when the key was new, else the slot's index before this insert's max / min.
 template <bool LAST_WINS>
-__device__ void table_insert(uint32_t* tab, uint32_t mask, const hlc_votes& v, const uint32_t* vote_prop,
-                             uint32_t idx, int f) {
+__device__ uint32_t table_insert(uint32_t* tab, uint32_t mask, const hlc_votes& v, const uint32_t* vote_prop,
+                                 uint32_t idx, int f) {
   const uint32_t p = vote_prop[idx];
   const uint8_t* kb = fptr(v, idx, f);
   const uint32_t kl = flen(v, idx, f);
   uint32_t h = key_hash(p, kb, kl) & mask;
   for (;;) {
     uint32_t cur = atomicCAS(&tab[h], EMPTY_SLOT, idx);
-    if (cur == EMPTY_SLOT) return;
-    if (vote_prop[cur] == p && bytes_eq(fptr(v, cur, f), flen(v, cur, f), kb, kl)) {
-      if (LAST_WINS) atomicMax(&tab[h], idx);
-      else atomicMin(&tab[h], idx);
-      return;
-    }
+    if (cur == EMPTY_SLOT) return EMPTY_SLOT;
+    if (vote_prop[cur] == p && bytes_eq(fptr(v, cur, f), flen(v, cur, f), kb, kl))
+      return LAST_WINS ? atomicMax(&tab[h], idx) : atomicMin(&tab[h], idx);
     h = (h + 1) & mask;
   }
 }
 
 __global__ void k_tables(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                         uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, const uint32_t* flags) {
-  if (flags && !(*flags & FLAG_LARGE_PROPOSAL)) return;  // every proposal is small: k_chain_small
+                         uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, const uint32_t* flags) {
+  if (!(*flags & FLAG_LARGE_PROPOSAL)) return;  // every proposal is small: k_chain_small
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t p = vote_prop[i];
   if (p == NO_PROP || props[p].vote_count <= SMALL_CAP) return;  // small: k_chain_small
-  // HashMap<vote_hash, (owner, ts, idx)>: last index wins (utils.rs:180-183)
-  if (props[p].vote_count > 1) table_insert<true>(chain_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_VOTE_HASH);
-  // seen_owners HashSet: the first occurrence is the one later duplicates collide with
-  table_insert<false>(dup_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_OWNER);
+  // HashMap<vote_hash, (owner, ts, idx)>: last index wins (utils.rs:180-183); built only when a
+  // large proposal's vote has a parent_hash to look up
+  if (props[p].vote_count > 1 && (*flags & FLAG_LARGE_PARENTS))
+    (void)table_insert<true>(chain_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_VOTE_HASH);
+  // seen_owners HashSet (session.rs:270-275): the DuplicateVote error sits at the first index whose
+  // owner appeared earlier = the smallest second-smallest index over the owner groups.  Every insert
+  // into an existing group reports max(its index, the group's minimum so far); the smallest report
+  // is that index (the group's second member reports it, or, when it came first, the group's first
+  // member does as it lowers the minimum to itself).
+  const uint32_t prev = table_insert<false>(dup_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_OWNER);
+  if (prev != EMPTY_SLOT) atomicMin(&red[4 * p + 2], max((uint32_t)i, prev) - (uint32_t)props[p].vote_begin);
 }
 
 __device__ __forceinline__ uint32_t table_find(const uint32_t* tab, uint32_t mask, const hlc_votes& v,
@@ -434,10 +447,7 @@ __global__ void __launch_bounds__(CHAIN_TPB) k_chain_check(hlc_votes v, uint64_t
     chain_code[i] = cc;
     if (status[i] != HLC_OK) atomicMin(&red[4 * p + 0], j);
     if (cc != HLC_OK) atomicMin(&red[4 * p + 1], j);
-    uint32_t first = table_find(dup_tab, mask, v, vote_prop, p, fptr(v, i, HLC_F_OWNER),
-                                flen(v, i, HLC_F_OWNER), HLC_F_OWNER);
-    if (first != (uint32_t)i) atomicMin(&red[4 * p + 2], j);
-    yes = v.vote[i] != 0;
+    yes = v.vote[i] != 0;  // (duplicates were reported by k_tables)
   }
   // YES count of large proposals: one atomic per BLOCK when the whole block shares a proposal
   // (config 3: one proposal of 1M votes -- same-address atomics serialise at the L2, so one per
@@ -1056,7 +1066,8 @@ void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_l
   if (n) hipLaunchKernelGGL(k_verify_pre, dim3(blocks_for(n)), dim3(TPB), 0, s, n, sig_len, id_len, pre, verify_out);
 }
 
-hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t* vote_prop, uint64_t nv,
+hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, const uint32_t* field_len, uint32_t* vote_prop,
+                               uint64_t nv,
                                uint32_t* flags, hipStream_t s) {
   if (nv) {
     const hipError_t e = hipMemsetAsync(vote_prop, 0xFF, nv * sizeof(uint32_t), s);
@@ -1064,7 +1075,9 @@ hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, uint32_t*
   }
   // a second grid dimension when proposals are large on average (each block then covers ~4k votes)
   const uint64_t g = np ? std::min<uint64_t>(std::max<uint64_t>((nv / np + 4095) / 4096, 1), 1024) : 1;
-  if (np) hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np, (unsigned)g), dim3(TPB), 0, s, props, vote_prop, flags);
+  if (np)
+    hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np, (unsigned)g), dim3(TPB), 0, s, props, field_len, vote_prop,
+                       flags);
   return hipSuccess;
 }
 
@@ -1112,14 +1125,16 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
 }
 
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, const uint32_t* flags, hipStream_t s) {
+                   uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, uint64_t np,
+                   const uint32_t* flags, hipStream_t s) {
+  if (np) hipLaunchKernelGGL(k_red_init, dim3((unsigned)((np + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np);
   if (!n) return;
   const uint64_t words = (uint64_t)mask + 1;
   const unsigned cb = (unsigned)std::min<uint64_t>((words + TPB - 1) / TPB, 4096);
-  hipLaunchKernelGGL(k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PROPOSAL, chain_tab, words);
+  hipLaunchKernelGGL(k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PARENTS, chain_tab, words);
   hipLaunchKernelGGL(k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PROPOSAL, dup_tab, words);
   hipLaunchKernelGGL(k_tables, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, chain_tab, dup_tab,
-                     mask, flags);
+                     mask, red, flags);
 }
 
 void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
@@ -1134,8 +1149,7 @@ void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab, uint32_t mask,
                         uint8_t* chain_code, uint32_t* red, uint64_t np, const uint32_t* flags, hipStream_t s) {
-  if (!np) return;
-  hipLaunchKernelGGL(k_red_init, dim3((unsigned)((np + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np);
+  if (!np) return;  // (red initialised by launch_tables)
   if (n)
     hipLaunchKernelGGL(k_chain_check, dim3((unsigned)((n + CHAIN_TPB - 1) / CHAIN_TPB)), dim3(CHAIN_TPB), 0, s, *v, n,
                        vote_prop, props, status,

@@ -113,6 +113,23 @@ def test_gpu_chain_and_duplicate_mutations(engine):
     assert {11, 12, 13}.issubset(got), got
 
 
+def test_gpu_chain_and_duplicate_mutations_large(engine):
+    """The same chain-level mutations in proposals of 600 votes (> 512: the global-table path,
+    k_tables / k_chain_check), including parent_hash links (the vote_hash table is built only when
+    a vote has one) and duplicate owners (reported by the owner-table inserts)."""
+    w = oracle_workload(12, 600, 600, True, 0x484C4307)
+    batch, desc, kinds = byzantine(w, fraction=1 / 300, seed=5,
+                                   kinds_pool=["bad_received", "parent_other", "ts_regress", "duplicate", "high_s"])
+    assert {"parent_other", "duplicate"}.issubset(set(kinds))
+    res, vst = compare(engine, batch, desc, w.now, "chain-mix-large")
+    got = set(int(s) for s in res["status"])
+    assert len(got - {0}) >= 2, got
+    # a large proposal whose only mutation is a duplicate owner: the first repeat index, exactly
+    w2 = oracle_workload(2, 600, 600, True, 0x484C4308)
+    batch2, desc2, kinds2 = byzantine(w2, fraction=1 / 600, seed=9, kinds_pool=["duplicate"])
+    compare(engine, batch2, desc2, w2.now, "duplicate-large")
+
+
 def test_gpu_generator_matches_oracle_generator(engine):
     a = synth.generate(4, 16, 16, True, 77, *synth.engine_signers(engine))
     b = oracle_workload(4, 16, 16, True, 77)
