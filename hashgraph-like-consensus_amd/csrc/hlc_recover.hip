@@ -8,7 +8,10 @@ namespace hlc {
 
 namespace {
 
-constexpr int REC_TPB = 256;
+#ifndef HLC_REC_TPB
+#define HLC_REC_TPB 256
+#endif
+constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
 #ifndef HLC_REC_WAVES
 #define HLC_REC_WAVES 2  // waves per SIMD the register allocator must admit for k_rec_main: with dynamic work
                          // hand-out 2 (256 VGPRs, no spills) beats 3 and 4 by 2.5% (profiles/r02_ab_waves_dynamic.txt)
