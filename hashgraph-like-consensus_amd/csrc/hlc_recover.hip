@@ -154,10 +154,12 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
 #endif
 }
 
-// ---- final: batched Z^-1 (one safegcd per REC_BATCH votes), affine, keccak, owner compare ----
-__global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, const uint8_t* pre, const uint8_t* bytes,
-                                                        const uint64_t* id_off, size_t off_stride, uint8_t* state,
-                                                        const uint32_t* q, uint32_t* pfx, uint8_t* addr_out) {
+// ---- final: batched Z^-1 (one safegcd per REC_BATCH votes) and affine Q, then (k_rec_addr, one
+// lane per vote at full occupancy) keccak of X || Y and the owner compare.  Split in two because
+// the eight keccak-f of a lane's batch made k_rec_final one long dependent chain per lane at ~1.2
+// waves/SIMD (latency-bound); the address stage runs 8x as many waves. ----
+__global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, const uint8_t* pre, uint8_t* state,
+                                                        uint32_t* q, uint32_t* pfx) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= L) return;
   fe acc;
@@ -191,21 +193,33 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, 
     fe_mul(y, y, zi3);
     fe_normalize(x, x);
     fe_normalize(y, y);
-    uint32_t addr[5];
-    pubkey_address(x, y, addr);
-    const uint8_t* id = bytes + id_off[i * off_stride];
-    uint32_t diff = 0;
+    store_fe_ws(x, q + i, n);  // affine X, Y over the Jacobian ones (k_rec_addr reads them)
+    store_fe_ws(y, q + (size_t)8 * n + i, n);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rec_addr(uint64_t n, const uint8_t* pre, const uint8_t* bytes,
+                                                  const uint64_t* id_off, size_t off_stride, uint8_t* state,
+                                                  const uint32_t* q, uint8_t* addr_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) return;
+  fe x, y;
+  load_fe_ws(x, q + i, n);
+  load_fe_ws(y, q + (size_t)8 * n + i, n);
+  uint32_t addr[5];
+  pubkey_address(x, y, addr);
+  const uint8_t* id = bytes + id_off[i * off_stride];
+  uint32_t diff = 0;
 #pragma unroll
-    for (int w = 0; w < 5; ++w) diff |= addr[w] ^ load_le32(id + 4 * w);
-    state[i] = diff == 0 ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
-    if (addr_out) {
+  for (int w = 0; w < 5; ++w) diff |= addr[w] ^ load_le32(id + 4 * w);
+  state[i] = diff == 0 ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
+  if (addr_out) {
 #pragma unroll
-      for (int w = 0; w < 5; ++w) {
-        addr_out[20 * i + 4 * w] = (uint8_t)addr[w];
-        addr_out[20 * i + 4 * w + 1] = (uint8_t)(addr[w] >> 8);
-        addr_out[20 * i + 4 * w + 2] = (uint8_t)(addr[w] >> 16);
-        addr_out[20 * i + 4 * w + 3] = (uint8_t)(addr[w] >> 24);
-      }
+    for (int w = 0; w < 5; ++w) {
+      addr_out[20 * i + 4 * w] = (uint8_t)addr[w];
+      addr_out[20 * i + 4 * w + 1] = (uint8_t)(addr[w] >> 8);
+      addr_out[20 * i + 4 * w + 2] = (uint8_t)(addr[w] >> 16);
+      addr_out[20 * i + 4 * w + 3] = (uint8_t)(addr[w] >> 24);
     }
   }
 }
@@ -362,8 +376,9 @@ void launch_recover_main(uint64_t n, const uint8_t* pre, const uint32_t* z_diges
   if (blocks > need) blocks = need;
   hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, z_digest, bytes, sig_off,
                      off_stride, gcomb, scratch, (uint64_t)blocks * REC_TPB, verify_out, b.rec, b.q, force_exact, b.ctr);
-  hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, pre, bytes, id_off, off_stride, verify_out,
-                     b.q, b.pfx, addr_out);
+  hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, pre, verify_out, b.q, b.pfx);
+  hipLaunchKernelGGL(k_rec_addr, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, pre, bytes, id_off, off_stride,
+                     verify_out, b.q, addr_out);
 }
 
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
