@@ -71,6 +71,7 @@ struct hlc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;                        // the recovery prep stage, concurrent with the prehash
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // caller stream -> aux -> caller stream
+  hipEvent_t ev_fork_chain = nullptr, ev_join_chain = nullptr;  // the small-proposal chain kernel on aux
   std::mutex mu;
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
@@ -84,7 +85,7 @@ struct hlc_ctx {
   // measurement hooks
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, rec_prep_ev, call_ev, chain_ev;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, rec_prep_ev, call_ev, chain_ev, chain_aux_ev;
   hipEvent_t take_event() {
     if (ev_pool.empty()) {
       hipEvent_t e = nullptr;
@@ -99,8 +100,11 @@ struct hlc_ctx {
     for (auto e : ev_pool) (void)hipEventDestroy(e);
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : rec_prep_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    if (ev_fork_chain) (void)hipEventDestroy(ev_fork_chain);
+    if (ev_join_chain) (void)hipEventDestroy(ev_join_chain);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   }
@@ -198,7 +202,7 @@ int ensure_fbtab(hlc_ctx* c) {
 // signature recovery, status assembly.  c->flag must hold the flags of the mapping step (cleared
 // or set by launch_assign_props).  Everything is enqueued on `s`: no host synchronisation.
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t now,
-               uint8_t* status, uint8_t* reason, uint8_t* drec, hipStream_t s) {
+               uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, hipStream_t s) {
   const uint64_t n = dv->n;
   CHK(c->pre.ensure(n));
   CHK(c->pre_reason.ensure(n));
@@ -241,7 +245,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     c->rec_ev.emplace_back(r0, r1);
   }
   hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
-                          c->verify.as<uint8_t>(), status, reason, s);
+                          c->verify.as<uint8_t>(), status, reason, red, s);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -271,7 +275,6 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     CHK(c->reason.ensure(n + 1));
     reason = c->reason.as<uint8_t>();
   }
-  if (n) CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, now, status, reason, drec, s));
   CHK(c->chain_code.ensure(n + 1));
   CHK(c->red.ensure(np * 16 + 16));
   // proposals > 512 votes use global chain / duplicate tables; the kernels are always enqueued and
@@ -280,18 +283,34 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   while (cap < 2 * n) cap <<= 1;
   CHK(c->chain_tab.ensure(cap * 4));
   CHK(c->dup_tab.ensure(cap * 4));
-  hipEvent_t ch0 = nullptr, ch1 = nullptr;
-  if (c->timing) {  // chain check + duplicate detection + tally bracket
+  hlc::launch_red_init(c->red.as<uint32_t>(), np, s);
+  // The small proposals' chain / duplicate / YES kernel needs no vote statuses (k_vote_status
+  // reports each proposal's first failing vote), so it runs on the aux stream, after the recovery's
+  // prep stage, beside the prehash and recovery kernels; joined back before k_finalize.
+  HIPCHK(hipEventRecord(c->ev_fork_chain, s));
+  HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork_chain, 0));
+  if (n) CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, now, status, reason, drec, c->red.as<uint32_t>(), s));
+  hipEvent_t cs0 = nullptr, cs1 = nullptr, ch0 = nullptr, ch1 = nullptr;
+  if (c->timing) {  // chain check + duplicate detection + tally: the aux bracket + the caller-stream one
+    cs0 = c->take_event();
+    cs1 = c->take_event();
     ch0 = c->take_event();
     ch1 = c->take_event();
-    HIPCHK(hipEventRecord(ch0, s));
+    HIPCHK(hipEventRecord(cs0, c->aux));
   }
+  hlc::launch_chain_small(dv, dprops, np, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), c->aux);
+  if (c->timing) {
+    HIPCHK(hipEventRecord(cs1, c->aux));
+    c->chain_aux_ev.emplace_back(cs0, cs1);
+  }
+  HIPCHK(hipEventRecord(c->ev_join_chain, c->aux));
+  if (c->timing) HIPCHK(hipEventRecord(ch0, s));
   hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
                      c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
   hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
                           c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
                           c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
-  hlc::launch_chain_small(dv, dprops, np, status, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), s);
+  HIPCHK(hipStreamWaitEvent(s, c->ev_join_chain, 0));
   hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
   HIPCHK(hipGetLastError());
   if (c->timing) {
@@ -513,7 +532,9 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork_chain, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join_chain, hipEventDisableTiming) != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     delete c;
@@ -609,14 +630,21 @@ int hlc_ctx_take_chain_time(hlc_ctx* ctx, double* chain_ms, uint64_t* launches) 
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
   double sum = 0;
-  for (auto& pr : ctx->chain_ev) {
-    HIPCHK(hipEventSynchronize(pr.second));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
-    sum += ms;
+  for (auto* vec : {&ctx->chain_ev, &ctx->chain_aux_ev}) {
+    for (auto& pr : *vec) {
+      HIPCHK(hipEventSynchronize(pr.second));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+      sum += ms;
+    }
   }
   if (chain_ms) *chain_ms = sum;
   if (launches) *launches = ctx->chain_ev.size();
+  for (auto& pr : ctx->chain_aux_ev) {
+    ctx->ev_pool.push_back(pr.first);
+    ctx->ev_pool.push_back(pr.second);
+  }
+  ctx->chain_aux_ev.clear();
   for (auto& pr : ctx->chain_ev) {
     ctx->ev_pool.push_back(pr.first);
     ctx->ev_pool.push_back(pr.second);
@@ -790,7 +818,7 @@ int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vses
   }
   CHK(ctx->flag.ensure(16));
   HIPCHK(hipMemsetAsync(ctx->flag.p, 0, sizeof(uint32_t), s));
-  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, now, ctx->status.as<uint8_t>(), rs, nullptr, s));
+  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, now, ctx->status.as<uint8_t>(), rs, nullptr, nullptr, s));
   // 2. each session's votes in delivery order
   CHK(ctx->s_keys.ensure(n * 4 + 4));
   CHK(ctx->s_iota.ensure(n * 4 + 4));

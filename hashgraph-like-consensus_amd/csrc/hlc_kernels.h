@@ -84,10 +84,12 @@ size_t gcomb_words();
 // ---- validation tail ----
 void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         uint64_t now, const uint8_t* pre, const uint8_t* pre_reason, const uint8_t* verify,
-                        uint8_t* status, uint8_t* reason, hipStream_t s);
+                        uint8_t* status, uint8_t* reason, uint32_t* red, hipStream_t s);
+// per-proposal reduction records: first failing vote / chain error / duplicate = none, YES = 0
+void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s);
 // large-proposal chain / duplicate tables: always enqueued, skipped on the device unless the call's
 // flag word has FLAG_LARGE_PROPOSAL (flags == nullptr: always run)
-// (also initialises the per-proposal reduction records `red`: the duplicate test reports from k_tables)
+// (the duplicate test reports into `red` from k_tables)
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                    uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, uint64_t np,
                    const uint32_t* flags, hipStream_t s);
@@ -98,10 +100,10 @@ void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
 // batched handle_consensus_timeout: new state + status per session
 void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status, hipStream_t s);
 // proposals with <= 512 votes: chain / duplicate / YES count in LDS, one wave per proposal
-// (writes chain_code and red for those; the global-table kernels skip them).  Run after
-// launch_chain_check (which clears red).
-void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, const uint8_t* status,
-                        uint8_t* chain_code, uint32_t* red, hipStream_t s);
+// (writes chain_code and red[4p+1..3] for those; the global-table kernels skip them).  Needs no vote
+// statuses: validate_device runs it on the aux stream beside the recovery, after launch_red_init.
+void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint8_t* chain_code,
+                        uint32_t* red, hipStream_t s);
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
                      const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red,
                      hlc_result* out, hipStream_t s);

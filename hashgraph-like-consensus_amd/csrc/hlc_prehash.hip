@@ -266,9 +266,11 @@ __global__ void k_pre_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop,
 }
 
 // validate_vote tail (utils.rs:154-168): scheme result, then timestamps
+// With red != nullptr also the first failing vote per proposal (red[4p + 0], the local index): the
+// chain / duplicate / tally kernels then need no vote statuses and run beside the recovery.
 __global__ void k_vote_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                               uint64_t now, const uint8_t* pre, const uint8_t* pre_reason,
-                              const uint8_t* verify, uint8_t* status, uint8_t* reason) {
+                              const uint8_t* verify, uint8_t* status, uint8_t* reason, uint32_t* red) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t st = pre[i], rs = pre_reason[i];
@@ -291,6 +293,10 @@ __global__ void k_vote_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop
   }
   status[i] = st;
   reason[i] = rs;
+  if (red && st != HLC_OK) {
+    const uint32_t p = vote_prop[i];
+    if (p != NO_PROP) atomicMin(&red[4 * p + 0], (uint32_t)(i - props[p].vote_begin));
+  }
 }
 
 // ---------------- chain / duplicate tables ----------------
@@ -445,8 +451,7 @@ __global__ void __launch_bounds__(CHAIN_TPB) k_chain_check(hlc_votes v, uint64_t
       }
     }
     chain_code[i] = cc;
-    if (status[i] != HLC_OK) atomicMin(&red[4 * p + 0], j);
-    if (cc != HLC_OK) atomicMin(&red[4 * p + 1], j);
+    if (cc != HLC_OK) atomicMin(&red[4 * p + 1], j);  // (first failing vote: k_vote_status)
     yes = v.vote[i] != 0;  // (duplicates were reported by k_tables)
   }
   // YES count of large proposals: one atomic per BLOCK when the whole block shares a proposal
@@ -523,8 +528,7 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 }
 
 __global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hlc_proposal* props,
-                                                           const uint8_t* status, uint8_t* chain_code,
-                                                           uint32_t* red) {
+                                                           uint8_t* chain_code, uint32_t* red) {
   __shared__ uint32_t h_own[SMALL_CAP], h_vh[SMALL_CAP];
   const uint32_t p = blockIdx.x;
   const hlc_proposal d = props[p];
@@ -538,7 +542,7 @@ __global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hl
   }
   __syncthreads();
   const uint32_t none = 0xFFFFFFFFu;
-  uint32_t bad = none, chain = none, dup = none, yes = 0;
+  uint32_t chain = none, dup = none, yes = 0;
   for (uint32_t j = threadIdx.x; j < nv; j += SMALL_TPB) {
     const uint64_t i = b0 + j;
     uint8_t cc = HLC_OK;
@@ -571,7 +575,6 @@ __global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hl
       }
     }
     chain_code[i] = cc;
-    if (status[i] != HLC_OK) bad = min(bad, j);
     if (cc != HLC_OK) chain = min(chain, j);
     // seen_owners: an earlier vote with the same owner makes this one the duplicate
     const uint32_t ho = h_own[j];
@@ -584,14 +587,12 @@ __global__ void __launch_bounds__(SMALL_TPB) k_chain_small(hlc_votes v, const hl
     }
     yes += v.vote[i] != 0;
   }
-  bad = wave_min(bad);
   chain = wave_min(chain);
   dup = wave_min(dup);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) yes += (uint32_t)__shfl_xor((int)yes, off);
   if (threadIdx.x == 0) {
-    red[4 * p + 0] = bad;
-    red[4 * p + 1] = chain;
+    red[4 * p + 1] = chain;  // (red[4p + 0], the first failing vote: k_vote_status)
     red[4 * p + 2] = dup;
     red[4 * p + 3] = yes;
   }
@@ -1118,16 +1119,21 @@ void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop
 
 void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         uint64_t now, const uint8_t* pre, const uint8_t* pre_reason, const uint8_t* verify,
-                        uint8_t* status, uint8_t* reason, hipStream_t s) {
+                        uint8_t* status, uint8_t* reason, uint32_t* red, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_vote_status, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, now, pre,
-                       pre_reason, verify, status, reason);
+                       pre_reason, verify, status, reason, red);
+}
+
+void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s) {
+  if (np) hipLaunchKernelGGL(k_red_init, dim3((unsigned)((np + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np);
 }
 
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                    uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, uint64_t np,
                    const uint32_t* flags, hipStream_t s) {
-  if (np) hipLaunchKernelGGL(k_red_init, dim3((unsigned)((np + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np);
+  (void)red;
+  (void)np;  // (red is initialised by launch_red_init before the vote stage)
   if (!n) return;
   const uint64_t words = (uint64_t)mask + 1;
   const unsigned cb = (unsigned)std::min<uint64_t>((words + TPB - 1) / TPB, 4096);
@@ -1161,10 +1167,9 @@ void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state,
   if (n) hipLaunchKernelGGL(k_timeout, dim3(blocks_for(n)), dim3(TPB), 0, s, n, ss, out_state, out_status);
 }
 
-void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, const uint8_t* status,
-                        uint8_t* chain_code, uint32_t* red, hipStream_t s) {
-  if (np)
-    hipLaunchKernelGGL(k_chain_small, dim3((unsigned)np), dim3(SMALL_TPB), 0, s, *v, props, status, chain_code, red);
+void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint8_t* chain_code,
+                        uint32_t* red, hipStream_t s) {
+  if (np) hipLaunchKernelGGL(k_chain_small, dim3((unsigned)np), dim3(SMALL_TPB), 0, s, *v, props, chain_code, red);
 }
 
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
