@@ -43,7 +43,7 @@ W_IMPL_LIMB_PRODUCTS_PER_VOTE = ROOFLINE["implementation"]["limb_products_per_vo
 # rocprofv3 passes of this bench (tools/profile.sh), committed under profiles/: kernel-trace
 # summary, FETCH_SIZE / WRITE_SIZE and the VALU / wave counters of the recovery kernels.
 PMC_PROFILE = os.path.join(ROOT, ROOFLINE["profile"])
-REC_KERNELS = ("k_rec_prep", "k_rec_main", "k_rec_final", "k_rec_addr")
+REC_KERNELS = ("k_rec_prep", "k_rec_main", "k_rec_comb", "k_rec_final", "k_rec_addr")
 
 
 def _pmc_rows(name: str):
@@ -565,7 +565,7 @@ def main() -> int:
         "counters_per_step": counters,
         "roofline": {
             "bound": "valu",
-            "kernel": "recovery: k_rec_prep (second stream) + k_rec_main + k_rec_final + k_rec_addr (HIP-event brackets)",
+            "kernel": "recovery: k_rec_prep + k_rec_main (second stream, beside the prehash) + k_rec_comb + k_rec_final + k_rec_addr (HIP-event brackets)",
             "achieved": achieved,
             "peak": MAD_PEAK_T_PER_S,
             "unit": "T limb-products/s (32x32->64, v_mad_u64_u32)",

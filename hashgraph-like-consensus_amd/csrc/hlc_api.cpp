@@ -71,7 +71,6 @@ struct hlc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;                        // the recovery prep stage, concurrent with the prehash
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // caller stream -> aux -> caller stream
-  hipEvent_t ev_fork_chain = nullptr, ev_join_chain = nullptr;  // the small-proposal chain kernel on aux
   std::mutex mu;
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
@@ -103,8 +102,6 @@ struct hlc_ctx {
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
-    if (ev_fork_chain) (void)hipEventDestroy(ev_fork_chain);
-    if (ev_join_chain) (void)hipEventDestroy(ev_join_chain);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   }
@@ -200,9 +197,13 @@ int ensure_fbtab(hlc_ctx* c) {
 // for votes already mapped to proposals (vote_prop, NO_PROP = skip): fused LDS prehash, the
 // streaming general path for oversize votes (skipped on the device when no vote needs it),
 // signature recovery, status assembly.  c->flag must hold the flags of the mapping step (cleared
-// or set by launch_assign_props).  Everything is enqueued on `s`: no host synchronisation.
-int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t now,
-               uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, hipStream_t s) {
+// or set by launch_assign_props).  Everything is enqueued on `s` (and the context's aux stream,
+// forked from and joined back into `s`): no host synchronisation.
+// chain_code != nullptr: also the small proposals' chain / duplicate / YES kernel (it needs no
+// vote statuses), on `s` beside the recovery's main stage.
+int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t np,
+               uint64_t now, uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, uint8_t* chain_code,
+               hipStream_t s) {
   const uint64_t n = dv->n;
   CHK(c->pre.ensure(n));
   CHK(c->pre_reason.ensure(n));
@@ -210,9 +211,11 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   CHK(c->kec_dig.ensure(n * 32));
   CHK(ensure_recover_scratch(c));
   CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
-  // the recovery's prep stage (signature parse, batched r^-1, GLV digits) needs only the signatures:
-  // it runs on the context's aux stream while the prehash kernels run on `s`; `s` waits for it
-  // before the main stage.  Measured recovery time = prep bracket (aux) + main/final bracket (s).
+  // The recovery's prep stage (signature parse, batched r^-1, GLV digits) and main stage (R, its
+  // table, the u2 R chain: ~93% of the recovery) need only the signatures, so they run on the
+  // context's aux stream while the prehash kernels (and the small-proposal chain kernel) run on
+  // `s`; `s` waits for them before the finish (u1 G with u1 = -z/r from the prehash, Z^-1,
+  // address).  Measured recovery time = prep bracket (aux) + main start (aux) .. finish end (s).
   HIPCHK(hipEventRecord(c->ev_fork, s));
   HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   hipEvent_t p0 = nullptr, p1 = nullptr, r0 = nullptr, r1 = nullptr;
@@ -228,18 +231,33 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   if (c->timing) {
     HIPCHK(hipEventRecord(p1, c->aux));
     c->rec_prep_ev.emplace_back(p0, p1);
+    HIPCHK(hipEventRecord(r0, c->aux));
   }
+  hlc::launch_recover_main(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, c->rec_scratch.as<uint32_t>(),
+                           c->rec_lanes, c->rec_work.as<uint32_t>(), c->aux, c->rec_force_exact);
   HIPCHK(hipEventRecord(c->ev_join, c->aux));
   hlc::launch_prehash_fused(dv, n, vote_prop, dprops, c->kec_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
                             c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
   hlc::launch_prehash_stream(dv, n, vote_prop, dprops, c->flag.as<uint32_t>(), c->kec_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
   if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
+  if (chain_code) {
+    hipEvent_t cs0 = nullptr, cs1 = nullptr;
+    if (c->timing) {
+      cs0 = c->take_event();
+      cs1 = c->take_event();
+      HIPCHK(hipEventRecord(cs0, s));
+    }
+    hlc::launch_chain_small(dv, dprops, np, chain_code, red, s);
+    if (c->timing) {
+      HIPCHK(hipEventRecord(cs1, s));
+      c->chain_aux_ev.emplace_back(cs0, cs1);
+    }
+  }
   HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
-  if (c->timing) HIPCHK(hipEventRecord(r0, s));
-  hlc::launch_recover_main(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_SIGNATURE,
-                           dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_scratch.as<uint32_t>(),
-                           c->rec_lanes, c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact);
+  hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_OWNER,
+                             HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
+                             drec, s, c->rec_force_exact);
   if (c->timing) {
     HIPCHK(hipEventRecord(r1, s));
     c->rec_ev.emplace_back(r0, r1);
@@ -284,33 +302,22 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   CHK(c->chain_tab.ensure(cap * 4));
   CHK(c->dup_tab.ensure(cap * 4));
   hlc::launch_red_init(c->red.as<uint32_t>(), np, s);
-  // The small proposals' chain / duplicate / YES kernel needs no vote statuses (k_vote_status
-  // reports each proposal's first failing vote), so it runs on the aux stream, after the recovery's
-  // prep stage, beside the prehash and recovery kernels; joined back before k_finalize.
-  HIPCHK(hipEventRecord(c->ev_fork_chain, s));
-  HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork_chain, 0));
-  if (n) CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, now, status, reason, drec, c->red.as<uint32_t>(), s));
-  hipEvent_t cs0 = nullptr, cs1 = nullptr, ch0 = nullptr, ch1 = nullptr;
-  if (c->timing) {  // chain check + duplicate detection + tally: the aux bracket + the caller-stream one
-    cs0 = c->take_event();
-    cs1 = c->take_event();
+  // (the small proposals' chain / duplicate / YES kernel runs inside vote_stage, beside the
+  // recovery's main stage: k_vote_status reports each proposal's first failing vote)
+  if (n)
+    CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, np, now, status, reason, drec, c->red.as<uint32_t>(),
+                   c->chain_code.as<uint8_t>(), s));
+  hipEvent_t ch0 = nullptr, ch1 = nullptr;
+  if (c->timing) {  // chain check + duplicate detection + tally (+ k_chain_small's bracket in vote_stage)
     ch0 = c->take_event();
     ch1 = c->take_event();
-    HIPCHK(hipEventRecord(cs0, c->aux));
+    HIPCHK(hipEventRecord(ch0, s));
   }
-  hlc::launch_chain_small(dv, dprops, np, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), c->aux);
-  if (c->timing) {
-    HIPCHK(hipEventRecord(cs1, c->aux));
-    c->chain_aux_ev.emplace_back(cs0, cs1);
-  }
-  HIPCHK(hipEventRecord(c->ev_join_chain, c->aux));
-  if (c->timing) HIPCHK(hipEventRecord(ch0, s));
   hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
                      c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
   hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
                           c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
                           c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
-  HIPCHK(hipStreamWaitEvent(s, c->ev_join_chain, 0));
   hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
   HIPCHK(hipGetLastError());
   if (c->timing) {
@@ -532,9 +539,7 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork_chain, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join_chain, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     delete c;
@@ -818,7 +823,7 @@ int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vses
   }
   CHK(ctx->flag.ensure(16));
   HIPCHK(hipMemsetAsync(ctx->flag.p, 0, sizeof(uint32_t), s));
-  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, now, ctx->status.as<uint8_t>(), rs, nullptr, nullptr, s));
+  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, n_sessions, now, ctx->status.as<uint8_t>(), rs, nullptr, nullptr, nullptr, s));
   // 2. each session's votes in delivery order
   CHK(ctx->s_keys.ensure(n * 4 + 4));
   CHK(ctx->s_iota.ensure(n * 4 + 4));

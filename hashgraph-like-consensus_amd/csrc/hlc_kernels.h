@@ -60,21 +60,23 @@ void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop
 // ---- recovery ----
 // items: i in [0, n) with pre[i] == PRE_PENDING; signature bytes / identity bytes read from
 // bytes + sig_off[i*stride_f] etc.  verify_out[i]: HLC_VERIFY_TRUE/FALSE or 1+SCHEME.
-// three kernels (hlc_recover.hpp): k_rec_prep, k_rec_main, k_rec_final; `work` holds
+// kernels (hlc_recover.hip): k_rec_prep, k_rec_main, k_rec_comb, k_rec_final, k_rec_addr; `work` holds
 // recover_work_words(n) words of per-vote records for the call
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                     const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* sig_len,
                     size_t len_stride, const uint32_t* gtab, uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work,
                     uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0);
-// the same in two halves: the prep stage reads only the signatures (65-byte ones by sig_len), so a
-// caller may enqueue it on a second stream concurrently with the prehash kernels, and the main +
-// final stages once both are done
+// the same in three parts: the prep stage reads only the signatures (65-byte ones by sig_len) and
+// the main stage (u2 R) only the prep records, so a caller may enqueue both on a second stream
+// concurrently with the prehash kernels; the finish (k_rec_comb: u1 G + the addition; k_rec_final;
+// k_rec_addr) once both are done
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s);
-void launch_recover_main(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
-                         const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gtab,
-                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, uint8_t* verify_out,
-                         uint8_t* addr_out, hipStream_t s, int force_exact = 0);
+void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
+                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact = 0);
+void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
+                           const uint64_t* id_off, size_t off_stride, const uint32_t* gtab, uint32_t* work,
+                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0);
 uint64_t recover_grid_lanes();
 uint64_t recover_scratch_words();  // per-lane workspace words of k_rec_main
 uint64_t recover_work_words(uint64_t n);

@@ -26,6 +26,10 @@ constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
 // run (hlc_api.cpp vote_stage); a vote's scheme error goes to bits 8-15 of its record flags and
 // the main stage turns it into the vote's state.
 constexpr int PREP_TPB = 64;
+constexpr uint32_t PREP_SKIP = 0xFFu;  // record flags bits 8-15: no 65-byte signature, not parsed
+// k_rec_main -> k_rec_comb, one byte per vote: u2 R finite / at infinity / nothing to recover, or
+// 1 + the scheme code (prep's v / r / s checks, or no point R)
+constexpr uint8_t MST_OK = 0x00, MST_INF = 0xFE, MST_SKIP = 0xFF;
 
 HLC_DEV bool prep_sig(const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len,
                       size_t len_stride, uint64_t i, fe& r, fe& s, int& parity, int& code) {
@@ -52,7 +56,10 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
     if (i >= n) break;
     fe r, s;
     int parity, code;
-    if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) continue;
+    if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) {
+      rec[(size_t)REC_FLAGS * n + i] = PREP_SKIP << 8;
+      continue;
+    }
     if (code != SCHEME_NONE) {
       rec[(size_t)REC_FLAGS * n + i] = (uint32_t)code << 8;
       continue;
@@ -77,18 +84,19 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
   }
 }
 
-// ---- main: decompress + u1 G + u2 R, one vote per lane at a time (persistent grid) ----
+// ---- main: decompress + u2 R, one vote per lane at a time (persistent grid) ----
+// Needs only the prep stage's records and the signatures, not the prehash: it runs beside the
+// prehash kernels (hlc_api.cpp vote_stage), on every vote with a parsed 65-byte signature (the
+// pre-checks' verdicts are not known yet; k_rec_comb discards the votes they reject).
 // Work is handed out dynamically, 64 consecutive votes per wave per grab (one atomic by lane 0).
 // The SIMD's arbiter favours its oldest wave, so with a static vote-per-lane stride the oldest of
 // the 3 resident waves finishes its share long before the youngest, which then runs alone at
 // lone-wave efficiency (measured with HLC_CLOCK_PROBE: 4-vote blocks done at 3.5 ms, the last
 // 3-vote blocks at 7.0 ms of one launch); grabbing keeps every wave busy until the work runs out.
-__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n, const uint8_t* pre,
-                                                                     const uint32_t* z_digest, const uint8_t* bytes,
+__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n, const uint8_t* bytes,
                                                                      const uint64_t* sig_off, size_t off_stride,
-                                                                     const uint32_t* gcomb, uint32_t* scratch,
-                                                                     uint64_t lanes, uint8_t* state,
-                                                                     const uint32_t* rec, uint32_t* q,
+                                                                     uint32_t* scratch, uint64_t lanes,
+                                                                     const uint32_t* rec, uint32_t* q, uint8_t* mst,
                                                                      int force_exact, unsigned long long* ctr) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
@@ -115,32 +123,20 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
 #ifdef HLC_CLOCK_PROBE
     ++done;
 #endif
-    if (pre && pre[i] != PRE_PENDING) continue;  // not recovered: state untouched (may hold a caller code)
     const uint32_t prep_code = (rec[(size_t)REC_FLAGS * n + i] >> 8) & 0xFFu;
-    if (prep_code != SCHEME_NONE) {  // v / r / s rejected by the prep stage
-      state[i] = (uint8_t)(1 + prep_code);
+    if (prep_code != SCHEME_NONE) {  // no 65-byte signature, or v / r / s rejected by the prep stage
+      mst[i] = prep_code == PREP_SKIP ? MST_SKIP : (uint8_t)(1 + prep_code);
       continue;
     }
-    fe r, z, u1;
-    bool neg_g;
+    fe r, qx, qy, qz;
+    bool inf = false;
     fe_load_be(r, bytes + sig_off[i * off_stride]);
-    fe_from_digest(z, z_digest + 8 * i);
-    rec_u1(z, rec + i, n, u1, neg_g);
-    fe qx, qy, qz;
-#ifdef HLC_FIELD32
-    // A/B variant (make variants): the saturated 8 x 32 field layer
-    gej acc;
-    int code = rec_main(r, u1, neg_g, rec + i, n, acc, gcomb, ws, lanes, tab);
-    if (code == SCHEME_NONE) {
-      qx = acc.x;
-      qy = acc.y;
-      qz = acc.z;
+    const int code = rec_u2r29(r, rec + i, n, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0);
+    if (code != SCHEME_NONE) {
+      mst[i] = (uint8_t)(1 + code);
+      continue;
     }
-#else
-    const int code = rec_main29(r, u1, neg_g, rec + i, n, qx, qy, qz, gcomb, ws, lanes, tab, force_exact != 0);
-#endif
-    state[i] = code != SCHEME_NONE ? (uint8_t)(1 + code) : REC_PENDING;
-    if (code != SCHEME_NONE) continue;
+    mst[i] = inf ? MST_INF : MST_OK;
     store_fe_ws(qx, q + i, n);
     store_fe_ws(qy, q + (size_t)8 * n + i, n);
     store_fe_ws(qz, q + (size_t)16 * n + i, n);
@@ -152,6 +148,38 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
            (unsigned long long)dw, dw ? (double)dc / ((double)dw * 10.0) : 0.0);
   }
 #endif
+}
+
+#ifndef HLC_COMB_WAVES
+#define HLC_COMB_WAVES 2  // 200 VGPRs, no spills (3 and 4 waves spill 124 / 284 B per lane)
+#endif
+// ---- comb: after the prehash, one lane per vote at full occupancy: u1 = -z / r, u1 G by the comb
+// (12 mixed additions from the HBM table), Q = u2 R + u1 G.  Votes the pre-checks rejected keep
+// their state untouched, as before the split. ----
+__global__ void __launch_bounds__(256, HLC_COMB_WAVES) k_rec_comb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
+                                                  const uint32_t* gcomb, uint8_t* state, const uint32_t* rec,
+                                                  uint32_t* q, const uint8_t* mst, int force_exact) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (pre && pre[i] != PRE_PENDING)) return;
+  const uint8_t m = mst[i];
+  if (m == MST_SKIP) return;
+  if (m != MST_OK && m != MST_INF) {
+    state[i] = m;
+    return;
+  }
+  fe z, u1, qx, qy, qz;
+  bool neg_g;
+  fe_from_digest(z, z_digest + 8 * i);
+  rec_u1(z, rec + i, n, u1, neg_g);
+  load_fe_ws(qx, q + i, n);
+  load_fe_ws(qy, q + (size_t)8 * n + i, n);
+  load_fe_ws(qz, q + (size_t)16 * n + i, n);
+  const int code = rec_comb29(u1, neg_g, m == MST_INF, qx, qy, qz, gcomb, force_exact != 0);
+  state[i] = code != SCHEME_NONE ? (uint8_t)(1 + code) : REC_PENDING;
+  if (code != SCHEME_NONE) return;
+  store_fe_ws(qx, q + i, n);
+  store_fe_ws(qy, q + (size_t)8 * n + i, n);
+  store_fe_ws(qz, q + (size_t)16 * n + i, n);
 }
 
 // ---- final: batched Z^-1 (one safegcd per REC_BATCH votes) and affine Q, then (k_rec_addr, one
@@ -324,7 +352,7 @@ uint64_t recover_scratch_words() { return SCRATCH_WORDS; }
 
 uint64_t recover_work_words(uint64_t n) {
   const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH;
-  return n * (uint64_t)(REC_WORDS + Q_WORDS) + L * REC_BATCH * 8 + 64;
+  return n * (uint64_t)(REC_WORDS + Q_WORDS) + L * REC_BATCH * 8 + (n + 3) / 4 + 64;
 }
 
 uint64_t recover_grid_lanes() {
@@ -339,6 +367,7 @@ uint64_t recover_grid_lanes() {
 namespace {
 struct RecBufs {
   uint32_t *rec, *q, *pfx;
+  uint8_t* mst;
   unsigned long long* ctr;
   uint64_t L;
 };
@@ -348,9 +377,9 @@ RecBufs rec_bufs(uint64_t n, uint32_t* work) {
   b.q = b.rec + n * (uint64_t)REC_WORDS;
   b.pfx = b.q + n * (uint64_t)Q_WORDS;
   b.L = (n + REC_BATCH - 1) / REC_BATCH;
+  b.mst = reinterpret_cast<uint8_t*>(b.pfx + b.L * REC_BATCH * 8);  // n bytes
   // k_rec_main's work counter: 8-byte aligned inside the 64-word tail of recover_work_words(n)
-  b.ctr = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(b.pfx + b.L * REC_BATCH * 8) + 7) &
-                                                ~uintptr_t(7));
+  b.ctr = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(b.mst + n) + 7) & ~uintptr_t(7));
   return b;
 }
 }  // namespace
@@ -364,21 +393,29 @@ void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
                      len_stride, b.rec, b.pfx, b.ctr);
 }
 
-void launch_recover_main(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
-                         const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb,
-                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, uint8_t* verify_out,
-                         uint8_t* addr_out, hipStream_t s, int force_exact) {
+void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
+                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact) {
   if (!n) return;
   const RecBufs b = rec_bufs(n, work);
-  const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (n + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
-  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, pre, z_digest, bytes, sig_off,
-                     off_stride, gcomb, scratch, (uint64_t)blocks * REC_TPB, verify_out, b.rec, b.q, force_exact, b.ctr);
+  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, bytes, sig_off, off_stride, scratch,
+                     (uint64_t)blocks * REC_TPB, b.rec, b.q, b.mst, force_exact, b.ctr);
+}
+
+void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
+                           const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb, uint32_t* work,
+                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact) {
+  if (!n) return;
+  const RecBufs b = rec_bufs(n, work);
+  const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
+  const unsigned vb = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_rec_comb, dim3(vb), dim3(256), 0, s, n, pre, z_digest, gcomb, verify_out, b.rec, b.q, b.mst,
+                     force_exact);
   hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, pre, verify_out, b.q, b.pfx);
-  hipLaunchKernelGGL(k_rec_addr, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, pre, bytes, id_off, off_stride,
-                     verify_out, b.q, addr_out);
+  hipLaunchKernelGGL(k_rec_addr, dim3(vb), dim3(256), 0, s, n, pre, bytes, id_off, off_stride, verify_out, b.q,
+                     addr_out);
 }
 
 void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
@@ -386,8 +423,8 @@ void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, co
                     size_t len_stride, const uint32_t* gcomb, uint32_t* scratch, uint64_t scratch_lanes,
                     uint32_t* work, uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact) {
   launch_recover_prep(n, bytes, sig_off, off_stride, sig_len, len_stride, work, s);
-  launch_recover_main(n, pre, z_digest, bytes, sig_off, id_off, off_stride, gcomb, scratch, scratch_lanes, work,
-                      verify_out, addr_out, s, force_exact);
+  launch_recover_main(n, bytes, sig_off, off_stride, scratch, scratch_lanes, work, s, force_exact);
+  launch_recover_finish(n, pre, z_digest, bytes, id_off, off_stride, gcomb, work, verify_out, addr_out, s, force_exact);
 }
 
 void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s) {

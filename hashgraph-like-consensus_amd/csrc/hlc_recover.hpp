@@ -617,6 +617,93 @@ HLC_DEV int rec_main29(const fe& r32, const fe& u1, bool neg_g, const uint32_t* 
   return SCHEME_NONE;
 }
 
+// The same in two stages, so that the long half needs no prehash: rec_u2r29 (k_rec_main, runs
+// beside the prehash kernels) = R = decompress(r, parity), the R table and the u2 R chain, Jacobian
+// result in 8 x 32 limbs (inf set for the point at infinity); rec_comb29 (k_rec_comb, after the
+// prehash) = the u1 G comb and the one full addition.  Each half re-runs only its own chain checked
+// when its own Z comes out zero (the unchecked chain is exact whenever its Z is non-zero, so this
+// is the combined stage's test split per chain).
+HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz, bool& inf,
+                      uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact) {
+  const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
+  const int parity = (int)((flags >> 5) & 1u);
+  ge29 R;
+  fe29_from32(R.x, r32.v);
+  {
+    fe29 x3, alpha, seven;
+    fe29_sqr(x3, R.x);
+    fe29_mul(x3, x3, R.x);
+    fe29_set(seven, 7);
+    fe29_add(alpha, x3, seven);
+    if (!fe29_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
+    if ((int)(R.y.v[0] & 1u) != parity) fe29_neg(R.y, R.y);
+  }
+  fe29 zg;
+  {
+    gej29 d;
+    gej29_set_ge(d, R);
+    gej29_double(d, d);
+    ge29 dp;
+    dp.x = d.x;
+    dp.y = d.y;
+    fe29 c2, c3;
+    fe29_sqr(c2, d.z);
+    fe29_mul(c3, c2, d.z);
+    ge29 a;
+    fe29_mul(a.x, R.x, c2);
+    fe29_mul(a.y, R.y, c3);
+    store_ge29_tab(a.x, a.y, tab);
+    uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
+    for (int i = 1; i < RTAB_N; ++i) {
+      fe29 zr;
+      gej29_zaddu(a, dp, zr);
+      store_ge29_tab(a.x, a.y, tab + RTAB_ENTRY * i);
+      store_fe29_ws(zr, zrws + (size_t)(9 * (i - 1)) * ws_stride, ws_stride);
+    }
+    fe29 sc;
+    fe29_set(sc, 1);
+    for (int i = RTAB_N - 2; i >= 0; --i) {
+      fe29 zr, s2, s3;
+      load_fe29_ws(zr, zrws + (size_t)(9 * i) * ws_stride, ws_stride);
+      fe29_mul(sc, sc, zr);
+      fe29_sqr(s2, sc);
+      fe29_mul(s3, s2, sc);
+      ge29 e;
+      load_ge29_tab(e, tab + RTAB_ENTRY * i);
+      fe29_mul(e.x, e.x, s2);
+      fe29_mul(e.y, e.y, s3);
+      store_ge29_tab(e.x, e.y, tab + RTAB_ENTRY * i);
+    }
+    fe29_mul(zg, sc, d.z);
+  }
+  gej29 acc;
+  chain_u2r29<false>(acc, rec, stride, tab, zg);
+  if (force_exact || (!acc.inf && fe29_is_zero_modp(acc.z))) chain_u2r29<true>(acc, rec, stride, tab, zg);
+  inf = acc.inf;
+  fe29_to32(qx.v, acc.x);
+  fe29_to32(qy.v, acc.y);
+  fe29_to32(qz.v, acc.z);
+  return SCHEME_NONE;
+}
+
+// second half: Q = (u2 R, from rec_u2r29) + u1 G; Q in 8 x 32 limbs.  SCHEME_NONE or SCHEME_INFINITY.
+HLC_DEV int rec_comb29(const fe& u1, bool neg_g, bool inf, fe& qx, fe& qy, fe& qz, const uint32_t* gcomb,
+                       bool force_exact) {
+  gej29 acc, ag;
+  acc.inf = inf;
+  fe29_from32(acc.x, qx.v);
+  fe29_from32(acc.y, qy.v);
+  fe29_from32(acc.z, qz.v);
+  comb_mul_g29<false>(ag, u1, neg_g, gcomb);
+  if (force_exact || fe29_is_zero_modp(ag.z)) comb_mul_g29<true>(ag, u1, neg_g, gcomb);
+  gej29_add(acc, acc, ag);
+  if (acc.inf) return SCHEME_INFINITY;
+  fe29_to32(qx.v, acc.x);
+  fe29_to32(qy.v, acc.y);
+  fe29_to32(qz.v, acc.z);
+  return SCHEME_NONE;
+}
+
 // Main stage for one vote: R = decompress(r, parity), Q = u1 G + u2 R (Jacobian, not normalised).
 // Returns SCHEME_NONE, SCHEME_NO_POINT or SCHEME_INFINITY.  rec: the vote's record (stride n);
 // gcomb: the fixed-base comb; ws: this lane's interleaved workspace column (stride = lanes);
