@@ -210,8 +210,9 @@ int hlc_abi_version(void);
 
 /* ---- Measurement hooks (bench.py roofline): HIP events on the launch stream ------ */
 /* enable != 0: every validate-many call records hipEvents around the signature-recovery
- * kernels (k_rec_prep + k_rec_main + k_rec_final), around the chain/tally kernels and around the
- * whole call, on the stream the kernels run on. */
+ * kernels (k_rec_prep and k_rec_main on the context's second stream; k_rec_comb, k_rec_final and
+ * k_rec_addr on the launch stream), around the chain/tally kernels and around the whole call, on
+ * the streams the kernels run on. */
 int hlc_ctx_set_kernel_timing(hlc_ctx* ctx, int enable);
 /* Waits for the recorded events, returns the summed device time (ms) and launch count of
  * the recovery and of whole validate-many calls since the previous take, then resets them. */
