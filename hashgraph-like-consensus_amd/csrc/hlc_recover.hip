@@ -13,8 +13,9 @@ namespace {
 #endif
 constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
 #ifndef HLC_REC_WAVES
-#define HLC_REC_WAVES 2  // waves per SIMD the register allocator must admit for k_rec_main: with dynamic work
-                         // hand-out 2 (256 VGPRs, no spills) beats 3 and 4 by 2.5% (profiles/r02_ab_waves_dynamic.txt)
+#define HLC_REC_WAVES 2  // minimum waves per SIMD the register allocator must admit for k_rec_main.  Since
+                         // the u2 R / comb split it takes 166 VGPRs (3 waves, no spills): 3 beats a grid
+                         // capped at 2 by 5-6% and a forced 4 (spills) by 2% (profiles/r02_ab_main_waves_split.txt)
 #endif
 
 // ---- prep: parse + batched r^-1 + scalars (REC_BATCH votes per lane, one safegcd) ----
@@ -361,6 +362,10 @@ uint64_t recover_grid_lanes() {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rec_main, REC_TPB, 0) != hipSuccess || per_cu < 1)
     per_cu = 2;
+#ifdef HLC_REC_GRID_WAVES
+  // A/B variant: a smaller persistent grid than the register budget admits (waves per SIMD)
+  per_cu = std::min(per_cu, HLC_REC_GRID_WAVES * 4 * 64 / REC_TPB);
+#endif
   return (uint64_t)cus * (uint64_t)per_cu * REC_TPB;
 }
 
