@@ -474,13 +474,15 @@ def main() -> int:
 
     def step():
         eng.validate_proposals_device(db, handle)
-        if dist is not None:
-            if backend == "nccl":
-                with torch.cuda.stream(stream):
-                    ex(db.results, db.status, P, db.n)
-            else:
-                torch.cuda.synchronize()
-                ex(db.results.cpu(), db.status.cpu(), P, db.n)
+        if dist is None:  # one GPU: the same outcome counters, on the device, with no exchange
+            with torch.cuda.stream(stream):
+                ex.local_counters(db.results, db.status, P, db.n)
+        elif backend == "nccl":
+            with torch.cuda.stream(stream):
+                ex(db.results, db.status, P, db.n)
+        else:
+            torch.cuda.synchronize()
+            ex(db.results.cpu(), db.status.cpu(), P, db.n)
 
     for _ in range(args.warmup):
         step()
@@ -516,11 +518,7 @@ def main() -> int:
         votes_per_step = int(nt.item())
     else:
         votes_per_step = db.n
-    if dist is None:  # one GPU: no exchange; the same counters, computed once outside the timed steps
-        with torch.cuda.stream(stream):
-            ex.local_counters(db.results, db.status, P, db.n)
-        torch.cuda.synchronize()
-    counters = ex.summary()
+    counters = ex.summary()  # the last timed step's counters (all-reduced over the ranks at N > 1)
     assert counters["verified_votes"] == votes_per_step, "all-reduced verified-vote counter != votes processed"
 
     value = votes_per_step * args.steps / elapsed

@@ -75,6 +75,7 @@ struct hlc_ctx {
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
   int rec_force_exact = 0;  // HLC_REC_FORCE_EXACT=1: every vote through the checked chains (tests)
+  int serial_stages = 0;    // HLC_SERIAL_STAGES=1: prep + main after the prehash on one stream (A/B, clock probes)
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
   DBuf in_off2, in_len2, in_off3, in_len3, in_priv;
@@ -216,45 +217,57 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   // context's aux stream while the prehash kernels (and the small-proposal chain kernel) run on
   // `s`; `s` waits for them before the finish (u1 G with u1 = -z/r from the prehash, Z^-1,
   // address).  Measured recovery time = prep bracket (aux) + main start (aux) .. finish end (s).
-  HIPCHK(hipEventRecord(c->ev_fork, s));
-  HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  // (HLC_SERIAL_STAGES=1: everything on `s`, prep + main after the prehash and the chain kernel --
+  // the measurement of k_rec_main running alone)
+  hipStream_t aux = c->serial_stages ? s : c->aux;
   hipEvent_t p0 = nullptr, p1 = nullptr, r0 = nullptr, r1 = nullptr;
   if (c->timing) {
     p0 = c->take_event();
     p1 = c->take_event();
     r0 = c->take_event();
     r1 = c->take_event();
-    HIPCHK(hipEventRecord(p0, c->aux));
   }
+  auto prehash_and_chain = [&]() -> int {
+    hlc::launch_prehash_fused(dv, n, vote_prop, dprops, c->kec_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
+                              c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
+    hlc::launch_prehash_stream(dv, n, vote_prop, dprops, c->flag.as<uint32_t>(), c->kec_dig.as<uint32_t>(),
+                               c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
+    if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
+    if (chain_code) {
+      hipEvent_t cs0 = nullptr, cs1 = nullptr;
+      if (c->timing) {
+        cs0 = c->take_event();
+        cs1 = c->take_event();
+        HIPCHK(hipEventRecord(cs0, s));
+      }
+      hlc::launch_chain_small(dv, dprops, np, chain_code, red, s);
+      if (c->timing) {
+        HIPCHK(hipEventRecord(cs1, s));
+        c->chain_aux_ev.emplace_back(cs0, cs1);
+      }
+    }
+    return 0;
+  };
+  if (c->serial_stages) CHK(prehash_and_chain());
+  else {
+    HIPCHK(hipEventRecord(c->ev_fork, s));
+    HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
+  }
+  if (c->timing) HIPCHK(hipEventRecord(p0, aux));
   hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
-                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), c->aux);
+                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux);
   if (c->timing) {
-    HIPCHK(hipEventRecord(p1, c->aux));
+    HIPCHK(hipEventRecord(p1, aux));
     c->rec_prep_ev.emplace_back(p0, p1);
-    HIPCHK(hipEventRecord(r0, c->aux));
+    HIPCHK(hipEventRecord(r0, aux));
   }
   hlc::launch_recover_main(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, c->rec_scratch.as<uint32_t>(),
-                           c->rec_lanes, c->rec_work.as<uint32_t>(), c->aux, c->rec_force_exact);
-  HIPCHK(hipEventRecord(c->ev_join, c->aux));
-  hlc::launch_prehash_fused(dv, n, vote_prop, dprops, c->kec_dig.as<uint32_t>(), c->pre.as<uint8_t>(),
-                            c->pre_reason.as<uint8_t>(), c->flag.as<uint32_t>(), s);
-  hlc::launch_prehash_stream(dv, n, vote_prop, dprops, c->flag.as<uint32_t>(), c->kec_dig.as<uint32_t>(),
-                             c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
-  if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
-  if (chain_code) {
-    hipEvent_t cs0 = nullptr, cs1 = nullptr;
-    if (c->timing) {
-      cs0 = c->take_event();
-      cs1 = c->take_event();
-      HIPCHK(hipEventRecord(cs0, s));
-    }
-    hlc::launch_chain_small(dv, dprops, np, chain_code, red, s);
-    if (c->timing) {
-      HIPCHK(hipEventRecord(cs1, s));
-      c->chain_aux_ev.emplace_back(cs0, cs1);
-    }
+                           c->rec_lanes, c->rec_work.as<uint32_t>(), aux, c->rec_force_exact);
+  if (!c->serial_stages) {
+    HIPCHK(hipEventRecord(c->ev_join, aux));
+    CHK(prehash_and_chain());
+    HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
   }
-  HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_OWNER,
                              HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
                              drec, s, c->rec_force_exact);
@@ -536,6 +549,7 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
   hlc_ctx* c = new hlc_ctx();
   c->device = device;
   if (const char* fx = std::getenv("HLC_REC_FORCE_EXACT")) c->rec_force_exact = std::atoi(fx) != 0;
+  if (const char* ss = std::getenv("HLC_SERIAL_STAGES")) c->serial_stages = std::atoi(ss) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -545,17 +559,24 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
     delete c;
     return set_err(HLC_EDEVICE, "stream creation failed");
   }
-  // fixed-base tables: the signing comb (32 x 256 points) and the recovery's u1 G comb
-  // (16 x 32768 points, 32 MiB), built once per context
+  // fixed-base tables, built once per context: the signing comb (32 x 256 points, 512 KiB) and the
+  // recovery's u1 G comb (12 windows x 2^21 affine points of 64 B = 1.5 GiB of HBM, hlc.h)
   if (c->fbtab.ensure(hlc::FBTAB_WORDS * sizeof(uint32_t)) != 0 ||
       c->gtab.ensure(hlc::gcomb_words() * sizeof(uint32_t)) != 0) {
-    delete c;
-    return HLC_ENOMEM;
+    const std::string why = g_err;
+    hipStream_t st = c->stream, ax = c->aux;
+    delete c;  // frees whichever table was allocated and the events
+    (void)hipStreamDestroy(st);
+    (void)hipStreamDestroy(ax);
+    return set_err(HLC_ENOMEM, "fixed-base table allocation (1.5 GiB u1 G comb) failed: " + why);
   }
   hlc::launch_build_fbtab(c->fbtab.as<uint32_t>(), c->stream);
   hlc::launch_build_gcomb(c->gtab.as<uint32_t>(), c->fbtab.as<uint32_t>(), c->stream);
   if (hipStreamSynchronize(c->stream) != hipSuccess) {
+    hipStream_t st = c->stream, ax = c->aux;
     delete c;
+    (void)hipStreamDestroy(st);
+    (void)hipStreamDestroy(ax);
     return set_err(HLC_EDEVICE, "generator table construction failed");
   }
   *out = c;

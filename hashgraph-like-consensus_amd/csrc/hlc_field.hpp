@@ -30,14 +30,6 @@ struct fe {
 // ------------------------------------------------------------------------------------
 // constants
 // ------------------------------------------------------------------------------------
-__constant__ static const uint32_t P_LIMBS[8] = {0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu,
-                                                  0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-__constant__ static const uint32_t N_LIMBS[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
-                                                  0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-
-HLC_DEV uint32_t p_limb(int i) {
-  return i == 0 ? 0xFFFFFC2Fu : (i == 1 ? 0xFFFFFFFEu : 0xFFFFFFFFu);
-}
 HLC_DEV uint32_t n_limb(int i) {
   const uint32_t n0 = 0xD0364141u, n1 = 0xBFD25E8Cu, n2 = 0xAF48A03Bu, n3 = 0xBAAEDCE6u,
                  n4 = 0xFFFFFFFEu;
@@ -53,19 +45,6 @@ HLC_DEV uint32_t nhalf_limb(int i) {
 // ------------------------------------------------------------------------------------
 // limb primitives
 // ------------------------------------------------------------------------------------
-// acc(64) += a*b with the 65th bit carried into hi (v_mad_u64_u32 carry-out + v_addc).
-HLC_DEV void mac(uint64_t& acc, uint32_t& hi, uint32_t a, uint32_t b) {
-  uint64_t c;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(c) : "v"(a), "v"(b));
-  asm("v_addc_co_u32_e64 %0, %1, 0, %0, %1" : "+v"(hi), "+s"(c));
-}
-
-// acc(64) += 2*a*b (for squaring off-diagonals): two MACs
-HLC_DEV void mac2(uint64_t& acc, uint32_t& hi, uint32_t a, uint32_t b) {
-  mac(acc, hi, a, b);
-  mac(acc, hi, a, b);
-}
-
 HLC_DEV uint32_t add_cc(uint32_t a, uint32_t b, uint32_t& carry) {
   uint64_t s = (uint64_t)a + b + carry;
   carry = (uint32_t)(s >> 32);
@@ -81,12 +60,6 @@ HLC_DEV bool fe_is_zero(const fe& a) {
   uint32_t x = a.v[0];
 #pragma unroll
   for (int i = 1; i < 8; ++i) x |= a.v[i];
-  return x == 0;
-}
-HLC_DEV bool fe_eq(const fe& a, const fe& b) {
-  uint32_t x = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) x |= a.v[i] ^ b.v[i];
   return x == 0;
 }
 HLC_DEV void fe_set(fe& r, uint32_t x) {
@@ -403,11 +376,6 @@ HLC_DEV void sc_add(fe& r, const fe& a, const fe& b) {
   for (int i = 0; i < 8; ++i) r.v[i] = use_d ? d[i] : s[i];
 }
 
-HLC_DEV void sc_load_const(fe& r, const uint32_t* c) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = c[i];
-}
-
 // R^2 mod n, for conversion into the Montgomery domain
 HLC_DEV void sc_r2(fe& r) {
   const uint32_t k[8] = {0x67D7D140u, 0x896CF214u, 0x0E7CF878u, 0x741496C2u,
@@ -418,20 +386,5 @@ HLC_DEV void sc_r2(fe& r) {
 
 // r = a^-1 mod n (a in [1, n)): safegcd divsteps
 HLC_DEV void sc_inv(fe& r, const fe& a) { modinv_safegcd(r.v, a.v, modinfo_n()); }
-
-// r = a*b mod n (plain domain) = mont(mont(a, b), R^2)
-HLC_DEV void sc_mul(fe& r, const fe& a, const fe& b) {
-  fe t, r2;
-  sc_mont_mul(t, a, b);
-  sc_r2(r2);
-  sc_mont_mul(r, t, r2);
-}
-
-// big-endian 32 bytes <-> limbs
-HLC_DEV void fe_from_be_words(fe& r, const uint32_t w_be[8]) {
-  // w_be[0] holds bytes 0..3 (most significant) already as a big-endian-decoded u32
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r.v[i] = w_be[7 - i];
-}
 
 }  // namespace hlc

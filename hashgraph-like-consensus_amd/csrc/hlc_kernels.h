@@ -103,7 +103,8 @@ void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
 void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status, hipStream_t s);
 // proposals with <= 512 votes: chain / duplicate / YES count in LDS, one wave per proposal
 // (writes chain_code and red[4p+1..3] for those; the global-table kernels skip them).  Needs no vote
-// statuses: validate_device runs it on the aux stream beside the recovery, after launch_red_init.
+// statuses: vote_stage enqueues it on the launch stream after the prehash kernels, beside k_rec_main
+// (which runs on the context's second stream), after launch_red_init.
 void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint8_t* chain_code,
                         uint32_t* red, hipStream_t s);
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,

@@ -70,7 +70,7 @@ HLC_HD void gej29_double(gej29& r, const gej29& a) {
 // EXACT = true handles the exceptional cases (a == b: doubling; a == -b: infinity) here.
 // EXACT = false (the hot chains) does NOT test for them: H == 0 gives Z3 == 0, every later Z
 // stays 0 (each step multiplies Z), and the caller tests the chain's final Z once per vote and
-// recomputes the vote with EXACT = true (rec_main29) -- bit-identical results either way.
+// recomputes the vote with EXACT = true (rec_u2r29 / rec_comb29) -- bit-identical results either way.
 template <bool EXACT>
 HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullptr) {
   if (a.inf) {

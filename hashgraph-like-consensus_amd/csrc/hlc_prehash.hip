@@ -387,14 +387,14 @@ __device__ uint32_t table_insert(uint32_t* tab, uint32_t mask, const hlc_votes& 
 
 __global__ void k_tables(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                          uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, const uint32_t* flags) {
-  if (!(*flags & FLAG_LARGE_PROPOSAL)) return;  // every proposal is small: k_chain_small
+  if (flags && !(*flags & FLAG_LARGE_PROPOSAL)) return;  // every proposal is small: k_chain_small
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t p = vote_prop[i];
   if (p == NO_PROP || props[p].vote_count <= SMALL_CAP) return;  // small: k_chain_small
   // HashMap<vote_hash, (owner, ts, idx)>: last index wins (utils.rs:180-183); built only when a
   // large proposal's vote has a parent_hash to look up
-  if (props[p].vote_count > 1 && (*flags & FLAG_LARGE_PARENTS))
+  if (props[p].vote_count > 1 && (!flags || (*flags & FLAG_LARGE_PARENTS)))
     (void)table_insert<true>(chain_tab, mask, v, vote_prop, (uint32_t)i, HLC_F_VOTE_HASH);
   // seen_owners HashSet (session.rs:270-275): the DuplicateVote error sits at the first index whose
   // owner appeared earlier = the smallest second-smallest index over the owner groups.  Every insert
@@ -1026,7 +1026,7 @@ __global__ void k_red_init(uint32_t* red, uint64_t np) {
 
 // clears a table when the device flag word has `bit` set (the large-proposal chain tables)
 __global__ void k_clear_if(const uint32_t* flags, uint32_t bit, uint32_t* tab, uint64_t words) {
-  if (!(*flags & bit)) return;
+  if (flags && !(*flags & bit)) return;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += stride) tab[k] = EMPTY_SLOT;
 }
@@ -1147,7 +1147,9 @@ void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_
                            const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason,
                            hipStream_t s) {
   if (!n) return;
-  const unsigned blocks = (unsigned)std::min<uint64_t>(blocks_for(n), 1024);
+  // one block per CU at most: the grid exits at once unless k_prehash_fused deferred a vote (rare),
+  // and a small grid keeps the queued no-op from occupying the dispatcher behind k_rec_main
+  const unsigned blocks = (unsigned)std::min<uint64_t>(blocks_for(n), 256);
   hipLaunchKernelGGL(k_prehash_stream, dim3(blocks), dim3(TPB), 0, s, *v, n, vote_prop, props, flags, kec_dig, pre,
                      pre_reason);
 }

@@ -12,10 +12,13 @@ namespace {
 #define HLC_REC_TPB 256
 #endif
 constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
-#ifndef HLC_REC_WAVES
-#define HLC_REC_WAVES 2  // minimum waves per SIMD the register allocator must admit for k_rec_main.  Since
-                         // the u2 R / comb split it takes 166 VGPRs (3 waves, no spills): 3 beats a grid
-                         // capped at 2 by 5-6% and a forced 4 (spills) by 2% (profiles/r02_ab_main_waves_split.txt)
+#ifndef HLC_REC_MIN_WAVES
+// __launch_bounds__ minimum waves per SIMD for k_rec_main: a floor for the register allocator, not
+// the occupancy it reaches.  With 2 the kernel takes 166 VGPRs and so RUNS at 3 waves per SIMD (no
+// spills); 3 beats a grid capped at 2 by 5-6% and a forced 4 (spills) by 2%
+// (profiles/r02_ab_main_waves_split.txt).  The grid is sized from the occupancy API
+// (recover_grid_lanes), so it follows whatever the build reaches.
+#define HLC_REC_MIN_WAVES 2
 #endif
 
 // ---- prep: parse + batched r^-1 + scalars (REC_BATCH votes per lane, one safegcd) ----
@@ -94,14 +97,21 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
 // the 3 resident waves finishes its share long before the youngest, which then runs alone at
 // lone-wave efficiency (measured with HLC_CLOCK_PROBE: 4-vote blocks done at 3.5 ms, the last
 // 3-vote blocks at 7.0 ms of one launch); grabbing keeps every wave busy until the work runs out.
-__global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n, const uint8_t* bytes,
+__global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_t n, const uint8_t* bytes,
                                                                      const uint64_t* sig_off, size_t off_stride,
                                                                      uint32_t* scratch, uint64_t lanes,
                                                                      const uint32_t* rec, uint32_t* q, uint8_t* mst,
                                                                      int force_exact, unsigned long long* ctr) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t* ws = scratch + tid;
-  uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tid * RTAB_WORDS;
+#ifdef HLC_PROBE_WAVE_TABLE
+  // timing probe only (wrong results): every lane of a wave builds and gathers ONE shared R table
+  // and z-ratio column (its wave's lane 0's), so the table traffic stays in L1/L2 (1.8 KB per wave)
+  const uint64_t tws = tid & ~(uint64_t)63;
+#else
+  const uint64_t tws = tid;
+#endif
+  uint32_t* ws = scratch + tws;
+  uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tws * RTAB_WORDS;
 #ifdef HLC_CLOCK_PROBE
   // A/B probe (make variant NAME=clk DEFS=-DHLC_CLOCK_PROBE): the shader clock a wave sees under
   // the real kernel = core-clock ticks (clock64) over constant 100 MHz ticks (wall_clock64)
@@ -151,13 +161,13 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_WAVES) k_rec_main(uint64_t n,
 #endif
 }
 
-#ifndef HLC_COMB_WAVES
-#define HLC_COMB_WAVES 2  // 200 VGPRs, no spills (3 and 4 waves spill 124 / 284 B per lane)
+#ifndef HLC_COMB_MIN_WAVES
+#define HLC_COMB_MIN_WAVES 2  // launch-bounds floor; 200 VGPRs, runs at 2 waves, no spills (3 and 4 spill 124 / 284 B per lane)
 #endif
 // ---- comb: after the prehash, one lane per vote at full occupancy: u1 = -z / r, u1 G by the comb
 // (12 mixed additions from the HBM table), Q = u2 R + u1 G.  Votes the pre-checks rejected keep
 // their state untouched, as before the split. ----
-__global__ void __launch_bounds__(256, HLC_COMB_WAVES) k_rec_comb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
+__global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_comb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
                                                   const uint32_t* gcomb, uint8_t* state, const uint32_t* rec,
                                                   uint32_t* q, const uint8_t* mst, int force_exact) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -1,5 +1,5 @@
-// hlc_recover.hpp -- secp256k1 public-key recovery (ecrecover) for a batch of votes, in three
-// stages (hlc_recover.hip: k_rec_prep, k_rec_main, k_rec_final).
+// hlc_recover.hpp -- secp256k1 public-key recovery (ecrecover) for a batch of votes, in five
+// kernels (hlc_recover.hip: k_rec_prep, k_rec_main, k_rec_comb, k_rec_final, k_rec_addr).
 //
 // Restates, bit-exactly, `Signature::from_raw_array(sig)?.recover_address_from_msg(payload)`
 // of alloy-primitives 1.6.0 on top of k256 0.13.4 `VerifyingKey::recover_from_prehash`
@@ -10,26 +10,27 @@
 // k256's post-recovery verify_prehash always succeeds on a recovered key (it re-derives R)
 // and is therefore not repeated.
 //
-// Stages (one lane per vote in the main stage; REC_BATCH votes per lane in the other two):
+// Stages (one lane per vote in main / comb / addr; REC_BATCH votes per lane in prep / final):
 //   prep : v / s / range checks, then r^-1 mod n for REC_BATCH votes with ONE inversion
-//          (Montgomery's trick: prefix products forward, one safegcd, a backward sweep), u1, u2,
+//          (Montgomery's trick: prefix products forward, one safegcd, a backward sweep), u2 = s/r,
 //          the GLV split of u2 and its regular signed digits -> a per-vote record in HBM;
-//   main : R = decompress(r) (square root), the R table, the u2 R chain, the u1 G comb and the
-//          final addition -> Jacobian Q in HBM (the VALU-bound bulk, ~97% of the work);
-//   final: Z^-1 mod p for REC_BATCH votes with one inversion (the same trick), affine Q,
-//          keccak address, owner compare.
+//   main : R = decompress(r) (square root), the R table, the u2 R chain -> Jacobian u2 R in HBM
+//          (the VALU-bound bulk, ~90% of the work; needs no prehash, so it runs beside it);
+//   comb : u1 = -z/r, the u1 G comb and the final addition Q = u2 R + u1 G;
+//   final: Z^-1 mod p for REC_BATCH votes with one inversion (the same trick), affine Q;
+//   addr : keccak address, owner compare.
 // In SIMT a per-lane inversion already costs the wave ONE instruction stream for 64 values, so
 // a cross-lane (DPP / ds_swizzle) prefix-product scan only adds multiplications and saves no issue
 // slots; the inversion count per wave only drops when each lane folds several of its own values
 // into one inversion -- which is what the batch does (measured in DESIGN.md §4.1).
 //
-// Scalar multiplication Q = u1 G + u2 R (main stage), in two independent parts:
+// Scalar multiplication Q = u1 G + u2 R, in two independent parts:
 //   u2 R: GLV endomorphism (lambda, beta) splits u2 into 128-bit halves b1 + b2 lambda; one
 //       doubling chain of 125 steps adds, every 5 bits, one odd multiple of R and one of
 //       lambda R ("regular" signed digits: every lane adds at the same positions).  The 16
 //       odd multiples 1..31 R live per lane in a lane-contiguous HBM/L2 workspace.  The R
-//       table is built on the isomorphic curve y^2 = x^3 + 7 C^6 (C = Z(2R)) and brought to one
-//       common Z ("effective affine", as libsecp256k1's ecmult_odd_multiples_table +
+//       table is built on the isomorphic curve y^2 = x^3 + 7 C^6 (C = Z(2R)) by co-Z additions
+//       and brought to one common Z ("effective affine", as libsecp256k1's
 //       ge_table_set_globalz), so every chain addition is one mixed Jacobian+affine add.
 //   u1 G: a fixed-base comb with NO doublings over a table resident in HBM: GC_WINDOWS windows of
 //       GC_W bits (12 x 22), T[w][j] = (2j+1) 2^(W w) G (affine), regular signed digits of the odd
@@ -238,43 +239,6 @@ HLC_DEV const uint32_t* comb_entry(const uint32_t* gcomb, int w, int d) {
   return gcomb + ((size_t)w * GC_ENTRIES + (size_t)idx) * 16;
 }
 
-// acc = k G for odd k < 2^256 (neg: acc = -k G), by the comb: 2^256 G + sum_w d_w 2^(16 w) G.
-HLC_DEV void comb_mul_g(gej& acc, fe k, bool neg, const uint32_t* gcomb) {
-  ge e;
-  load_ge_global(e, gcomb + GC_TOP_OFF);
-  if (neg) fe_neg(e.y, e.y);
-  gej_set_ge(acc, e);
-  int d = comb_digit(k);
-  load_ge_global(e, comb_entry(gcomb, 0, d));
-#pragma unroll 1
-  for (int w = 0; w < GC_WINDOWS; ++w) {
-    ge cur = e;
-    const int dc = d;
-    if (w + 1 < GC_WINDOWS) {  // prefetch the next window's entry
-      d = comb_digit(k);
-      load_ge_global(e, comb_entry(gcomb, w + 1, d));
-    }
-    if ((dc < 0) != neg) fe_neg(cur.y, cur.y);
-    gej_add_ge(acc, acc, cur);
-  }
-}
-
-HLC_DEV void store_ge_ws(const fe& x, const fe& y, uint32_t* ws, size_t stride) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    ws[(size_t)i * stride] = x.v[i];
-    ws[(size_t)(8 + i) * stride] = y.v[i];
-  }
-}
-
-HLC_DEV void store_ge_tab(const fe& x, const fe& y, uint32_t* t) {
-  uint4* p = reinterpret_cast<uint4*>(t);
-  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-  p[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-  p[2] = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
-  p[3] = make_uint4(y.v[4], y.v[5], y.v[6], y.v[7]);
-}
-
 HLC_DEV void store_fe_ws(const fe& x, uint32_t* ws, size_t stride) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) ws[(size_t)i * stride] = x.v[i];
@@ -283,47 +247,6 @@ HLC_DEV void store_fe_ws(const fe& x, uint32_t* ws, size_t stride) {
 HLC_DEV void load_fe_ws(fe& x, const uint32_t* ws, size_t stride) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) x.v[i] = ws[(size_t)i * stride];
-}
-
-// a += b (b affine, a finite, a != +-b: used only for the R-table build where (2i-1)R and 2R
-// are distinct, non-opposite multiples of a point of prime order n); zr = Z(a') / Z(a) = 2H.
-HLC_DEV void gej_madd_zr(gej& a, const ge& b, fe& zr) {
-  fe z1z1, u2, s2, h, hh, i4, j, rr, v, t;
-  fe_sqr(z1z1, a.z);
-  fe_mul(u2, b.x, z1z1);
-  fe_mul(s2, b.y, a.z);
-  fe_mul(s2, s2, z1z1);
-  fe_sub(h, u2, a.x);
-  fe_sub(rr, s2, a.y);
-  fe_sqr(hh, h);
-  fe_dbl(i4, hh);
-  fe_dbl(i4, i4);
-  fe_mul(j, h, i4);
-  fe_dbl(rr, rr);
-  fe_mul(v, a.x, i4);
-  fe_dbl(zr, h);
-  fe_mul(a.z, a.z, zr);
-  fe x3;
-  fe_sqr(x3, rr);
-  fe_sub(x3, x3, j);
-  fe_dbl(t, v);
-  fe_sub(x3, x3, t);
-  fe_sub(t, v, x3);
-  fe y3;
-  fe_mul(y3, rr, t);
-  fe_mul(t, a.y, j);
-  fe_dbl(t, t);
-  fe_sub(a.y, y3, t);
-  a.x = x3;
-  a.inf = 0;
-}
-
-HLC_DEV void load_ge_ws(ge& p, const uint32_t* ws, size_t stride) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    p.x.v[i] = ws[(size_t)i * stride];
-    p.y.v[i] = ws[(size_t)(8 + i) * stride];
-  }
 }
 
 // Recovered address as 5 big-endian u32 words (bytes 12..31 of the keccak of X||Y).
@@ -446,7 +369,8 @@ HLC_DEV void load_ge_global29(ge29& g, const uint32_t* t) {
   fe29_from32(g.y, e.y.v);
 }
 
-// acc = k G for odd k < 2^256 (neg: acc = -k G), by the comb (see comb_mul_g), in 29-bit limbs.
+// acc = k G for odd k < 2^256 (neg: acc = -k G) by the comb, 2^(W windows) G + sum_w d_w 2^(W w) G,
+// in 29-bit limbs.
 // EXACT: see gej29_madd (the fast form leaves exceptional steps to the caller's final-Z test).
 template <bool EXACT>
 HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
@@ -534,89 +458,6 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
   if (!acc.inf) fe29_mul(acc.z, acc.z, zg);
 }
 
-// Main stage for one vote, over the 29-bit unsaturated field layer (hlc_fe29.hpp: ~24% fewer
-// issue cycles per multiplication than the saturated 8 x 32 layer, profiles/r02_ubench_field29.txt).
-// R = decompress(r, parity), Q = u1 G + u2 R, Q returned in 8 x 32 canonical limbs (x, y, z) for
-// the final stage.  Returns SCHEME_NONE, SCHEME_NO_POINT or SCHEME_INFINITY.
-// The two chains run with the unchecked addition (gej29_madd<false>); an exceptional step (an
-// accumulator equal to +- the added point: never for honest signatures, constructible for crafted
-// ones) leaves a zero Z behind, so one test of both final Z values per vote routes such a vote
-// through the same chains with every step checked.  (With the shipped 22-bit comb no such
-// collision exists at all: see DESIGN.md §4.1.  The test stays as the guard.)
-HLC_DEV int rec_main29(const fe& r32, const fe& u1, bool neg_g, const uint32_t* rec, size_t stride, fe& qx, fe& qy,
-                       fe& qz, const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact) {
-  const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
-  const int parity = (int)((flags >> 5) & 1u);
-  ge29 R;
-  fe29_from32(R.x, r32.v);
-  {
-    fe29 x3, alpha, seven;
-    fe29_sqr(x3, R.x);
-    fe29_mul(x3, x3, R.x);
-    fe29_set(seven, 7);
-    fe29_add(alpha, x3, seven);
-    if (!fe29_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
-    if ((int)(R.y.v[0] & 1u) != parity) fe29_neg(R.y, R.y);
-  }
-  fe29 zg;
-  {
-    gej29 d;
-    gej29_set_ge(d, R);
-    gej29_double(d, d);  // 2R = (X, Y, C); on the iso curve it is the affine point (X, Y)
-    ge29 dp;
-    dp.x = d.x;
-    dp.y = d.y;
-    fe29 c2, c3;
-    fe29_sqr(c2, d.z);
-    fe29_mul(c3, c2, d.z);
-    ge29 a;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve (co-Z with dp: Z = 1)
-    fe29_mul(a.x, R.x, c2);
-    fe29_mul(a.y, R.y, c3);
-    store_ge29_tab(a.x, a.y, tab);
-    uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
-    // (2i+1) R = (2i-1) R + 2R by co-Z additions (gej29_zaddu: 4M + 2S, 2R rescaled alongside);
-    // entry i lives in frame Z_i = prod_{j <= i} zr_j.
-    for (int i = 1; i < RTAB_N; ++i) {
-      fe29 zr;
-      gej29_zaddu(a, dp, zr);
-      store_ge29_tab(a.x, a.y, tab + RTAB_ENTRY * i);
-      store_fe29_ws(zr, zrws + (size_t)(9 * (i - 1)) * ws_stride, ws_stride);
-    }
-    // every entry into the last frame (libsecp256k1's ge_table_set_globalz): entry i times
-    // (prod_{j > i} zr_j)^(2, 3); sc ends as prod of all zr = the common Z relative to the iso frame
-    fe29 sc;
-    fe29_set(sc, 1);
-    for (int i = RTAB_N - 2; i >= 0; --i) {
-      fe29 zr, s2, s3;
-      load_fe29_ws(zr, zrws + (size_t)(9 * i) * ws_stride, ws_stride);
-      fe29_mul(sc, sc, zr);
-      fe29_sqr(s2, sc);
-      fe29_mul(s3, s2, sc);
-      ge29 e;
-      load_ge29_tab(e, tab + RTAB_ENTRY * i);
-      fe29_mul(e.x, e.x, s2);
-      fe29_mul(e.y, e.y, s3);
-      store_ge29_tab(e.x, e.y, tab + RTAB_ENTRY * i);
-    }
-    fe29_mul(zg, sc, d.z);
-  }
-  gej29 acc, ag;
-  chain_u2r29<false>(acc, rec, stride, tab, zg);
-  comb_mul_g29<false>(ag, u1, neg_g, gcomb);
-  // force_exact (HLC_REC_FORCE_EXACT=1 at context creation): every vote takes the checked
-  // chains -- the GPU tests compare that path with the oracle too
-  if (force_exact || (!acc.inf && fe29_is_zero_modp(acc.z)) || fe29_is_zero_modp(ag.z)) {
-    chain_u2r29<true>(acc, rec, stride, tab, zg);
-    comb_mul_g29<true>(ag, u1, neg_g, gcomb);
-  }
-  gej29_add(acc, acc, ag);
-  if (acc.inf) return SCHEME_INFINITY;
-  fe29_to32(qx.v, acc.x);
-  fe29_to32(qy.v, acc.y);
-  fe29_to32(qz.v, acc.z);
-  return SCHEME_NONE;
-}
-
 // The same in two stages, so that the long half needs no prehash: rec_u2r29 (k_rec_main, runs
 // beside the prehash kernels) = R = decompress(r, parity), the R table and the u2 R chain, Jacobian
 // result in 8 x 32 limbs (inf set for the point at infinity); rec_comb29 (k_rec_comb, after the
@@ -702,117 +543,6 @@ HLC_DEV int rec_comb29(const fe& u1, bool neg_g, bool inf, fe& qx, fe& qy, fe& q
   fe29_to32(qy.v, acc.y);
   fe29_to32(qz.v, acc.z);
   return SCHEME_NONE;
-}
-
-// Main stage for one vote: R = decompress(r, parity), Q = u1 G + u2 R (Jacobian, not normalised).
-// Returns SCHEME_NONE, SCHEME_NO_POINT or SCHEME_INFINITY.  rec: the vote's record (stride n);
-// gcomb: the fixed-base comb; ws: this lane's interleaved workspace column (stride = lanes);
-// tab: this lane's R table.
-HLC_DEV int rec_main(const fe& r, const fe& u1, bool neg_g, const uint32_t* rec, size_t stride, gej& acc,
-                     const uint32_t* gcomb, uint32_t* ws, size_t ws_stride, uint32_t* tab) {
-  const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
-  const int parity = (int)((flags >> 5) & 1u);
-  // R = decompress(r, parity): y^2 = x^3 + 7 (x = r < n < p)
-  ge R;
-  R.x = r;
-  {
-    fe x3, alpha, seven;
-    fe_sqr(x3, r);
-    fe_mul(x3, x3, r);
-    fe_set(seven, 7);
-    fe_add(alpha, x3, seven);
-    if (!fe_sqrt(R.y, alpha)) return SCHEME_NO_POINT;
-    if ((int)(R.y.v[0] & 1u) != parity) fe_neg(R.y, R.y);
-  }
-  const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
-  // R table on the isomorphic curve with C = Z(2R): entries (2i+1)R, i < 16, common Z
-  fe zg;  // real Z of the table frame
-  {
-    gej d;
-    gej_set_ge(d, R);
-    gej_double(d, d);  // 2R = (X, Y, C); on the iso curve it is the affine point (X, Y)
-    ge dp;
-    dp.x = d.x;
-    dp.y = d.y;
-    fe c2, c3;
-    fe_sqr(c2, d.z);
-    fe_mul(c3, c2, d.z);
-    gej a;  // phi(R) = (Rx C^2, Ry C^3), affine on the iso curve
-    fe_mul(a.x, R.x, c2);
-    fe_mul(a.y, R.y, c3);
-    fe_set(a.z, 1);
-    store_ge_tab(a.x, a.y, tab);
-    uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
-    for (int i = 1; i < RTAB_N; ++i) {
-      fe zr;
-      gej_madd_zr(a, dp, zr);  // (2i+1)R, Z_i = Z_{i-1} * zr
-      store_ge_tab(a.x, a.y, tab + 16 * i);
-      store_fe_ws(zr, zrws + (size_t)(8 * (i - 1)) * ws_stride, ws_stride);
-    }
-    // common Z = Z_15: entry i scaled by s_i = Z_15 / Z_i = prod_{k > i} zr_k
-    fe sc;
-    fe_set(sc, 1);
-    for (int i = RTAB_N - 2; i >= 0; --i) {
-      fe zr, s2, s3;
-      load_fe_ws(zr, zrws + (size_t)(8 * i) * ws_stride, ws_stride);  // zr_{i+1}
-      fe_mul(sc, sc, zr);
-      fe_sqr(s2, sc);
-      fe_mul(s3, s2, sc);
-      ge e;
-      load_ge_global(e, tab + 16 * i);
-      fe_mul(e.x, e.x, s2);
-      fe_mul(e.y, e.y, s3);
-      store_ge_tab(e.x, e.y, tab + 16 * i);
-    }
-    fe_mul(zg, a.z, d.z);  // real Z of the frame: Z_15 * C
-  }
-  fe beta;
-  fe_beta(beta);
-  const uint32_t* dws = rec + (size_t)REC_DIG * stride;
-  gej_set_inf(acc);
-  // Additions in order (window 25, b1), (25, b2), 5 doublings, (24, b1), ... -- the two halves
-  // add at the same positions (uniform across the wave).  The next addition's table entry is
-  // loaded before the current one is added, so its latency hides behind >= 1 addition.
-  auto digit_at = [&](int step) {
-    const int win = M_R - 1 - (step >> 1), k = step & 1;
-    return digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
-  };
-  auto entry_of = [&](int d) { return tab + 16 * (((d < 0 ? -d : d) - 1) >> 1); };
-  int d_next = digit_at(0);
-  ge g_next;
-  load_ge_global(g_next, entry_of(d_next));
-#pragma unroll 1
-  for (int step = 0; step < 2 * M_R; ++step) {
-    const int k = step & 1;
-    if (k == 0 && step != 0) {
-#pragma unroll 1
-      for (int q = 0; q < W_R; ++q) gej_double(acc, acc);
-    }
-    ge g = g_next;
-    const int d = d_next;
-    if (step + 1 < 2 * M_R) {
-      d_next = digit_at(step + 1);
-      load_ge_global(g_next, entry_of(d_next));
-    }
-    if (k == 1) fe_mul(g.x, g.x, beta);
-    if ((d < 0) != (((negs >> k) & 1) != 0)) fe_neg(g.y, g.y);
-    gej_add_ge(acc, acc, g);
-  }
-  // skew corrections: the digits encoded |b| + 1 for even |b|; subtract one (signed) base point
-#pragma unroll 1
-  for (int k = 0; k < 2; ++k) {
-    if (((skews >> k) & 1) == 0) continue;
-    ge g;
-    load_ge_global(g, tab);
-    if (k == 1) fe_mul(g.x, g.x, beta);
-    if (((negs >> k) & 1) == 0) fe_neg(g.y, g.y);  // add -(sign * P)
-    gej_add_ge(acc, acc, g);
-  }
-  if (!acc.inf) fe_mul(acc.z, acc.z, zg);  // u2 R back on the real curve
-  gej ag;
-  comb_mul_g(ag, u1, neg_g, gcomb);
-  gej_add(acc, acc, ag);
-  return acc.inf ? SCHEME_INFINITY : SCHEME_NONE;
 }
 
 }  // namespace hlc

@@ -101,10 +101,16 @@ class ShardExchange:
         self.counters = torch.zeros(2 * N_CODES, dtype=torch.int64, device=device)
 
     def local_counters(self, results_u8, status_u8, n_props: int, n_votes: int) -> None:
+        """Fixed-width histograms by scatter_add_ into the counter tensor: no host read-back (a
+        torch.bincount reads max/min back and synchronises the host every step).  Every HLC_* code
+        is < N_CODES; a larger byte would be counted in the last bin."""
         t = self.torch
-        self.counters[:N_CODES] = t.bincount(status_u8[:n_votes], minlength=N_CODES)[:N_CODES]
-        self.counters[N_CODES:] = t.bincount(results_u8[: n_props * 16].view(-1, 16)[:, 0],
-                                             minlength=N_CODES)[:N_CODES]
+        c = self.counters
+        c.zero_()
+        sv = status_u8[:n_votes].long().clamp_(max=N_CODES - 1)
+        c[:N_CODES].scatter_add_(0, sv, t.ones_like(sv))
+        pv = results_u8[: n_props * 16].view(-1, 16)[:, 0].long().clamp_(max=N_CODES - 1)
+        c[N_CODES:].scatter_add_(0, pv, t.ones_like(pv))
 
     def __call__(self, results_u8, status_u8, n_props: int, n_votes: int) -> None:
         import torch.distributed as dist

@@ -198,7 +198,11 @@ typedef struct hlc_ctx hlc_ctx;
 
 /* ---- Context -------------------------------------------------------------------- */
 /* Creates a context on HIP device `device` (process-global lazily-initialised device
- * state is what the static `Signer::verify` of signing.rs:69 needs). */
+ * state is what the static `Signer::verify` of signing.rs:69 needs).  Every context allocates
+ * and builds its fixed-base tables (~40 ms): the u1 G comb of the recovery, 12 x 2^21 affine
+ * points = 1.5 GiB of HBM, and the 512 KiB signing comb; HLC_ENOMEM (with hlc_last_error) when
+ * they do not fit.  The recovery's per-lane workspace (~360 MB) and the per-vote workspace
+ * (~0.5 KB per vote of the largest batch) are allocated on first use (or hlc_ctx_reserve). */
 int hlc_ctx_create(int device, hlc_ctx** out);
 void hlc_ctx_destroy(hlc_ctx* ctx);
 /* Pre-sizes the validate-many workspace (hlc_validate_proposals[_device] up to these sizes then

@@ -1,6 +1,6 @@
 """The checked recovery chains on the GPU.  k_rec_main runs its u2 R and u1 G chains with the
 unchecked mixed addition and reroutes a vote through the checked chains (every addition tests
-a == +-b) only when a final Z is zero (hlc_recover.hpp rec_main29).  Crafted inputs that reach
+a == +-b) only when a final Z is zero (hlc_recover.hpp rec_u2r29 / rec_comb29).  Crafted inputs that reach
 that route cannot be built for the shipped comb (tests/crypto_items.py
 comb_collisions_possible), so a context created with HLC_REC_FORCE_EXACT=1 sends EVERY vote
 through the checked chains: its outcomes must equal the default context's and the oracle's,
