@@ -54,6 +54,10 @@ def load():
     lib.hlco_consensus_result.restype = c_int
     lib.hlco_threshold_value.argtypes = [c_uint32, c_double]
     lib.hlco_threshold_value.restype = c_uint32
+    lib.hlco_check_round_limit.argtypes = [c_int, c_uint32, c_double, c_uint32, c_uint32, c_uint64]
+    lib.hlco_check_round_limit.restype = c_int
+    lib.hlco_update_round.argtypes = [c_int, c_uint32, c_uint64]
+    lib.hlco_update_round.restype = c_uint32
     _lib = lib
     return lib
 
@@ -152,3 +156,13 @@ def consensus_result(total, yes, n, t, liveness, is_timeout):
 
 def threshold_value(n, t):
     return int(load().hlco_threshold_value(n, t))
+
+
+def check_round_limit(gossipsub: bool, max_rounds: int, t: float, n: int, round_: int, vote_count: int) -> bool:
+    """session.rs:306-344 restated in C (any round, usize vote_count)."""
+    return bool(load().hlco_check_round_limit(int(gossipsub), max_rounds, t, n, round_, vote_count))
+
+
+def update_round(gossipsub: bool, round_: int, vote_count: int) -> int:
+    """session.rs:351-366 restated in C (P2P saturating at u32::MAX)."""
+    return int(load().hlco_update_round(int(gossipsub), round_, vote_count))

@@ -892,6 +892,35 @@ int hlco_consensus_result(u32 total, u32 yes, u32 n, double t, int liveness, int
 
 u32 hlco_threshold_value(u32 n, double t) { return threshold_value(n, t); }
 
+/* ConsensusConfig::max_round_limit (session.rs:120-128) */
+static u32 max_round_limit(int gossipsub, u32 max_rounds, double t, u32 n) {
+  if (gossipsub) return max_rounds;
+  return max_rounds ? max_rounds : threshold_value(n, t);
+}
+
+/* check_round_limit (session.rs:306-344) for any round and a usize vote_count: 1 = within the
+ * limit, 0 = MaxRoundsExceeded.  vote_count is compared with n (u32) before any u32 arithmetic
+ * (session.rs:308); the P2P projection saturates in u32 (session.rs:330-331). */
+int hlco_check_round_limit(int gossipsub, u32 max_rounds, double t, u32 n, u32 round, u64 vote_count) {
+  if (vote_count > (u64)n) return 0;
+  u32 projected;
+  if (gossipsub) {
+    projected = (round == 2 || (round == 1 && vote_count > 0)) ? 2u : round;
+  } else {
+    const u32 cur = round ? round - 1u : 0u;
+    const u64 sum = (u64)cur + (u32)vote_count;
+    projected = sum > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)sum;
+  }
+  return projected <= max_round_limit(gossipsub, max_rounds, t, n);
+}
+
+/* update_round (session.rs:351-366): Gossipsub 1 -> 2 on any votes; P2P saturating_add */
+u32 hlco_update_round(int gossipsub, u32 round, u64 vote_count) {
+  if (gossipsub) return (round == 1 && vote_count > 0) ? 2u : round;
+  const u64 sum = (u64)round + (u32)vote_count;
+  return sum > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)sum;
+}
+
 static void finish_proposal(const hlc_votes* vs, const hlc_proposal* p, u64 now, const u8* vst,
                             const u8* vreason, hlc_result* res) {
   memset(res, 0, sizeof *res);
@@ -912,12 +941,11 @@ static void finish_proposal(const hlc_votes* vs, const hlc_proposal* p, u64 now,
   if (st) { res->status = (u8)st; res->bad_index = bad; return; }
   u32 ev = p->expected_voters_count;
   if (n > ev) { res->status = HLC_MAX_ROUNDS_EXCEEDED; return; }
-  /* check_round_limit at round 1 (session.rs:306-344) */
-  u32 projected = p->use_gossipsub_rounds ? 2u : n;
-  u32 limit;
-  if (p->use_gossipsub_rounds) limit = p->max_rounds;
-  else limit = p->max_rounds ? p->max_rounds : threshold_value(ev, p->consensus_threshold);
-  if (projected > limit) { res->status = HLC_MAX_ROUNDS_EXCEEDED; return; }
+  /* check_round_limit at round 1 (session.rs:289, 306-344) */
+  if (!hlco_check_round_limit(p->use_gossipsub_rounds, p->max_rounds, p->consensus_threshold, ev, 1u, n)) {
+    res->status = HLC_MAX_ROUNDS_EXCEEDED;
+    return;
+  }
   u32 yes = 0;
   for (u32 j = 0; j < n; ++j) yes += vs->vote[p->vote_begin + j] ? 1 : 0;
   res->yes = yes;

@@ -561,14 +561,25 @@ class ConsensusConfig:
 
 
 def check_round_limit(cfg: ConsensusConfig, n: int, round_: int, vote_count: int) -> bool:
-    """session.rs:306-344 -> True if within limit."""
+    """session.rs:306-344 -> True if within limit.  vote_count is a usize: it is compared with n
+    before any u32 arithmetic (session.rs:308), so a count past u32::MAX fails there (the
+    reference's own test, session.rs:644-672); the P2P projection is
+    round.saturating_sub(1).saturating_add(vote_count as u32) in u32 (session.rs:330-331)."""
     if vote_count > n:
         return False
     if cfg.use_gossipsub_rounds:
         projected = 2 if (round_ == 2 or (round_ == 1 and vote_count > 0)) else round_
     else:
-        projected = min(max(round_ - 1, 0) + vote_count, _U32)
+        projected = min(max(round_ - 1, 0) + (vote_count & _U32), _U32)
     return projected <= cfg.max_round_limit(n)
+
+
+def update_round(cfg: ConsensusConfig, round_: int, vote_count: int) -> int:
+    """session.rs:351-366: Gossipsub moves 1 -> 2 on any votes; P2P adds the count with
+    saturation at u32::MAX (session.rs:364; the reference's test at session.rs:674-699)."""
+    if cfg.use_gossipsub_rounds:
+        return 2 if (round_ == 1 and vote_count > 0) else round_
+    return min(round_ + (vote_count & _U32), _U32)
 
 
 @dataclass
@@ -617,7 +628,7 @@ def from_proposal(p: Proposal, cfg: ConsensusConfig, now: int,
     if not check_round_limit(cfg, n, 1, len(votes)):                # session.rs:289
         out.status = MAX_ROUNDS_EXCEEDED
         return out
-    out.round = 2 if cfg.use_gossipsub_rounds else min(1 + len(votes), _U32)   # session.rs:351-366
+    out.round = update_round(cfg, 1, len(votes))                    # session.rs:290, 351-366
     out.total = len(votes)
     out.yes = sum(1 for v in votes if v.vote)
     res = calculate_consensus_result(out.total, out.yes, n, cfg.consensus_threshold,

@@ -59,12 +59,8 @@ def _check_round_limit(s: Session, vote_count: int) -> bool:
 
 
 def _update_round(s: Session, vote_count: int) -> None:
-    """session.rs:350-366."""
-    if s.use_gossipsub_rounds:
-        if s.round == 1 and vote_count > 0:
-            s.round = 2
-    else:
-        s.round = min(s.round + vote_count, _U32)
+    """session.rs:350-366 (saturating at u32::MAX for P2P)."""
+    s.round = po.update_round(s.config(), s.round, vote_count)
 
 
 def add_vote(s: Session, v: po.Vote, now: int) -> Tuple[int, int, bool]:

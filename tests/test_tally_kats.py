@@ -75,3 +75,53 @@ def test_threshold_edge_arithmetic():
     for n in [3, 10, 1000, 2**20 + 7]:
         for t in [0.5, 0.75, 0.9, 1.0, T23]:
             assert po.calculate_threshold_based_value(n, t) == coracle.threshold_value(n, t)
+
+
+U32 = 2**32 - 1
+
+
+def test_p2p_round_limit_rejects_huge_vote_count():
+    """session.rs:644-672 (p2p_round_limit_should_reject_effectively_huge_vote_count): a P2P
+    session with expected_voters_count = 1 fed vote_count = u32::MAX + 1 must fail
+    check_round_limit -- the usize count is compared with n before any u32 truncation."""
+    p2p = po.ConsensusConfig.p2p()
+    huge = U32 + 1
+    assert not po.check_round_limit(p2p, 1, 1, huge)
+    assert not coracle.check_round_limit(False, 0, T23, 1, 1, huge)
+    # the same count truncated to u32 would be 0 and pass: the order of the checks matters
+    assert po.check_round_limit(p2p, 1, 1, huge & U32) and coracle.check_round_limit(False, 0, T23, 1, 1, 0)
+
+
+def test_p2p_update_round_saturates_at_u32_max():
+    """session.rs:674-699 (p2p_update_round_should_advance_for_max_u32_vote_count): from round 1,
+    update_round(u32::MAX) advances to exactly u32::MAX (saturating_add, no wrap)."""
+    p2p, g = po.ConsensusConfig.p2p(), po.ConsensusConfig.gossipsub()
+    assert po.update_round(p2p, 1, U32) == U32 == coracle.update_round(False, 1, U32)
+    assert po.update_round(p2p, U32, 1) == U32 == coracle.update_round(False, U32, 1)
+    assert po.update_round(p2p, U32 - 1, 1) == U32 == coracle.update_round(False, U32 - 1, 1)
+    assert po.update_round(p2p, 7, 3) == 10 == coracle.update_round(False, 7, 3)
+    # Gossipsub: round 1 -> 2 on any votes, stays otherwise (session.rs:352-359)
+    for r, k, e in [(1, 0, 1), (1, 1, 2), (1, U32, 2), (2, 5, 2)]:
+        assert po.update_round(g, r, k) == e == coracle.update_round(True, r, k)
+
+
+def test_round_limit_boundaries_agree():
+    """check_round_limit at the u32 edges, both restatements: P2P projections saturate
+    ((round - 1) + count past u32::MAX stays u32::MAX), the ceil(2n/3) cap wraps for n >= 2^31."""
+    cases = [
+        # (gossipsub, max_rounds, n, round, vote_count, expected)
+        (False, U32, U32, U32, 1, True),          # projected saturates to u32::MAX == limit
+        (False, U32, U32, U32, 2, True),
+        (False, U32 - 1, U32, U32, 1, False),     # saturated projection above an explicit cap
+        (False, 0, U32, 1, 1431655765, True),     # (2n).div_ceil(3) wraps: cap 1431655765
+        (False, 0, U32, 1, 1431655766, False),
+        (False, 0, 2**31 + 5, 1, 4, True),        # 2n wraps to 10 -> cap 4
+        (False, 0, 2**31 + 5, 1, 5, False),
+        (False, 0, 1, 0, 1, True),                # round 0: saturating_sub keeps 0
+        (True, 2, 4, 1, 0, True), (True, 2, 4, 1, 4, True), (True, 1, 4, 1, 1, False),
+        (True, 2, 4, 3, 1, False),                # a round past 2 stays as it is
+    ]
+    for goss, mr, n, r, k, e in cases:
+        cfg = po.ConsensusConfig(T23, mr, goss, True)
+        assert po.check_round_limit(cfg, n, r, k) == e, (goss, mr, n, r, k)
+        assert coracle.check_round_limit(goss, mr, T23, n, r, k) == e, (goss, mr, n, r, k)
