@@ -39,8 +39,9 @@ int set_err(int code, const std::string& msg) {
 struct DBuf {
   void* p = nullptr;
   size_t cap = 0;
+  bool borrowed = false;  // a pipeline child's view of its parent's fixed-base tables
   ~DBuf() {
-    if (p) (void)hipFree(p);
+    if (p && !borrowed) (void)hipFree(p);
   }
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
@@ -76,9 +77,13 @@ struct hlc_ctx {
   uint64_t rec_lanes = 0;
   int rec_force_exact = 0;  // HLC_REC_FORCE_EXACT=1: every vote through the checked chains (tests)
   int serial_stages = 0;    // HLC_SERIAL_STAGES=1: prep + main after the prehash on one stream (A/B, clock probes)
+  // hlc_validate_proposals pipeline: two child contexts (own streams and workspace, the parent's
+  // fixed-base tables) that take alternate proposal chunks, so one chunk's host->device copy and
+  // the next chunk's kernels overlap the previous chunk's kernels (created on first use)
+  hlc_ctx* pipe[2] = {nullptr, nullptr};
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
-  DBuf in_off2, in_len2, in_off3, in_len3, in_priv;
+  DBuf in_off2, in_len2, in_off3, in_len3, in_priv, byz_key;
   // outputs staged on device
   DBuf out_res, out_status, out_reason, out_rec, out_misc;
   // internal workspace
@@ -528,6 +533,175 @@ int stage_votes(hlc_ctx* c, const hlc_votes* v, hlc_votes* dv, hipStream_t s) {
   return 0;
 }
 
+// Pointer/field checks of votes [v0, v1) (check_votes_host's rule) and the arena span they use.
+int check_vote_range(const hlc_votes* v, uint64_t v0, uint64_t v1, uint64_t* a_lo, uint64_t* a_hi) {
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (uint64_t i = v0 * HLC_NFIELDS; i < v1 * HLC_NFIELDS; ++i) {
+    const uint64_t off = v->field_off[i], len = v->field_len[i];
+    if (!len) continue;
+    if (!v->bytes || off + len > v->bytes_len || off + len < off)
+      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+    lo = std::min(lo, off);
+    hi = std::max(hi, off + len);
+  }
+  *a_lo = lo == UINT64_MAX ? 0 : lo;
+  *a_hi = lo == UINT64_MAX ? 0 : hi;
+  return 0;
+}
+
+int make_child(hlc_ctx* parent, hlc_ctx** out) {
+  hlc_ctx* c = new hlc_ctx();
+  c->device = parent->device;
+  c->rec_force_exact = parent->rec_force_exact;
+  c->serial_stages = parent->serial_stages;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    hipStream_t st = c->stream, ax = c->aux;
+    delete c;
+    if (st) (void)hipStreamDestroy(st);
+    if (ax) (void)hipStreamDestroy(ax);
+    return set_err(HLC_EDEVICE, "pipeline stream creation failed");
+  }
+  for (auto pr : {std::make_pair(&c->gtab, &parent->gtab), std::make_pair(&c->fbtab, &parent->fbtab)}) {
+    pr.first->p = pr.second->p;
+    pr.first->cap = pr.second->cap;
+    pr.first->borrowed = true;
+  }
+  *out = c;
+  return 0;
+}
+
+void destroy_ctx(hlc_ctx* ctx) {
+  if (!ctx) return;
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
+  hipStream_t s = ctx->stream, a = ctx->aux;
+  delete ctx;
+  if (s) (void)hipStreamDestroy(s);
+  if (a) (void)hipStreamDestroy(a);
+}
+
+// Votes per pipeline chunk (HLC_PIPE_CHUNK_VOTES overrides; 0 disables the pipeline).
+uint64_t pipe_chunk_votes() {
+  const char* e = std::getenv("HLC_PIPE_CHUNK_VOTES");
+  return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)131072;
+}
+
+struct Chunk {
+  uint64_t p0, p1, v0, v1;
+};
+
+// hlc_validate_proposals over host buffers, pipelined: the proposals are cut into chunks of about
+// pipe_chunk_votes() votes (contiguous proposal ranges whose vote ranges are disjoint and in
+// order -- the layout of prost-decoded / packed batches; any other layout returns *used = false and
+// takes the one-shot path).  Chunk k runs on child context pipe[k % 2]: the host checks chunk k's
+// fields and copies its SoA slices + arena span in while chunk k-1's kernels run on the other
+// child, then launches chunk k, then copies chunk k-1's outputs back.  Chunks on the two children
+// also overlap on the device (the next chunk's blocks fill the previous one's grid tail).
+int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
+                       hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec, bool* used) {
+  *used = false;
+  const uint64_t target = pipe_chunk_votes(), n = v->n;
+  if (!target || n < 2 * target || np < 2) return 0;
+  std::vector<Chunk> ch;
+  {
+    Chunk cur{0, 0, UINT64_MAX, 0};
+    uint64_t acc = 0;
+    for (uint64_t p = 0; p < np; ++p) {
+      const uint64_t b = props[p].vote_begin, e = b + props[p].vote_count;
+      if (props[p].vote_count) {
+        cur.v0 = std::min(cur.v0, b);
+        cur.v1 = std::max(cur.v1, e);
+      }
+      acc += props[p].vote_count;
+      cur.p1 = p + 1;
+      if (acc >= target || p + 1 == np) {
+        if (cur.v0 == UINT64_MAX) cur.v0 = cur.v1 = ch.empty() ? 0 : ch.back().v1;
+        ch.push_back(cur);
+        cur = Chunk{p + 1, p + 1, UINT64_MAX, 0};
+        acc = 0;
+      }
+    }
+  }
+  for (size_t k = 1; k < ch.size(); ++k)
+    if (ch[k].v0 < ch[k - 1].v1) return 0;  // interleaved vote ranges: one-shot path
+  if (ch.size() < 2) return 0;
+  for (int k = 0; k < 2; ++k)
+    if (!c->pipe[k]) CHK(make_child(c, &c->pipe[k]));
+  *used = true;
+  std::vector<hlc_proposal> cp;
+  auto finish = [&](size_t k) -> int {
+    hlc_ctx* w = c->pipe[k & 1];
+    const Chunk& q = ch[k];
+    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
+    hipStream_t s = w->stream;
+    if (npk)
+      HIPCHK(hipMemcpyAsync(out_res + q.p0, w->out_res.p, npk * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
+    if (out_st && nv) HIPCHK(hipMemcpyAsync(out_st + q.v0, w->out_status.p, nv, hipMemcpyDeviceToHost, s));
+    if (out_rs && nv) HIPCHK(hipMemcpyAsync(out_rs + q.v0, w->out_reason.p, nv, hipMemcpyDeviceToHost, s));
+    if (out_rec && nv) HIPCHK(hipMemcpyAsync(out_rec + 20 * q.v0, w->out_rec.p, nv * 20, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+  };
+  auto drain = [&]() {
+    for (int k = 0; k < 2; ++k) (void)hipStreamSynchronize(c->pipe[k]->stream);
+  };
+  for (size_t k = 0; k < ch.size(); ++k) {
+    hlc_ctx* w = c->pipe[k & 1];
+    const Chunk& q = ch[k];
+    uint64_t a_lo = 0, a_hi = 0, g_lo = 0, g_hi = 0;
+    // the chunk's votes, and (same rule as the one-shot path) the uncovered votes before it
+    int rc = check_vote_range(v, k ? ch[k - 1].v1 : 0, q.v0, &g_lo, &g_hi);
+    if (!rc) rc = check_vote_range(v, q.v0, q.v1, &a_lo, &a_hi);
+    if (!rc && k + 1 == ch.size()) rc = check_vote_range(v, q.v1, n, &g_lo, &g_hi);
+    if (rc) {
+      drain();
+      return rc;
+    }
+    hipStream_t s = w->stream;
+    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
+    hlc_votes hv;
+    hv.n = nv;
+    hv.vote_id = v->vote_id + q.v0;
+    hv.proposal_id = v->proposal_id + q.v0;
+    hv.timestamp = v->timestamp + q.v0;
+    hv.vote = v->vote + q.v0;
+    hv.field_off = v->field_off + q.v0 * HLC_NFIELDS;
+    hv.field_len = v->field_len + q.v0 * HLC_NFIELDS;
+    hv.bytes = v->bytes ? v->bytes + a_lo : nullptr;
+    hv.bytes_len = a_hi - a_lo;
+    hlc_votes dv;
+    CHK(stage_votes(w, &hv, &dv, s));
+    dv.bytes -= a_lo;  // the field offsets stay absolute: bytes + off lands in the staged span
+    cp.assign(props + q.p0, props + q.p1);
+    for (auto& pr : cp) pr.vote_begin = pr.vote_count ? pr.vote_begin - q.v0 : 0;
+    CHK(upload(w->in_props, cp.data(), npk, s));
+    CHK(w->out_res.ensure(npk * sizeof(hlc_result) + 16));
+    CHK(w->out_status.ensure(nv + 1));
+    CHK(w->out_reason.ensure(nv + 1));
+    if (out_rec) CHK(w->out_rec.ensure(nv * 20 + 20));
+    CHK(validate_device(w, &dv, w->in_props.as<hlc_proposal>(), npk, now, w->out_res.as<hlc_result>(),
+                        w->out_status.as<uint8_t>(), w->out_reason.as<uint8_t>(),
+                        out_rec ? w->out_rec.as<uint8_t>() : nullptr, s));
+    if (k) CHK(finish(k - 1));
+  }
+  CHK(finish(ch.size() - 1));
+  // votes between the chunks' ranges are covered by no proposal: not evaluated (as the one-shot path)
+  uint64_t prev = 0;
+  for (size_t k = 0; k <= ch.size(); ++k) {
+    const uint64_t g1 = k < ch.size() ? ch[k].v0 : n;
+    if (g1 > prev) {
+      if (out_st) std::memset(out_st + prev, 0xFF, g1 - prev);
+      if (out_rs) std::memset(out_rs + prev, 0, g1 - prev);
+      if (out_rec) std::memset(out_rec + 20 * prev, 0, 20 * (g1 - prev));
+    }
+    if (k < ch.size()) prev = std::max(prev, ch[k].v1);
+  }
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -586,12 +760,11 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
 void hlc_ctx_destroy(hlc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
-  hipStream_t s = ctx->stream, a = ctx->aux;
-  delete ctx;
-  if (s) (void)hipStreamDestroy(s);
-  if (a) (void)hipStreamDestroy(a);
+  for (auto& ch : ctx->pipe) {  // children first: they borrow the parent's fixed-base tables
+    destroy_ctx(ch);
+    ch = nullptr;
+  }
+  destroy_ctx(ctx);
 }
 
 int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, uint64_t max_bytes) {
@@ -696,14 +869,26 @@ int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_propo
                            uint64_t n_proposals, uint64_t now, hlc_result* out_results, uint8_t* out_vote_status,
                            uint8_t* out_vote_reason, uint8_t* out_recovered) {
   if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
-  CHK(check_votes_host(votes));
+  if (!votes) return set_err(HLC_EINVAL, "votes is NULL");
+  if (votes->n && (!votes->vote_id || !votes->proposal_id || !votes->timestamp || !votes->vote ||
+                   !votes->field_off || !votes->field_len))
+    return set_err(HLC_EINVAL, "NULL vote array");
   if (n_proposals && (!proposals || !out_results)) return set_err(HLC_EINVAL, "NULL proposals/results");
   for (uint64_t p = 0; p < n_proposals; ++p) {
-    if (proposals[p].vote_begin + proposals[p].vote_count > votes->n)
+    if (proposals[p].vote_begin + proposals[p].vote_count > votes->n ||
+        proposals[p].vote_begin + proposals[p].vote_count < proposals[p].vote_begin)
       return set_err(HLC_EINVAL, "proposal vote range outside the vote batch");
   }
+  if (votes->n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
+  {
+    bool used = false;
+    CHK(validate_pipelined(ctx, votes, proposals, n_proposals, now, out_results, out_vote_status, out_vote_reason,
+                           out_recovered, &used));
+    if (used) return 0;
+  }
+  CHK(check_votes_host(votes));
   hipStream_t s = ctx->stream;
   const uint64_t n = votes->n;
   hlc_votes dv;
@@ -1046,6 +1231,27 @@ int hlc_synth_votes_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_proposal,
   CHK(ensure_fbtab(ctx));
   hlc::launch_synth(seed, start_proposal, n_proposals, votes_per_proposal, expected_voters, gossipsub, out_votes,
                     out_proposals, out_priv, ctx->fbtab.as<uint32_t>(), s);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int hlc_synth_byzantine_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_proposal, uint64_t n_proposals,
+                               uint32_t votes_per_proposal, const hlc_votes* votes, uint8_t* out_kind,
+                               void* stream) {
+  if (!ctx || !votes) return set_err(HLC_EINVAL, "NULL argument");
+  const uint64_t n = n_proposals * (uint64_t)votes_per_proposal;
+  if (votes_per_proposal && n / votes_per_proposal != n_proposals) return set_err(HLC_EINVAL, "size overflow");
+  if (votes->n != n) return set_err(HLC_EINVAL, "votes->n must be n_proposals * votes_per_proposal");
+  if (n && (!out_kind || !votes->bytes || !votes->field_off || !votes->field_len || !votes->timestamp ||
+            !votes->proposal_id || !votes->vote_id || !votes->vote))
+    return set_err(HLC_EINVAL, "NULL vote / output array");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  CHK(ensure_fbtab(ctx));
+  CHK(ctx->byz_key.ensure(n * 8 + 8));
+  hlc::launch_synth_byzantine(seed, start_proposal, n_proposals, votes_per_proposal, votes, out_kind,
+                              ctx->byz_key.as<uint64_t>(), ctx->fbtab.as<uint32_t>(), s);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -175,6 +175,11 @@ uint64_t synth_arena_bytes(uint64_t n_proposals, uint64_t votes_per_proposal);
 void launch_synth(uint64_t seed, uint64_t start, uint64_t n_proposals, uint32_t votes_per_proposal, uint32_t expected,
                   int gossipsub, const hlc_votes* out, hlc_proposal* props, uint8_t* priv_out, const uint32_t* fbtab,
                   hipStream_t s);
+// config 5 on the device (hlc_synth.hip k_byz_*): mutates a launch_synth batch in place; kind_out[n]
+// (HLC_BYZ_*), key_work u64[n] scratch
+void launch_synth_byzantine(uint64_t seed, uint64_t start, uint64_t n_proposals, uint32_t votes_per_proposal,
+                            const hlc_votes* votes, uint8_t* kind_out, uint64_t* key_work, const uint32_t* fbtab,
+                            hipStream_t s);
 
 constexpr size_t FBTAB_WORDS = 32 * 256 * 16;   // fixed-base comb: 32 windows x 256 affine points
 

@@ -103,15 +103,23 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
                                                                      const uint32_t* rec, uint32_t* q, uint8_t* mst,
                                                                      int force_exact, unsigned long long* ctr) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#ifdef HLC_PROBE_WAVE_TABLE
-  // timing probe only (wrong results): every lane of a wave builds and gathers ONE shared R table
-  // and z-ratio column (its wave's lane 0's), so the table traffic stays in L1/L2 (1.8 KB per wave)
-  const uint64_t tws = tid & ~(uint64_t)63;
+#if defined(HLC_PROBE_SHARE_TABLE)
+  // timing probe only (wrong results): HLC_PROBE_SHARE_TABLE lanes (a power of two) build and gather
+  // ONE shared R table and z-ratio column: 64 keeps the table traffic in L1/L2 (1.8 KB per wave), 2
+  // halves the workspace footprint (358 -> 179 MB, inside the 256 MB Infinity Cache)
+  const uint64_t tws = tid & ~(uint64_t)(HLC_PROBE_SHARE_TABLE - 1);
 #else
   const uint64_t tws = tid;
 #endif
   uint32_t* ws = scratch + tws;
   uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tws * RTAB_WORDS;
+#ifdef HLC_REC_GLDS
+  // per wave: the LDS-DMA staging slots of the u2 R chain's table gathers (chain_u2r29), 10 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t s_rt[REC_TPB / 64][RT_WAVE_WORDS];
+  uint32_t* lds = s_rt[threadIdx.x >> 6];
+#else
+  uint32_t* lds = nullptr;
+#endif
 #ifdef HLC_CLOCK_PROBE
   // A/B probe (make variant NAME=clk DEFS=-DHLC_CLOCK_PROBE): the shader clock a wave sees under
   // the real kernel = core-clock ticks (clock64) over constant 100 MHz ticks (wall_clock64)
@@ -142,7 +150,7 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
     fe r, qx, qy, qz;
     bool inf = false;
     fe_load_be(r, bytes + sig_off[i * off_stride]);
-    const int code = rec_u2r29(r, rec + i, n, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0);
+    const int code = rec_u2r29(r, rec + i, n, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0, lds);
     if (code != SCHEME_NONE) {
       mst[i] = (uint8_t)(1 + code);
       continue;

@@ -393,10 +393,36 @@ HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
   }
 }
 
+// A/B variant -DHLC_REC_GLDS (not the default): LDS staging of the R-table gathers.  A window's two
+// entries (b1, b2) arrive by LDS-DMA -- global_load_lds_dwordx4, 5 pieces of 16 B per lane, 1 KiB
+// per wave-instruction, no VGPR destination -- issued right after the previous window's additions,
+// so the gathers' latency hides behind 5 doublings with no registers held in flight.  Measured
+// neutral (91.17 vs 91.13 M votes/s, profiles/r03_ab_glds.txt): the gathers' latency is already
+// hidden by the other waves; what the table costs is traffic.  RT_SLOT words per
+// entry slot: piece k of lane l at word 256 k + 4 l.
+constexpr int RT_SLOT = 5 * 256;
+constexpr int RT_WAVE_WORDS = 2 * RT_SLOT;  // b1 and b2 slots: 10 KiB per wave
+HLC_DEV void glds_entry(const uint32_t* ent, uint32_t* slot) {
+#pragma unroll
+  for (int k = 0; k < 5; ++k) __builtin_amdgcn_global_load_lds((const void*)(ent + 4 * k), (void*)(slot + 256 * k), 16, 0, 0);
+}
+HLC_DEV void lds_entry(ge29& g, const uint32_t* slot, unsigned lane) {
+  const uint4* p = reinterpret_cast<const uint4*>(slot) + lane;
+  const uint4 a = p[0], b = p[64], c = p[128], d = p[192], e = p[256];
+  g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
+  g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
+  g.x.v[8] = c.x; g.y.v[0] = c.y; g.y.v[1] = c.z; g.y.v[2] = c.w;
+  g.y.v[3] = d.x; g.y.v[4] = d.y; g.y.v[5] = d.z; g.y.v[6] = d.w;
+  g.y.v[7] = e.x; g.y.v[8] = e.y;
+}
+HLC_DEV void wait_glds() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // u2 R over the lane's R table (odd multiples 1..31 of R in one common-Z frame, zg = that Z):
 // regular signed digits of the GLV halves b1, b2 (b2 against lambda R = (beta x, y)).
+// lds: this wave's RT_WAVE_WORDS staging words (HLC_REC_GLDS only).
 template <bool EXACT>
-HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const uint32_t* tab, const fe29& zg) {
+HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const uint32_t* tab, const fe29& zg,
+                         uint32_t* lds) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
   fe29 beta;
@@ -404,17 +430,51 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
   const uint32_t* dws = rec + (size_t)REC_DIG * stride;
   gej29_set_inf(acc);
   // Additions in order (window 25, b1), (25, b2), 5 doublings, (24, b1), ... -- the two halves add
-  // at the same positions (uniform across the wave).  Register pressure, not load latency, bounds
-  // this loop: the b1 entry is loaded before the last doubling of its window (one point operation
-  // ahead) and the b2 entry right after the b1 addition (its latency hidden by the other waves).
-  auto digit_at = [&](int win, int k) {
-    return digit16(dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride], win & 1);
-  };
+  // at the same positions (uniform across the wave).
+  auto word_at = [&](int win, int k) { return dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride]; };
+  auto digit_at = [&](int win, int k) { return digit16(word_at(win, k), win & 1); };
 #ifdef HLC_PROBE_HOT_GATHER
   auto entry_of = [&](int d) { return tab; };  // timing probe only (wrong results): no table traffic
 #else
   auto entry_of = [&](int d) { return tab + RTAB_ENTRY * (((d < 0 ? -d : d) - 1) >> 1); };
 #endif
+#ifdef HLC_REC_GLDS
+  const unsigned lane = threadIdx.x & 63u;
+  uint32_t* s1 = lds;
+  uint32_t* s2 = lds + RT_SLOT;
+  int win = M_R - 1;
+  int d1 = digit_at(win, 0), d2 = digit_at(win, 1);
+  glds_entry(entry_of(d1), s1);
+  glds_entry(entry_of(d2), s2);
+#pragma unroll 1
+  for (;;) {
+    // the next window's digit words: ordinary loads, first used after this window's additions
+    uint32_t n1 = 0, n2 = 0;
+    if (win > 0) {
+      n1 = word_at(win - 1, 0);
+      n2 = word_at(win - 1, 1);
+    }
+    if (win != M_R - 1) {
+#pragma unroll 1
+      for (int q = 0; q < W_R; ++q) gej29_double(acc, acc);
+    }
+    wait_glds();
+    ge29 g;
+    lds_entry(g, s1, lane);
+    fe29_cneg_lazy(g.y, g.y, (d1 < 0) != ((negs & 1) != 0));
+    gej29_madd<EXACT>(acc, acc, g);
+    lds_entry(g, s2, lane);
+    fe29_mul_uniform(g.x, g.x, beta);
+    fe29_cneg_lazy(g.y, g.y, (d2 < 0) != ((negs & 2) != 0));
+    gej29_madd<EXACT>(acc, acc, g);
+    if (win == 0) break;
+    --win;
+    d1 = digit16(n1, win & 1);
+    d2 = digit16(n2, win & 1);
+    glds_entry(entry_of(d1), s1);  // the slots were read above (the additions used them)
+    glds_entry(entry_of(d2), s2);
+  }
+#else
 #pragma unroll 1
   for (int win = M_R - 1; win >= 0; --win) {
     ge29 g;
@@ -427,12 +487,6 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
     } else {
       load_ge29_tab(g, entry_of(d));
     }
-#ifdef HLC_B2_LATE
-    fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 1) != 0));
-    gej29_madd<EXACT>(acc, acc, g);
-    d = digit_at(win, 1);
-    load_ge29_tab(g, entry_of(d));
-#else
     // the b2 entry is loaded before the b1 addition: its gather latency hides behind that addition
     const int d2 = digit_at(win, 1);
     ge29 g2;
@@ -441,11 +495,11 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
     gej29_madd<EXACT>(acc, acc, g);
     g = g2;
     d = d2;
-#endif
     fe29_mul_uniform(g.x, g.x, beta);
     fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 2) != 0));
     gej29_madd<EXACT>(acc, acc, g);
   }
+#endif
 #pragma unroll 1
   for (int k = 0; k < 2; ++k) {
     if (((skews >> k) & 1) == 0) continue;
@@ -465,7 +519,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
 // when its own Z comes out zero (the unchecked chain is exact whenever its Z is non-zero, so this
 // is the combined stage's test split per chain).
 HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz, bool& inf,
-                      uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact) {
+                      uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact, uint32_t* lds) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int parity = (int)((flags >> 5) & 1u);
   ge29 R;
@@ -518,8 +572,8 @@ HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx,
     fe29_mul(zg, sc, d.z);
   }
   gej29 acc;
-  chain_u2r29<false>(acc, rec, stride, tab, zg);
-  if (force_exact || (!acc.inf && fe29_is_zero_modp(acc.z))) chain_u2r29<true>(acc, rec, stride, tab, zg);
+  chain_u2r29<false>(acc, rec, stride, tab, zg, lds);
+  if (force_exact || (!acc.inf && fe29_is_zero_modp(acc.z))) chain_u2r29<true>(acc, rec, stride, tab, zg, lds);
   inf = acc.inf;
   fe29_to32(qx.v, acc.x);
   fe29_to32(qy.v, acc.y);

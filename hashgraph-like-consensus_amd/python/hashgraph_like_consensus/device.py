@@ -69,6 +69,20 @@ class DeviceBatch:
             self.torch.cuda.synchronize(device)
         return self
 
+    def make_byzantine(self, engine, seed: int, start_proposal: int = 0) -> np.ndarray:
+        """SURVEY.md §8d config 5 on the device: mutate this synthetic batch (made by `synthetic`
+        with the same seed / start) into the 1/3-Byzantine mix in place (hlc_synth_byzantine_device)
+        and return the per-vote mutation kinds (byzantine.py)."""
+        import torch
+        V = self.n // max(self.n_proposals, 1)
+        kinds = torch.zeros(max(self.n, 1), dtype=torch.uint8, device=self.device)
+        engine.synth_byzantine_device(self, seed, start_proposal, self.n_proposals, V, kinds.data_ptr())
+        torch.cuda.synchronize(self.device)
+        return kinds[: self.n].cpu().numpy()
+
+    def choice_numpy(self) -> np.ndarray:
+        return self._t["vote"][: self.n].cpu().numpy()
+
     def _bind(self, t, n: int, bytes_len: int, n_proposals: int, now: int, device: str) -> None:
         import torch
         self.torch = torch

@@ -240,6 +240,14 @@ class Engine:
             ctypes.byref(dbatch.view), c_void_p(ctypes.cast(dbatch.props_ptr, c_void_p).value),
             c_void_p(priv_ptr) if priv_ptr else None, c_void_p(stream_handle) if stream_handle else None))
 
+    def synth_byzantine_device(self, dbatch, seed: int, start_proposal: int, n_proposals: int,
+                               votes_per_proposal: int, kind_ptr: int, stream_handle: int = 0) -> None:
+        """hlc_synth_byzantine_device: the config-5 mutations, in place, over a batch made by
+        synth_votes_device with the same arguments; per-vote kinds (HLC_BYZ_*) into kind_ptr."""
+        _ffi.check(self.lib.hlc_synth_byzantine_device(
+            self.ctx, seed, start_proposal, n_proposals, votes_per_proposal, ctypes.byref(dbatch.view),
+            c_void_p(kind_ptr), c_void_p(stream_handle) if stream_handle else None))
+
     def validate_wire_proposals_device(self, dwire, stream_handle: int = 0) -> None:
         """hlc_validate_wire_proposals_device over a `device.DeviceWire` (wire bytes, message
         extents and scope configs in HBM); results land in dwire.results."""

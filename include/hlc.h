@@ -304,6 +304,34 @@ int hlc_synth_votes_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_proposal,
                            const hlc_votes* out_votes, hlc_proposal* out_proposals, uint8_t* out_priv,
                            void* stream);
 
+/* SURVEY.md §8d config 5 on the device: turns a batch made by hlc_synth_votes_device with the
+ * same (seed, start_proposal, n_proposals, votes_per_proposal) into the 1/3-Byzantine mix, in
+ * place, by product code only (re-hashing and re-signing on the device), and reports each vote's
+ * mutation kind in out_kind[n] (HLC_BYZ_*).  Every kind is built to have one validate_vote /
+ * from_proposal outcome (hlc_synth.hip; the host-side expectation is
+ * python/hashgraph_like_consensus/byzantine.py).  Device pointers, enqueued on `stream`. */
+#define HLC_BYZ_NONE 0
+#define HLC_BYZ_WRONG_KEY 1     /* InvalidVoteSignature */
+#define HLC_BYZ_FLIP_S 2        /* InvalidVoteSignature */
+#define HLC_BYZ_BAD_V 3         /* SignatureScheme, parity */
+#define HLC_BYZ_HIGH_S 4        /* Ok: alloy normalises a high s */
+#define HLC_BYZ_NO_POINT 5      /* SignatureScheme, no point */
+#define HLC_BYZ_INFINITY 6      /* SignatureScheme, Q = infinity */
+#define HLC_BYZ_TAMPER_HASH 7   /* InvalidVoteHash */
+#define HLC_BYZ_SIG_LEN 8       /* SignatureScheme, length */
+#define HLC_BYZ_EMPTY_OWNER 9   /* EmptyVoteOwner */
+#define HLC_BYZ_EMPTY_HASH 10   /* EmptyVoteHash */
+#define HLC_BYZ_EMPTY_SIG 11    /* EmptySignature */
+#define HLC_BYZ_WRONG_PID 12    /* VoteProposalIdMismatch */
+#define HLC_BYZ_TS_OLD 13       /* TimestampOlderThanCreationTime */
+#define HLC_BYZ_BAD_RECEIVED 14 /* per-vote Ok; chain ReceivedHashMismatch */
+#define HLC_BYZ_TS_REGRESS 15   /* per-vote Ok; chain ReceivedHashMismatch */
+#define HLC_BYZ_PARENT_OTHER 16 /* per-vote Ok; chain ParentHashMismatch */
+#define HLC_BYZ_DUPLICATE 17    /* per-vote Ok; DuplicateVote */
+int hlc_synth_byzantine_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_proposal, uint64_t n_proposals,
+                               uint32_t votes_per_proposal, const hlc_votes* votes, uint8_t* out_kind,
+                               void* stream);
+
 /* ---- Streaming votes ---------------------------------------------- */
 
 /* `ConsensusService::process_incoming_vote` (service.rs:286-305) for n votes delivered in

@@ -89,9 +89,18 @@ def eip191_hash(b: bytes) -> bytes:
     return out.tobytes()
 
 
-def ecrecover(prehash: bytes, sig: bytes, reverify: bool = True):
+REVERIFY, GLV = 1, 2  # hlco_* flags (hlc_oracle.c)
+
+
+def _flags(reverify: bool, glv: bool) -> int:
+    return (REVERIFY if reverify else 0) | (GLV if glv else 0)
+
+
+def ecrecover(prehash: bytes, sig: bytes, reverify: bool = True, glv: bool = False):
+    """glv: the k256-class recovery (GLV + wNAF + binary-GCD inversions), the timed CPU baseline;
+    default: the independent non-GLV checker."""
     out = np.zeros(20, np.uint8)
-    code = load().hlco_ecrecover(_u8(_buf(prehash)), _u8(_buf(sig)), _u8(out), int(reverify))
+    code = load().hlco_ecrecover(_u8(_buf(prehash)), _u8(_buf(sig)), _u8(out), _flags(reverify, glv))
     return code, (out.tobytes() if code == 0 else None)
 
 
@@ -129,7 +138,8 @@ def encode_vote(batch, i: int) -> bytes:
     return out[:n].tobytes()
 
 
-def validate_proposals(batch, desc: np.ndarray, now: int, threads: int = 8, reverify: bool = False):
+def validate_proposals(batch, desc: np.ndarray, now: int, threads: int = 8, reverify: bool = False,
+                       glv: bool = False):
     """-> (results structured array, vote_status u8[n], vote_reason u8[n], recovered u8[n,20])"""
     from hashgraph_like_consensus import _ffi  # struct layout only
     n = batch.n
@@ -139,14 +149,15 @@ def validate_proposals(batch, desc: np.ndarray, now: int, threads: int = 8, reve
     rec = np.zeros((max(n, 1), 20), np.uint8)
     view = batch.view()
     load().hlco_validate_proposals(ctypes.byref(view), desc.ctypes.data, desc.shape[0], now,
-                                   res.ctypes.data, _u8(vst), _u8(vrs), _u8(rec), threads, int(reverify))
+                                   res.ctypes.data, _u8(vst), _u8(vrs), _u8(rec), threads, _flags(reverify, glv))
     return res, vst[:n], vrs[:n], rec[:n]
 
 
-def validate_votes_only(batch, desc: np.ndarray, now: int, threads: int, reverify: bool = True) -> int:
+def validate_votes_only(batch, desc: np.ndarray, now: int, threads: int, reverify: bool = True,
+                        glv: bool = False) -> int:
     view = batch.view()
     return int(load().hlco_validate_votes_only(ctypes.byref(view), desc.ctypes.data, desc.shape[0], now,
-                                               threads, int(reverify)))
+                                               threads, _flags(reverify, glv)))
 
 
 def consensus_result(total, yes, n, t, liveness, is_timeout):

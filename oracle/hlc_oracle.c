@@ -8,7 +8,8 @@
  * It is an independent restatement of the same semantics as oracle/pyoracle.py, with a
  * deliberately different algorithm from the GPU kernels (4x64-bit limbs, 4-bit fixed
  * windows, no GLV, per-item Fermat inversions) so that agreement is evidence rather than
- * shared bugs.  Reference call sites restated (paths under /root/reference):
+ * shared bugs.  A second, k256-class recovery (GLV + wNAF + binary-GCD inversions, flag
+ * HLCO_GLV) is the timed CPU baseline; it must agree with the checker item for item.  Reference call sites restated (paths under /root/reference):
  *   compute_vote_hash        src/utils.rs:37-47          (sha2 0.10.9)
  *   validate_vote            src/utils.rs:127-171
  *   Vote encode_to_vec       src/utils.rs:150-152        (prost 0.14.4, consensus.proto:19-29)
@@ -30,6 +31,11 @@
 #include <string.h>
 
 #include "../include/hlc.h"
+
+/* hlco_ecrecover / validate flags: also run k256's post-recovery verify_prehash; use the
+ * k256-class GLV path instead of the independent non-GLV checker */
+#define HLCO_REVERIFY 1
+#define HLCO_GLV 2
 
 typedef uint64_t u64;
 typedef uint32_t u32;
@@ -482,6 +488,187 @@ static void ecmult(gej* r, const sc* a, const ge* P, const sc* b) {
   *r = acc;
 }
 
+/* ============== k256-class scalar multiplication (the timed CPU baseline) ==============
+ * The recovery algorithm class of k256 0.13.4 (/root/reference/Cargo.lock; reached at
+ * src/signing/ethereum.rs:89 through alloy's recover_address_from_msg), written the faster
+ * libsecp256k1 way so that the CPU baseline is conservative:
+ *   - GLV endomorphism: every scalar k = k1 + k2 lambda with |k1|, |k2| < 2^128 (k256 lincomb's
+ *     decompose_scalar), so the doubling chain is 129 steps, not 256;
+ *   - variable-time wNAF digits: width 5 for the per-signature point R (odd multiples 1..15 R and
+ *     lambda R, made affine with ONE field inversion by Montgomery's trick), width 8 for G (64 odd
+ *     multiples of G and lambda G, affine, built once);
+ *   - binary extended-Euclid inversions mod p and mod n (k256 uses Fermat chains);
+ *   - Jacobian doublings 2M+5S and mixed additions 8M+3S (k256's complete projective formulas cost
+ *     more per operation).
+ * The non-GLV path above (ecmult) stays the independent checker; the two must agree on every
+ * item (tests/test_openssl_pin.py). */
+static const sc GLV_LAMBDA = {{0xDF02967C1B23BD72ULL, 0x122E22EA20816678ULL, 0xA5261C028812645AULL, 0x5363AD4CC05C30E0ULL}};
+static const fe GLV_BETA = {{0xC1396C28719501EEULL, 0x9CF0497512F58995ULL, 0x6E64479EAC3434E9ULL, 0x7AE96A2B657C0710ULL}};
+static const sc GLV_MINUS_B1 = {{0x6F547FA90ABFE4C3ULL, 0xE4437ED6010E8828ULL, 0, 0}};
+static const sc GLV_MINUS_B2 = {{0xD765CDA83DB1562CULL, 0x8A280AC50774346DULL, 0xFFFFFFFFFFFFFFFEULL, 0xFFFFFFFFFFFFFFFFULL}};
+static const u256 GLV_G1 = {{0xE893209A45DBB031ULL, 0x3DAA8A1471E8CA7FULL, 0xE86C90E49284EB15ULL, 0x3086D221A7D46BCDULL}};
+static const u256 GLV_G2 = {{0x1571B4AE8AC47F71ULL, 0x221208AC9DF506C6ULL, 0x6F547FA90ABFE4C4ULL, 0xE4437ED6010E8828ULL}};
+
+/* round(k g / 2^384) */
+static u256 mul_shift_384(const u256* k, const u256* g) {
+  u64 w[8];
+  mul256(w, k, g);
+  u256 r = {{w[6], w[7], 0, 0}};
+  if (w[5] >> 63) {
+    u256 one = {{1, 0, 0, 0}};
+    u256_add(&r, &r, &one);
+  }
+  return r;
+}
+
+/* k = k1 + k2 lambda (mod n): magnitudes < 2^129 and signs (libsecp256k1 scalar_split_lambda) */
+static void glv_split(const sc* k, sc* k1, int* neg1, sc* k2, int* neg2) {
+  u256 c1 = mul_shift_384(k, &GLV_G1), c2 = mul_shift_384(k, &GLV_G2);
+  sc t1, t2, r2, r1;
+  sc_mul(&t1, &c1, &GLV_MINUS_B1);
+  sc_mul(&t2, &c2, &GLV_MINUS_B2);
+  sc_add(&r2, &t1, &t2);
+  sc_mul(&t1, &r2, &GLV_LAMBDA);
+  sc_neg(&t1, &t1);
+  sc_add(&r1, k, &t1);
+  *neg1 = u256_cmp(&r1, &FN_HALF) > 0;
+  *neg2 = u256_cmp(&r2, &FN_HALF) > 0;
+  if (*neg1) sc_neg(&r1, &r1);
+  if (*neg2) sc_neg(&r2, &r2);
+  *k1 = r1;
+  *k2 = r2;
+}
+
+/* width-w NAF of k (< 2^130): digits[i] odd in (-2^(w-1), 2^(w-1)) or 0; returns the length */
+static int wnaf(int* d, const u256* k, int w) {
+  u256 x = *k;
+  int len = 0;
+  memset(d, 0, 132 * sizeof(int));
+  while (!u256_is_zero(&x)) {
+    int digit = 0;
+    if (x.v[0] & 1) {
+      digit = (int)(x.v[0] & ((1u << w) - 1));
+      if (digit >= (1 << (w - 1))) digit -= (1 << w);
+      u256 dv = {{(u64)(digit < 0 ? -digit : digit), 0, 0, 0}};
+      if (digit < 0) u256_add(&x, &x, &dv); else u256_sub(&x, &x, &dv);
+    }
+    d[len++] = digit;
+    for (int i = 0; i < 3; ++i) x.v[i] = (x.v[i] >> 1) | (x.v[i + 1] << 63);
+    x.v[3] >>= 1;
+  }
+  return len;
+}
+
+/* a^-1 mod m (m odd, 0 < a < m) by the binary extended Euclidean algorithm (variable time) */
+static void modinv_binary(u256* r, const u256* a, const u256* m) {
+  u256 u = *a, v = *m, x1 = {{1, 0, 0, 0}}, x2 = {{0, 0, 0, 0}};
+  const u256 one = {{1, 0, 0, 0}};
+  while (u256_cmp(&u, &one) != 0 && u256_cmp(&v, &one) != 0) {
+    while (!(u.v[0] & 1)) {
+      for (int i = 0; i < 3; ++i) u.v[i] = (u.v[i] >> 1) | (u.v[i + 1] << 63);
+      u.v[3] >>= 1;
+      u64 c = 0;
+      if (x1.v[0] & 1) c = u256_add(&x1, &x1, m);
+      for (int i = 0; i < 3; ++i) x1.v[i] = (x1.v[i] >> 1) | (x1.v[i + 1] << 63);
+      x1.v[3] = (x1.v[3] >> 1) | (c << 63);
+    }
+    while (!(v.v[0] & 1)) {
+      for (int i = 0; i < 3; ++i) v.v[i] = (v.v[i] >> 1) | (v.v[i + 1] << 63);
+      v.v[3] >>= 1;
+      u64 c = 0;
+      if (x2.v[0] & 1) c = u256_add(&x2, &x2, m);
+      for (int i = 0; i < 3; ++i) x2.v[i] = (x2.v[i] >> 1) | (x2.v[i + 1] << 63);
+      x2.v[3] = (x2.v[3] >> 1) | (c << 63);
+    }
+    if (u256_cmp(&u, &v) >= 0) {
+      u256_sub(&u, &u, &v);
+      if (u256_sub(&x1, &x1, &x2)) u256_add(&x1, &x1, m);
+    } else {
+      u256_sub(&v, &v, &u);
+      if (u256_sub(&x2, &x2, &x1)) u256_add(&x2, &x2, m);
+    }
+  }
+  *r = u256_cmp(&u, &one) == 0 ? x1 : x2;
+}
+
+static void gej_to_ge_bin(ge* r, const gej* a) {
+  if (a->inf) { r->inf = 1; return; }
+  fe zi, zi2, zi3;
+  modinv_binary(&zi, &a->z, &FP);
+  fe_sqr(&zi2, &zi); fe_mul(&zi3, &zi2, &zi);
+  fe_mul(&r->x, &a->x, &zi2); fe_mul(&r->y, &a->y, &zi3); r->inf = 0;
+}
+
+/* odd multiples (2i+1) P, i < n, made affine with one inversion (Montgomery's trick) */
+static void odd_multiples_affine(ge* out, const ge* P, int n) {
+  gej pj[64], d;
+  gej_set_ge(&pj[0], P);
+  gej_double(&d, &pj[0]);
+  ge d_aff;
+  gej_to_ge_bin(&d_aff, &d);
+  for (int i = 1; i < n; ++i) gej_add_ge(&pj[i], &pj[i - 1], &d_aff);
+  fe pre[64], inv, t;
+  pre[0] = pj[0].z;
+  for (int i = 1; i < n; ++i) fe_mul(&pre[i], &pre[i - 1], &pj[i].z);
+  modinv_binary(&inv, &pre[n - 1], &FP);
+  for (int i = n - 1; i >= 0; --i) {
+    fe zi, zi2, zi3;
+    if (i) { fe_mul(&zi, &inv, &pre[i - 1]); fe_mul(&inv, &inv, &pj[i].z); } else zi = inv;
+    fe_sqr(&zi2, &zi); fe_mul(&zi3, &zi2, &zi);
+    fe_mul(&out[i].x, &pj[i].x, &zi2); fe_mul(&out[i].y, &pj[i].y, &zi3); out[i].inf = 0;
+    (void)t;
+  }
+}
+
+#define GLV_WG 8
+static ge GTAB_GLV[1 << (GLV_WG - 2)], GTAB_GLV_L[1 << (GLV_WG - 2)];
+static pthread_once_t gtab_glv_once = PTHREAD_ONCE_INIT;
+static void build_gtab_glv(void) {
+  ge g = {GX, GY, 0};
+  odd_multiples_affine(GTAB_GLV, &g, 1 << (GLV_WG - 2));
+  for (int i = 0; i < (1 << (GLV_WG - 2)); ++i) {
+    fe_mul(&GTAB_GLV_L[i].x, &GTAB_GLV[i].x, &GLV_BETA);
+    GTAB_GLV_L[i].y = GTAB_GLV[i].y;
+    GTAB_GLV_L[i].inf = 0;
+  }
+}
+
+static void add_digit(gej* acc, const ge* tab, int d, int neg) {
+  if (!d) return;
+  ge e = tab[((d < 0 ? -d : d) - 1) >> 1];
+  if ((d < 0) != (neg != 0)) fe_neg(&e.y, &e.y);
+  gej_add_ge(acc, acc, &e);
+}
+
+/* r = a G + b P, GLV + wNAF (see above) */
+static void ecmult_glv(gej* r, const sc* a, const ge* P, const sc* b) {
+  pthread_once(&gtab_glv_once, build_gtab_glv);
+  sc a1, a2, b1, b2;
+  int na1, na2, nb1, nb2;
+  glv_split(a, &a1, &na1, &a2, &na2);
+  glv_split(b, &b1, &nb1, &b2, &nb2);
+  int da1[132], da2[132], db1[132], db2[132];
+  int la1 = wnaf(da1, &a1, GLV_WG), la2 = wnaf(da2, &a2, GLV_WG);
+  int lb1 = wnaf(db1, &b1, 5), lb2 = wnaf(db2, &b2, 5);
+  ge pt[8], ptl[8];
+  odd_multiples_affine(pt, P, 8);
+  for (int i = 0; i < 8; ++i) { fe_mul(&ptl[i].x, &pt[i].x, &GLV_BETA); ptl[i].y = pt[i].y; ptl[i].inf = 0; }
+  int len = la1;
+  if (la2 > len) len = la2;
+  if (lb1 > len) len = lb1;
+  if (lb2 > len) len = lb2;
+  gej acc;
+  acc.inf = 1;
+  for (int i = len - 1; i >= 0; --i) {
+    if (!acc.inf) gej_double(&acc, &acc);
+    add_digit(&acc, pt, db1[i], nb1);
+    add_digit(&acc, ptl, db2[i], nb2);
+    add_digit(&acc, GTAB_GLV, da1[i], na1);
+    add_digit(&acc, GTAB_GLV_L, da2[i], na2);
+  }
+  *r = acc;
+}
+
 /* ================================ ECDSA ======================================== */
 static void ge_to_address(const ge* q, u8 addr[20]) {
   u8 buf[64], h[32];
@@ -496,9 +683,10 @@ static long g_verify_failures = 0; /* post-recovery verify must never fail */
 long hlco_verify_failures(void) { return g_verify_failures; }
 
 /* alloy Signature::from_raw_array + recover_address_from_prehash (see pyoracle.ecrecover).
- * Returns HLC_SCHEME_* (0 = success, addr filled).  reverify != 0 also runs k256's
+ * Returns HLC_SCHEME_* (0 = success, addr filled).  flags & HLCO_REVERIFY also runs k256's
  * post-recovery verify_prehash, as upstream does (timed CPU baseline). */
-int hlco_ecrecover(const u8 prehash[32], const u8 sig[65], u8 addr[20], int reverify) {
+int hlco_ecrecover(const u8 prehash[32], const u8 sig[65], u8 addr[20], int flags) {
+  const int reverify = flags & HLCO_REVERIFY, glv = flags & HLCO_GLV;
   u8 v = sig[64];
   int parity;
   if (v == 0 || v == 27) parity = 0;
@@ -522,25 +710,25 @@ int hlco_ecrecover(const u8 prehash[32], const u8 sig[65], u8 addr[20], int reve
   if ((int)(y.v[0] & 1) != parity) fe_neg(&y, &y);
   ge R = {x, y, 0};
   sc rinv, u1, u2;
-  sc_inv(&rinv, &r);
+  if (glv) modinv_binary(&rinv, &r, &FN); else sc_inv(&rinv, &r);
   sc_mul(&u1, &z, &rinv); sc_neg(&u1, &u1);
   sc_mul(&u2, &s, &rinv);
   gej Qj;
-  ecmult(&Qj, &u1, &R, &u2);
+  if (glv) ecmult_glv(&Qj, &u1, &R, &u2); else ecmult(&Qj, &u1, &R, &u2);
   if (Qj.inf) return HLC_SCHEME_INFINITY;
   ge Q;
-  gej_to_ge(&Q, &Qj);
+  if (glv) gej_to_ge_bin(&Q, &Qj); else gej_to_ge(&Q, &Qj);
   if (reverify) {
     /* k256 verify_prehash: x(z/s G + r/s Q) mod n == r (low-s signature) */
     sc sinv, v1, v2;
-    sc_inv(&sinv, &s);
+    if (glv) modinv_binary(&sinv, &s, &FN); else sc_inv(&sinv, &s);
     sc_mul(&v1, &z, &sinv);
     sc_mul(&v2, &r, &sinv);
     gej Pj; ge Pa;
-    ecmult(&Pj, &v1, &Q, &v2);
+    if (glv) ecmult_glv(&Pj, &v1, &Q, &v2); else ecmult(&Pj, &v1, &Q, &v2);
     int ok = 0;
     if (!Pj.inf) {
-      gej_to_ge(&Pa, &Pj);
+      if (glv) gej_to_ge_bin(&Pa, &Pj); else gej_to_ge(&Pa, &Pj);
       sc xr = Pa.x;
       while (u256_cmp(&xr, &FN) >= 0) u256_sub(&xr, &xr, &FN);
       ok = u256_cmp(&xr, &r) == 0;
@@ -717,23 +905,23 @@ size_t hlco_encode_vote(const hlc_votes* vs, u64 i, u8* out) {
 
 /* EthereumConsensusSigner::verify (ethereum.rs:66-97) -> HLC_VERIFY_* / 1+HLC_SCHEME_* */
 static int eth_verify(const u8* id, u32 idlen, const u8* payload, size_t plen, const u8* sig,
-                      u32 siglen, u8 addr[20], int reverify) {
+                      u32 siglen, u8 addr[20], int flags) {
   if (siglen != 65) return 1 + HLC_SCHEME_SIG_LEN;
   if (idlen != 20) return 1 + HLC_SCHEME_ID_LEN;
   u8 h[32];
   eip191_hash(payload, plen, h);
-  int sub = hlco_ecrecover(h, sig, addr, reverify);
+  int sub = hlco_ecrecover(h, sig, addr, flags);
   if (sub) return 1 + sub;
   return memcmp(addr, id, 20) == 0 ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
 }
 
 int hlco_verify_batch(u64 n, const u8* bytes, const u64* id_off, const u32* id_len,
                       const u64* p_off, const u32* p_len, const u64* s_off, const u32* s_len,
-                      u8* out_status, u8* out_addr, int reverify) {
+                      u8* out_status, u8* out_addr, int flags) {
   for (u64 i = 0; i < n; ++i) {
     u8 addr[20] = {0};
     out_status[i] = (u8)eth_verify(bytes + id_off[i], id_len[i], bytes + p_off[i], p_len[i],
-                                   bytes + s_off[i], s_len[i], addr, reverify);
+                                   bytes + s_off[i], s_len[i], addr, flags);
     if (out_addr) memcpy(out_addr + 20 * i, addr, 20);
   }
   return 0;
@@ -741,7 +929,7 @@ int hlco_verify_batch(u64 n, const u8* bytes, const u64* id_off, const u32* id_l
 
 /* validate_vote (utils.rs:127-171) preceded by the proposal_id check (utils.rs:113-115) */
 static void validate_one(const hlc_votes* vs, u64 i, const hlc_proposal* p, u64 now, u8* st,
-                         u8* reason, u8 addr[20], int reverify) {
+                         u8* reason, u8 addr[20], int flags) {
   vview v;
   vote_view(vs, i, &v);
   *reason = 0;
@@ -760,7 +948,7 @@ static void validate_one(const hlc_votes* vs, u64 i, const hlc_proposal* p, u64 
   u8* enc = elen <= sizeof stackbuf ? stackbuf : (u8*)malloc(elen);
   encode_vote(&v, enc);
   int vr = eth_verify(v.f[HLC_F_OWNER], v.flen[HLC_F_OWNER], enc, elen, v.f[HLC_F_SIGNATURE],
-                      v.flen[HLC_F_SIGNATURE], addr, reverify);
+                      v.flen[HLC_F_SIGNATURE], addr, flags);
   if (enc != stackbuf) free(enc);
   if (vr >= 2) { *st = HLC_SIGNATURE_SCHEME; *reason = (u8)(vr - 1); return; }
   if (vr == HLC_VERIFY_FALSE) { *st = HLC_INVALID_VOTE_SIGNATURE; return; }
@@ -960,7 +1148,7 @@ typedef struct {
   u64 p0, p1, now;
   u8 *vst, *vreason, *rec;
   hlc_result* res;
-  int reverify;
+  int flags;
 } job;
 
 static void* worker(void* arg) {
@@ -970,7 +1158,7 @@ static void* worker(void* arg) {
     for (u32 j = 0; j < p->vote_count; ++j) {
       u64 i = p->vote_begin + j;
       u8 addr[20];
-      validate_one(jb->vs, i, p, jb->now, &jb->vst[i], &jb->vreason[i], addr, jb->reverify);
+      validate_one(jb->vs, i, p, jb->now, &jb->vst[i], &jb->vreason[i], addr, jb->flags);
       if (jb->rec) memcpy(jb->rec + 20 * i, addr, 20);
     }
     if (jb->res) finish_proposal(jb->vs, p, jb->now, jb->vst, jb->vreason, &jb->res[pi]);
@@ -979,10 +1167,11 @@ static void* worker(void* arg) {
 }
 
 /* Same contract as hlc_validate_proposals (include/hlc.h); vote_status / vote_reason are
- * required here.  threads <= 1 runs inline.  reverify: also run k256's verify_prehash. */
+ * required here.  threads <= 1 runs inline.  flags: HLCO_REVERIFY (also run k256's verify_prehash),
+ * HLCO_GLV (the k256-class recovery instead of the non-GLV checker). */
 int hlco_validate_proposals(const hlc_votes* vs, const hlc_proposal* ps, u64 np, u64 now,
                             hlc_result* res, u8* vst, u8* vreason, u8* rec, int threads,
-                            int reverify) {
+                            int flags) {
   if (threads < 1) threads = 1;
   if ((u64)threads > np) threads = np ? (int)np : 1;
   /* balance by vote count */
@@ -993,7 +1182,7 @@ int hlco_validate_proposals(const hlc_votes* vs, const hlc_proposal* ps, u64 np,
   u64 pi = 0;
   for (int t = 0; t < threads; ++t) {
     u64 target = total * (u64)(t + 1) / (u64)threads, acc = 0;
-    jobs[t] = (job){vs, ps, pi, pi, now, vst, vreason, rec, res, reverify};
+    jobs[t] = (job){vs, ps, pi, pi, now, vst, vreason, rec, res, flags};
     if (t == threads - 1) jobs[t].p1 = np;
     else {
       u64 done = 0;
@@ -1016,14 +1205,14 @@ int hlco_validate_proposals(const hlc_votes* vs, const hlc_proposal* ps, u64 np,
 }
 
 /* validate_vote-only timing loop for the CPU baseline: votes [v0, v1) against proposal p */
-typedef struct { const hlc_votes* vs; const hlc_proposal* ps; u64 p0, p1, now; int reverify; u64 ok; } vjob;
+typedef struct { const hlc_votes* vs; const hlc_proposal* ps; u64 p0, p1, now; int flags; u64 ok; } vjob;
 static void* vworker(void* arg) {
   vjob* jb = (vjob*)arg;
   for (u64 pi = jb->p0; pi < jb->p1; ++pi) {
     const hlc_proposal* p = &jb->ps[pi];
     for (u32 j = 0; j < p->vote_count; ++j) {
       u8 st, rs, addr[20];
-      validate_one(jb->vs, p->vote_begin + j, p, jb->now, &st, &rs, addr, jb->reverify);
+      validate_one(jb->vs, p->vote_begin + j, p, jb->now, &st, &rs, addr, jb->flags);
       jb->ok += st == HLC_OK;
     }
   }
@@ -1033,12 +1222,12 @@ static void* vworker(void* arg) {
 /* Times nothing itself: runs validate_vote over every vote of proposals [0, np) on
  * `threads` threads (static split by proposal) and returns how many were OK. */
 u64 hlco_validate_votes_only(const hlc_votes* vs, const hlc_proposal* ps, u64 np, u64 now,
-                             int threads, int reverify) {
+                             int threads, int flags) {
   if (threads < 1) threads = 1;
   vjob* jobs = (vjob*)calloc((size_t)threads, sizeof(vjob));
   pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
   for (int t = 0; t < threads; ++t)
-    jobs[t] = (vjob){vs, ps, np * (u64)t / (u64)threads, np * (u64)(t + 1) / (u64)threads, now, reverify, 0};
+    jobs[t] = (vjob){vs, ps, np * (u64)t / (u64)threads, np * (u64)(t + 1) / (u64)threads, now, flags, 0};
   for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, vworker, &jobs[t]);
   u64 ok = 0;
   for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); ok += jobs[t].ok; }

@@ -96,3 +96,17 @@ def test_valid_items_recover_the_signer(ec, items):
             continue
         code, pub = ec.recover(it.prehash, it.sig)
         assert code == 0 and pub == ec.pubkey(it.priv.to_bytes(32, "big"))
+
+
+def test_glv_baseline_matches_checker_and_openssl(ec, items):
+    """The k256-class recovery the CPU baseline times (GLV + wNAF + binary-GCD inversions,
+    coracle glv=True) equals the independent non-GLV checker and OpenSSL on every item, and its
+    post-recovery verify (k256's verify_prehash) never fails."""
+    before = coracle.verify_failures()
+    for it in items[:4000]:
+        code_g, addr_g = coracle.ecrecover(it.prehash, it.sig, reverify=True, glv=True)
+        code_c, addr_c = coracle.ecrecover(it.prehash, it.sig, reverify=False)
+        assert (code_g, addr_g) == (code_c, addr_c), it.kind
+        code_o, pub = ec.recover(it.prehash, it.sig)
+        assert code_g == code_o and (code_o != 0 or coracle.keccak256(pub)[12:] == addr_g), it.kind
+    assert coracle.verify_failures() == before

@@ -8,7 +8,7 @@ tail -1 gpurun_out/ab_parity.log
 for round in 1 2; do
   for v in default "$@"; do
     LIB=""; [ $v != default ] && LIB=$PWD/hashgraph-like-consensus_amd/lib/variants/libhlc_$v.so
-    HLC_LIB=$LIB timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config3 --no-wire --no-stream > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { tail gpurun_out/ab_$v.err; exit 1; }
+    HLC_LIB=$LIB timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { tail gpurun_out/ab_$v.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('$round $v', round(d['value']), 'votes/s rec_ms', round(d['roofline']['kernel_ms_avg'],3))"
   done
 done

@@ -1,0 +1,63 @@
+"""The host-buffer entry hlc_validate_proposals (what the Rust process_incoming_proposals of
+INTEGRATION.md calls) on the config-2 workload, one-shot vs pipelined (GPU box).
+
+The pipeline chunk size is read from HLC_PIPE_CHUNK_VOTES on every call (0 = one-shot).  For each
+setting: outputs equal the one-shot outputs bit for bit, then --steps calls are timed (host buffers
+in, per-vote statuses + per-proposal results out, blocking).
+
+    python tools/host_pipe.py --steps 10 --chunks 0,65536,131072,262144
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--chunks", default="0,65536,131072,262144")
+    ap.add_argument("--proposals", type=int, default=10_000)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from hashgraph_like_consensus import synth
+    from hashgraph_like_consensus.device import DeviceBatch
+    from hashgraph_like_consensus.engine import Engine
+
+    eng = Engine(0)
+    db = DeviceBatch.synthetic(eng, a.proposals, 64, 64, True, synth.config_seed(2))
+    b, d, _ = db.to_host()
+    torch.cuda.synchronize()
+    bytes_in = int(b.arena.nbytes + b.vote_id.nbytes + b.proposal_id.nbytes + b.timestamp.nbytes + b.vote.nbytes
+                   + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
+    ref = None
+    out = []
+    for c in [int(x) for x in a.chunks.split(",")]:
+        os.environ["HLC_PIPE_CHUNK_VOTES"] = str(c)
+        r = eng.validate_proposals(b, d, db.now, want_votes=True)
+        if ref is None:
+            ref = r
+            assert (r[1] == 0).all() and (r[0]["status"] == 0).all()
+        assert np.array_equal(r[0], ref[0]) and np.array_equal(r[1], ref[1]) and np.array_equal(r[2], ref[2])
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            eng.validate_proposals(b, d, db.now, want_votes=True)
+        el = (time.perf_counter() - t) / a.steps
+        row = {"chunk_votes": c, "ms_per_call": el * 1e3, "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in,
+               "outputs_equal_one_shot": True}
+        print(json.dumps(row), flush=True)
+        out.append(row)
+    eng.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -8,7 +8,7 @@ set -o pipefail
 TAG=${1:-r03}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p $OUT
-LEGS="--no-cpu-baseline --no-config3 --no-wire --no-stream --no-e2e"
+LEGS="--no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e"
 BENCH="$PWD/bench.py --steps 20 --warmup 5 $LEGS"
 PBENCH="$PWD/bench.py --steps 3 --warmup 1 $LEGS"
 cd /tmp && export TMPDIR=/tmp
