@@ -93,46 +93,86 @@ def pmc_traffic():
     return tot
 
 
-def valu_figures(votes: int):
-    """Measured VALU figures of k_rec_main from the committed PMC pass: lane-instructions per vote,
-    and the issue fraction = SQ_INSTS_VALU per SIMD x the hot point operations' measured issue
-    cycles per instruction (tools/ubench_field.hip, roofline.json) / the kernel's own cycles
-    (GRBM_GUI_ACTIVE per XCD) -- clock-independent; the kernel's sustained clock is given beside."""
+VALU_PEAK_LANE_OPS = ROOFLINE["peak"]["valu_lane_ops_T_per_s"]
+
+
+def valu_figures():
+    """Hardware VALU figures of the recovery from the committed profile of this bench command
+    (one build, one box): per kernel SQ_INSTS_VALU (PMC pass) x 64 lanes / its kernel-trace
+    duration, against the guide's VALU issue peak (256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz =
+    78.6 T lane-ops/s) -- `valu_lane_op_frac`, the figure the north star asks for; the issue
+    fraction (SQ_INSTS_VALU per SIMD x the chain's measured 4.03 cycles per instruction over the
+    kernel's GRBM cycles, both from the same PMC pass); and the clocks (PMC pass, in-kernel)."""
     insts = {k: pmc_per_launch("pmc_valu", "SQ_INSTS_VALU", k) for k in REC_KERNELS}
     grbm = pmc_per_launch("pmc_valu", "GRBM_GUI_ACTIVE", "k_rec_main")
-    dur = pmc_duration_ms("pmc_valu", "k_rec_main")
-    if insts["k_rec_main"] is None or not grbm or not dur:
+    dur_pmc = pmc_duration_ms("pmc_valu", "k_rec_main")
+    tr = rocprof_kernel_ms()
+    if insts["k_rec_main"] is None or not grbm or not dur_pmc or not tr:
         return None
     hot = ROOFLINE["implementation"]["hot_op_issue"]
     simds, xcds = 256 * 4, 8
     cycles = grbm / xcds
     issue = insts["k_rec_main"] / simds * hot["cycles_per_wave_instruction"]
     pv = ROOFLINE["profile_votes_per_launch"]
+    main_ms = tr["k_rec_main"]
+    rate = insts["k_rec_main"] * 64.0 / (main_ms * 1e-3) / 1e12
+    rec_insts = sum(v for v in insts.values() if v is not None)
+    clk = ROOFLINE.get("measured_clock", {})
     return {
         "valu_instr_per_vote": {k: v * 64.0 / pv for k, v in insts.items() if v is not None},
+        "valu_lane_op_rate_T": rate,
+        "valu_lane_op_frac": rate / VALU_PEAK_LANE_OPS,
+        "valu_lane_op_frac_basis": (f"k_rec_main: SQ_INSTS_VALU {insts['k_rec_main']:.4g} wave-instructions/launch "
+                                    f"x 64 / {main_ms:.3f} ms (kernel-trace average of the timed steps) / "
+                                    f"{VALU_PEAK_LANE_OPS} T lane-ops/s ({ROOFLINE['peak']['valu_basis']})"),
+        "recovery_valu_instr_per_launch": rec_insts,
         "valu_issue_frac": issue / cycles,
-        "kernel_sclk_GHz": cycles / (dur * 1e6),
-        "valu_issue_basis": (f"k_rec_main: SQ_INSTS_VALU {insts['k_rec_main']:.4g}/launch / {simds} SIMDs x "
-                             f"{hot['cycles_per_wave_instruction']} cycles/instruction ({hot['source']}) / "
-                             f"{cycles:.4g} cycles (GRBM_GUI_ACTIVE per XCD, {dur:.3f} ms under PMC, "
-                             f"{os.path.relpath(PMC_PROFILE, ROOT)})"),
+        "pmc_pass_sclk_GHz": cycles / (dur_pmc * 1e6),
+        "in_kernel_sclk_GHz": clk.get("k_rec_main_GHz"),
+        "clock_ceiling_GHz": clk.get("point_op_loop_GHz"),
+        "clock_source": clk.get("source"),
+        "valu_issue_basis": (f"k_rec_main: SQ_INSTS_VALU / {simds} SIMDs x {hot['cycles_per_wave_instruction']} "
+                             f"cycles/instruction ({hot['source']}) / {cycles:.4g} cycles (GRBM_GUI_ACTIVE per XCD, "
+                             f"{dur_pmc:.3f} ms under PMC: profiled passes run at a lower clock, hence the separate "
+                             f"in-kernel clock)"),
     }
 
 
 def rocprof_kernel_ms():
-    """Average durations (ms) of the recovery kernels in the committed kernel-trace summary."""
+    """Average durations (ms) of the recovery kernels over the timed steps of the committed
+    kernel trace of this bench command (the last 20 validate-many calls), their serial-chain sum
+    (prep -> main -> comb -> final -> addr run one after another) and the traced step period."""
     import csv
-    path = os.path.join(PMC_PROFILE, "trace", "run_kernel_stats.csv")
+    import re
+    import statistics
+    path = os.path.join(PMC_PROFILE, "trace", "run_kernel_trace.csv")
     if not os.path.exists(path):
         return None
-    out = {}
+    rows = []
     with open(path, newline="") as f:
         for r in csv.DictReader(f):
-            for k in REC_KERNELS:
-                if f"::{k}(" in r["Name"]:
-                    out[k] = float(r["AverageNs"]) / 1e6
-    if len(out) == len(REC_KERNELS):
-        out["sum"] = sum(out[k] for k in REC_KERNELS)
+            m = re.search(r"::(k_\w+)\(", r["Kernel_Name"])
+            if m:
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1)))
+    rows.sort()
+    starts = [i for i, r in enumerate(rows) if r[2] == "k_rec_prep"]
+    calls = []
+    for ci, i0 in enumerate(starts):
+        seg = rows[i0:starts[ci + 1] if ci + 1 < len(starts) else len(rows)]
+        first = {}
+        for t0, t1, k in seg:
+            first.setdefault(k, (t0, t1))
+        if all(k in first for k in REC_KERNELS):
+            calls.append({k: (first[k][1] - first[k][0]) / 1e6 for k in REC_KERNELS} | {"_t0": first["k_rec_prep"][0]})
+    calls = calls[-20:]
+    if not calls:
+        return None
+    out = {k: statistics.mean(c[k] for c in calls) for k in REC_KERNELS}
+    out["serial_chain_sum"] = sum(out[k] for k in REC_KERNELS)
+    out["traced_step_period"] = (statistics.mean((calls[i + 1]["_t0"] - calls[i]["_t0"]) / 1e6
+                                                 for i in range(len(calls) - 1)) if len(calls) > 1 else None)
+    out["calls"] = len(calls)
+    out["source"] = os.path.relpath(path, ROOT)
     return out
 
 
@@ -535,7 +575,7 @@ def main() -> int:
     # results all-gathered over RCCL plus an all_reduce(sum) of the verified / rejected-by-code
     # counters; at N = 1 only the local counters
     from hashgraph_like_consensus.parallel import ShardExchange
-    ex = ShardExchange(max_p, world, coll_dev)
+    ex = ShardExchange(max_p, world, coll_dev, engine=eng)
 
     def step():
         eng.validate_proposals_device(db, handle)
@@ -595,7 +635,8 @@ def main() -> int:
     rec_avg_s = rec_ms / max(rec_n, 1) / 1e3
     achieved = W_LIMB_PRODUCTS_PER_VOTE * db.n / rec_avg_s / 1e12
     traffic = pmc_traffic()
-    valu = valu_figures(db.n)
+    valu = valu_figures()
+    rk = rocprof_kernel_ms()
     chain_avg_s = chain_ms / max(chain_n, 1) / 1e3
     ct = ROOFLINE["chain_tally"]
     chain_bytes = ct["bytes_per_vote"] * db.n + ct["bytes_per_proposal"] * P
@@ -638,6 +679,15 @@ def main() -> int:
             "peak": MAD_PEAK_T_PER_S,
             "unit": "T limb-products/s (32x32->64, v_mad_u64_u32)",
             "frac": achieved / MAD_PEAK_T_PER_S,
+            "frac_basis": ("algorithmic: W limb products per vote x votes / the live recovery bracket / the "
+                           "limb-product issue ceiling (roofline.json peak.basis); the hardware figure is "
+                           "valu_lane_op_frac"),
+            "frac_rocprof_chain": (W_LIMB_PRODUCTS_PER_VOTE * ROOFLINE["profile_votes_per_launch"]
+                                   / (rk["serial_chain_sum"] * 1e-3) / 1e12 / MAD_PEAK_T_PER_S) if rk else None,
+            "valu_lane_op_frac": valu["valu_lane_op_frac"] if valu else None,
+            "valu_lane_op_rate_T": valu["valu_lane_op_rate_T"] if valu else None,
+            "valu_lane_op_frac_basis": valu["valu_lane_op_frac_basis"] if valu else None,
+            "valu_peak_lane_ops_T": VALU_PEAK_LANE_OPS,
             # per launch of THIS run: the profiled bytes per vote x this launch's votes
             "traffic": traffic["bytes"] / ROOFLINE["profile_votes_per_launch"] * db.n if traffic else None,
             "traffic_per_vote": traffic["bytes"] / ROOFLINE["profile_votes_per_launch"] if traffic else None,
@@ -649,10 +699,13 @@ def main() -> int:
             "valu_instr_per_vote": valu["valu_instr_per_vote"] if valu else None,
             "valu_issue_frac": valu["valu_issue_frac"] if valu else None,
             "valu_issue_basis": valu["valu_issue_basis"] if valu else None,
-            "kernel_sclk_GHz": valu["kernel_sclk_GHz"] if valu else None,
+            "pmc_pass_sclk_GHz": valu["pmc_pass_sclk_GHz"] if valu else None,
+            "in_kernel_sclk_GHz": valu["in_kernel_sclk_GHz"] if valu else None,
+            "clock_ceiling_GHz": valu["clock_ceiling_GHz"] if valu else None,
+            "clock_source": valu["clock_source"] if valu else None,
             "kernel_ms_avg": rec_avg_s * 1e3,
             "kernel_launches": rec_n,
-            "rocprof_kernel_ms": rocprof_kernel_ms(),
+            "rocprof_kernel_ms": rk,
             "call_ms_avg": call_ms / max(calls, 1),
             "kernel_share_of_step": rec_ms / max(call_ms, 1e-9),
         },

@@ -3,11 +3,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hlc.h"
@@ -65,6 +69,86 @@ struct DBuf {
   }
 };
 
+// Page-locked host memory (the pipeline's staging buffers: DMA runs asynchronously from it).
+struct PBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~PBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = bytes + bytes / 4 + 4096;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return set_err(HLC_ENOMEM, std::string("hipHostMalloc failed: ") + hipGetErrorString(e));
+    }
+    cap = want;
+    return 0;
+  }
+  uint8_t* at(size_t off) const { return static_cast<uint8_t*>(p) + off; }
+};
+
+// A small host worker pool for the pipeline's field checks and staging copies: run(fn) calls
+// fn(part, parts) for every part on the workers and the calling thread and returns when all are done.
+class HostPool {
+ public:
+  explicit HostPool(int workers) {
+    for (int i = 0; i < workers; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int parts() const { return (int)th_.size() + 1; }
+  void run(const std::function<void(int, int)>& fn) {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      fn_ = &fn;
+      pending_ = (int)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0, parts());
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [&] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop(int part) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int, int)>* f;
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = fn_;
+      }
+      (*f)(part, parts());
+      std::lock_guard<std::mutex> l(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int, int)>* fn_ = nullptr;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 struct hlc_ctx {
@@ -81,6 +165,14 @@ struct hlc_ctx {
   // fixed-base tables) that take alternate proposal chunks, so one chunk's host->device copy and
   // the next chunk's kernels overlap the previous chunk's kernels (created on first use)
   hlc_ctx* pipe[2] = {nullptr, nullptr};
+  std::unique_ptr<HostPool> pool;  // the parent's staging workers (HLC_PIPE_THREADS)
+  // a pipeline child's staging: page-locked inputs / outputs, one device input buffer, the event
+  // after its chunk's output copy, and which chunk it holds
+  PBuf pin_in, pin_out;
+  DBuf dev_in;
+  hipEvent_t ev_done = nullptr;
+  bool busy = false;
+  uint64_t chunk_p0 = 0, chunk_p1 = 0, chunk_v0 = 0, chunk_v1 = 0;
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
   DBuf in_off2, in_len2, in_off3, in_len3, in_priv, byz_key;
@@ -106,6 +198,7 @@ struct hlc_ctx {
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : rec_prep_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    if (ev_done) (void)hipEventDestroy(ev_done);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -533,22 +626,6 @@ int stage_votes(hlc_ctx* c, const hlc_votes* v, hlc_votes* dv, hipStream_t s) {
   return 0;
 }
 
-// Pointer/field checks of votes [v0, v1) (check_votes_host's rule) and the arena span they use.
-int check_vote_range(const hlc_votes* v, uint64_t v0, uint64_t v1, uint64_t* a_lo, uint64_t* a_hi) {
-  uint64_t lo = UINT64_MAX, hi = 0;
-  for (uint64_t i = v0 * HLC_NFIELDS; i < v1 * HLC_NFIELDS; ++i) {
-    const uint64_t off = v->field_off[i], len = v->field_len[i];
-    if (!len) continue;
-    if (!v->bytes || off + len > v->bytes_len || off + len < off)
-      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-    lo = std::min(lo, off);
-    hi = std::max(hi, off + len);
-  }
-  *a_lo = lo == UINT64_MAX ? 0 : lo;
-  *a_hi = lo == UINT64_MAX ? 0 : hi;
-  return 0;
-}
-
 int make_child(hlc_ctx* parent, hlc_ctx** out) {
   hlc_ctx* c = new hlc_ctx();
   c->device = parent->device;
@@ -557,7 +634,8 @@ int make_child(hlc_ctx* parent, hlc_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess) {
     hipStream_t st = c->stream, ax = c->aux;
     delete c;
     if (st) (void)hipStreamDestroy(st);
@@ -593,13 +671,26 @@ struct Chunk {
   uint64_t p0, p1, v0, v1;
 };
 
+// Staging workers of the pipeline (HLC_PIPE_THREADS, default 4, including the calling thread).
+int pipe_threads() {
+  const char* e = std::getenv("HLC_PIPE_THREADS");
+  const int t = e ? std::atoi(e) : 4;
+  return std::max(1, std::min(t, 64));
+}
+
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 // hlc_validate_proposals over host buffers, pipelined: the proposals are cut into chunks of about
-// pipe_chunk_votes() votes (contiguous proposal ranges whose vote ranges are disjoint and in
-// order -- the layout of prost-decoded / packed batches; any other layout returns *used = false and
-// takes the one-shot path).  Chunk k runs on child context pipe[k % 2]: the host checks chunk k's
-// fields and copies its SoA slices + arena span in while chunk k-1's kernels run on the other
-// child, then launches chunk k, then copies chunk k-1's outputs back.  Chunks on the two children
-// also overlap on the device (the next chunk's blocks fill the previous one's grid tail).
+// pipe_chunk_votes() votes (contiguous proposal ranges whose vote ranges are disjoint and in order --
+// the layout of prost-decoded / packed batches; any other layout returns *used = false and takes the
+// one-shot path).  Chunk k runs on child context pipe[k % 2] (own streams and workspace):
+//   host   : wait for the child's previous chunk (k-2) and copy its outputs out of page-locked
+//            memory; check chunk k's fields and copy its SoA slices, proposals and arena span into
+//            the child's page-locked staging buffer (the pool's threads);
+//   device : one H2D DMA of the staging buffer, the validate-many kernels, the outputs' D2H into
+//            page-locked memory, an event -- all asynchronous on the child's stream.
+// So while the host stages chunk k, the device runs chunk k-1 (and chunk k-2's tail): copies,
+// checks and kernels overlap, and the two children's grids fill each other's tails.
 int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
                        hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec, bool* used) {
   *used = false;
@@ -630,64 +721,142 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
   if (ch.size() < 2) return 0;
   for (int k = 0; k < 2; ++k)
     if (!c->pipe[k]) CHK(make_child(c, &c->pipe[k]));
+  if (!c->pool || c->pool->parts() != pipe_threads()) c->pool.reset(new HostPool(pipe_threads() - 1));
+  HostPool& pool = *c->pool;
   *used = true;
-  std::vector<hlc_proposal> cp;
-  auto finish = [&](size_t k) -> int {
-    hlc_ctx* w = c->pipe[k & 1];
-    const Chunk& q = ch[k];
-    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
-    hipStream_t s = w->stream;
-    if (npk)
-      HIPCHK(hipMemcpyAsync(out_res + q.p0, w->out_res.p, npk * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
-    if (out_st && nv) HIPCHK(hipMemcpyAsync(out_st + q.v0, w->out_status.p, nv, hipMemcpyDeviceToHost, s));
-    if (out_rs && nv) HIPCHK(hipMemcpyAsync(out_rs + q.v0, w->out_reason.p, nv, hipMemcpyDeviceToHost, s));
-    if (out_rec && nv) HIPCHK(hipMemcpyAsync(out_rec + 20 * q.v0, w->out_rec.p, nv * 20, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+
+  // output layout in a child's pin_out: results | status | reason | recovered
+  auto out_layout = [&](uint64_t nv, uint64_t npk, size_t o[4]) {
+    o[0] = 0;
+    o[1] = al256(npk * sizeof(hlc_result));
+    o[2] = o[1] + al256(nv);
+    o[3] = o[2] + al256(nv);
+    return o[3] + (out_rec ? nv * 20 : 0);
+  };
+  auto copy_out = [&](hlc_ctx* w) -> int {
+    if (!w->busy) return 0;
+    HIPCHK(hipEventSynchronize(w->ev_done));
+    w->busy = false;
+    const uint64_t nv = w->chunk_v1 - w->chunk_v0, npk = w->chunk_p1 - w->chunk_p0;
+    size_t o[4];
+    out_layout(nv, npk, o);
+    std::memcpy(out_res + w->chunk_p0, w->pin_out.at(o[0]), npk * sizeof(hlc_result));
+    if (out_st) std::memcpy(out_st + w->chunk_v0, w->pin_out.at(o[1]), nv);
+    if (out_rs) std::memcpy(out_rs + w->chunk_v0, w->pin_out.at(o[2]), nv);
+    if (out_rec) std::memcpy(out_rec + 20 * w->chunk_v0, w->pin_out.at(o[3]), nv * 20);
     return 0;
   };
   auto drain = [&]() {
-    for (int k = 0; k < 2; ++k) (void)hipStreamSynchronize(c->pipe[k]->stream);
+    for (int k = 0; k < 2; ++k) {
+      (void)hipStreamSynchronize(c->pipe[k]->stream);
+      c->pipe[k]->busy = false;
+    }
   };
+  std::vector<hlc_proposal> cp;
   for (size_t k = 0; k < ch.size(); ++k) {
     hlc_ctx* w = c->pipe[k & 1];
+    CHK(copy_out(w));  // its previous chunk (k - 2): also frees its staging buffers
     const Chunk& q = ch[k];
-    uint64_t a_lo = 0, a_hi = 0, g_lo = 0, g_hi = 0;
-    // the chunk's votes, and (same rule as the one-shot path) the uncovered votes before it
-    int rc = check_vote_range(v, k ? ch[k - 1].v1 : 0, q.v0, &g_lo, &g_hi);
-    if (!rc) rc = check_vote_range(v, q.v0, q.v1, &a_lo, &a_hi);
-    if (!rc && k + 1 == ch.size()) rc = check_vote_range(v, q.v1, n, &g_lo, &g_hi);
-    if (rc) {
-      drain();
-      return rc;
-    }
-    hipStream_t s = w->stream;
     const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
-    hlc_votes hv;
-    hv.n = nv;
-    hv.vote_id = v->vote_id + q.v0;
-    hv.proposal_id = v->proposal_id + q.v0;
-    hv.timestamp = v->timestamp + q.v0;
-    hv.vote = v->vote + q.v0;
-    hv.field_off = v->field_off + q.v0 * HLC_NFIELDS;
-    hv.field_len = v->field_len + q.v0 * HLC_NFIELDS;
-    hv.bytes = v->bytes ? v->bytes + a_lo : nullptr;
-    hv.bytes_len = a_hi - a_lo;
-    hlc_votes dv;
-    CHK(stage_votes(w, &hv, &dv, s));
-    dv.bytes -= a_lo;  // the field offsets stay absolute: bytes + off lands in the staged span
+    // field checks of the chunk's votes and of the uncovered votes before it (the one-shot path's
+    // rule), and the arena span of the chunk's votes, on the pool
+    const uint64_t g0 = k ? ch[k - 1].v1 : 0, g1 = k + 1 == ch.size() ? n : q.v1;
+    const int parts = pool.parts();
+    std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
+    std::vector<int> bad(parts, 0);
+    pool.run([&](int t, int T) {
+      const uint64_t a0 = g0 + (g1 - g0) * t / T, a1 = g0 + (g1 - g0) * (t + 1) / T;
+      uint64_t l = UINT64_MAX, h = 0;
+      for (uint64_t i = a0 * HLC_NFIELDS; i < a1 * HLC_NFIELDS; ++i) {
+        const uint64_t off = v->field_off[i], len = v->field_len[i];
+        if (!len) continue;
+        if (!v->bytes || off + len > v->bytes_len || off + len < off) {
+          bad[t] = 1;
+          return;
+        }
+        const uint64_t vi = i / HLC_NFIELDS;
+        if (vi >= q.v0 && vi < q.v1) {
+          l = std::min(l, off);
+          h = std::max(h, off + len);
+        }
+      }
+      lo[t] = l;
+      hi[t] = h;
+    });
+    uint64_t a_lo = UINT64_MAX, a_hi = 0;
+    for (int t = 0; t < parts; ++t) {
+      if (bad[t]) {
+        drain();
+        return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+      }
+      a_lo = std::min(a_lo, lo[t]);
+      a_hi = std::max(a_hi, hi[t]);
+    }
+    if (a_lo == UINT64_MAX) a_lo = a_hi = 0;
+    // input layout: vote_id | proposal_id | timestamp | vote | field_off | field_len | props | arena
+    size_t o[9];
+    o[0] = 0;
+    o[1] = o[0] + al256(nv * 4);
+    o[2] = o[1] + al256(nv * 4);
+    o[3] = o[2] + al256(nv * 8);
+    o[4] = o[3] + al256(nv);
+    o[5] = o[4] + al256(nv * 8 * HLC_NFIELDS);
+    o[6] = o[5] + al256(nv * 4 * HLC_NFIELDS);
+    o[7] = o[6] + al256(npk * sizeof(hlc_proposal));
+    o[8] = o[7] + (a_hi - a_lo);
+    CHK(w->pin_in.ensure(o[8] + 16));
+    CHK(w->dev_in.ensure(o[8] + 16));
+    size_t oo[4];
+    CHK(w->pin_out.ensure(out_layout(nv, npk, oo) + 16));
     cp.assign(props + q.p0, props + q.p1);
     for (auto& pr : cp) pr.vote_begin = pr.vote_count ? pr.vote_begin - q.v0 : 0;
-    CHK(upload(w->in_props, cp.data(), npk, s));
+    std::memcpy(w->pin_in.at(o[6]), cp.data(), npk * sizeof(hlc_proposal));
+    const uint64_t arena = a_hi - a_lo;
+    pool.run([&](int t, int T) {
+      const uint64_t b0 = q.v0 + nv * t / T, b1 = q.v0 + nv * (t + 1) / T, m = b1 - b0, r = b0 - q.v0;
+      std::memcpy(w->pin_in.at(o[0] + 4 * r), v->vote_id + b0, 4 * m);
+      std::memcpy(w->pin_in.at(o[1] + 4 * r), v->proposal_id + b0, 4 * m);
+      std::memcpy(w->pin_in.at(o[2] + 8 * r), v->timestamp + b0, 8 * m);
+      std::memcpy(w->pin_in.at(o[3] + r), v->vote + b0, m);
+      std::memcpy(w->pin_in.at(o[4] + 8 * HLC_NFIELDS * r), v->field_off + HLC_NFIELDS * b0, 8 * HLC_NFIELDS * m);
+      std::memcpy(w->pin_in.at(o[5] + 4 * HLC_NFIELDS * r), v->field_len + HLC_NFIELDS * b0, 4 * HLC_NFIELDS * m);
+      const uint64_t c0 = arena * t / T, c1 = arena * (t + 1) / T;
+      if (c1 > c0) std::memcpy(w->pin_in.at(o[7] + c0), v->bytes + a_lo + c0, c1 - c0);
+    });
+    hipStream_t s = w->stream;
+    HIPCHK(hipMemcpyAsync(w->dev_in.p, w->pin_in.p, o[8], hipMemcpyHostToDevice, s));
+    uint8_t* d = w->dev_in.as<uint8_t>();
+    hlc_votes dv;
+    dv.n = nv;
+    dv.vote_id = reinterpret_cast<const uint32_t*>(d + o[0]);
+    dv.proposal_id = reinterpret_cast<const uint32_t*>(d + o[1]);
+    dv.timestamp = reinterpret_cast<const uint64_t*>(d + o[2]);
+    dv.vote = d + o[3];
+    dv.field_off = reinterpret_cast<const uint64_t*>(d + o[4]);
+    dv.field_len = reinterpret_cast<const uint32_t*>(d + o[5]);
+    dv.bytes = d + o[7] - a_lo;  // the field offsets stay absolute: bytes + off lands in the staged span
+    dv.bytes_len = a_hi;
     CHK(w->out_res.ensure(npk * sizeof(hlc_result) + 16));
     CHK(w->out_status.ensure(nv + 1));
     CHK(w->out_reason.ensure(nv + 1));
     if (out_rec) CHK(w->out_rec.ensure(nv * 20 + 20));
-    CHK(validate_device(w, &dv, w->in_props.as<hlc_proposal>(), npk, now, w->out_res.as<hlc_result>(),
+    CHK(validate_device(w, &dv, reinterpret_cast<const hlc_proposal*>(d + o[6]), npk, now, w->out_res.as<hlc_result>(),
                         w->out_status.as<uint8_t>(), w->out_reason.as<uint8_t>(),
                         out_rec ? w->out_rec.as<uint8_t>() : nullptr, s));
-    if (k) CHK(finish(k - 1));
+    if (npk) HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[0]), w->out_res.p, npk * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
+    if (nv) {
+      HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[1]), w->out_status.p, nv, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[2]), w->out_reason.p, nv, hipMemcpyDeviceToHost, s));
+      if (out_rec) HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[3]), w->out_rec.p, nv * 20, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipEventRecord(w->ev_done, s));
+    w->busy = true;
+    w->chunk_p0 = q.p0;
+    w->chunk_p1 = q.p1;
+    w->chunk_v0 = q.v0;
+    w->chunk_v1 = q.v1;
   }
-  CHK(finish(ch.size() - 1));
+  for (size_t k = ch.size(); k < ch.size() + 2; ++k) CHK(copy_out(c->pipe[k & 1]));
   // votes between the chunks' ranges are covered by no proposal: not evaluated (as the one-shot path)
   uint64_t prev = 0;
   for (size_t k = 0; k <= ch.size(); ++k) {
@@ -863,6 +1032,21 @@ int hlc_validate_proposals_device(hlc_ctx* ctx, const hlc_votes* votes, const hl
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
   return validate_device(ctx, votes, proposals, n_proposals, now, out_results, out_vote_status, out_vote_reason,
                          out_recovered, s);
+}
+
+int hlc_outcome_counts_device(hlc_ctx* ctx, const uint8_t* vote_status, uint64_t n_votes,
+                              const hlc_result* results, uint64_t n_proposals, uint64_t* out_counts,
+                              void* stream) {
+  if (!ctx || !out_counts || (n_votes && !vote_status) || (n_proposals && !results))
+    return set_err(HLC_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  HIPCHK(hipMemsetAsync(out_counts, 0, 64 * sizeof(uint64_t), s));
+  hlc::launch_outcome_hist(vote_status, n_votes, results, n_proposals,
+                           reinterpret_cast<unsigned long long*>(out_counts), s);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,

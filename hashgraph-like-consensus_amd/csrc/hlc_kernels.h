@@ -107,6 +107,9 @@ void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state,
 // (which runs on the context's second stream), after launch_red_init.
 void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint8_t* chain_code,
                         uint32_t* red, hipStream_t s);
+// outcome counters: bins[0..31] += votes by status, bins[32..63] += proposals by status
+void launch_outcome_hist(const uint8_t* vote_status, uint64_t n, const hlc_result* res, uint64_t np,
+                         unsigned long long* bins, hipStream_t s);
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
                      const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red,
                      hlc_result* out, hipStream_t s);

@@ -1174,6 +1174,34 @@ void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t 
   if (np) hipLaunchKernelGGL(k_chain_small, dim3((unsigned)np), dim3(SMALL_TPB), 0, s, *v, props, chain_code, red);
 }
 
+namespace {
+// Outcome counters of a call (the verified / rejected-by-code counters a sharded run
+// all-reduces): bins[0..31] = votes by status byte, bins[32..63] = proposals by result status.
+// Per block an LDS histogram (one LDS atomic per item), then one global atomic per non-zero bin:
+// an all-OK batch costs ~1 global atomic per block, not one per vote on the same address.
+constexpr int HIST_BINS = 32;
+__global__ void k_outcome_hist(const uint8_t* vst, uint64_t n, const hlc_result* res, uint64_t np,
+                               unsigned long long* bins) {
+  __shared__ unsigned int h[2 * HIST_BINS];
+  if (threadIdx.x < 2 * HIST_BINS) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    atomicAdd(&h[min((unsigned)vst[i], (unsigned)HIST_BINS - 1)], 1u);
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < np; p += stride)
+    atomicAdd(&h[HIST_BINS + min((unsigned)res[p].status, (unsigned)HIST_BINS - 1)], 1u);
+  __syncthreads();
+  if (threadIdx.x < 2 * HIST_BINS && h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+}  // namespace
+
+void launch_outcome_hist(const uint8_t* vote_status, uint64_t n, const hlc_result* res, uint64_t np,
+                         unsigned long long* bins, hipStream_t s) {
+  const uint64_t m = std::max(n, np);
+  const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m + 4 * TPB - 1) / (4 * TPB), 1024));
+  hipLaunchKernelGGL(k_outcome_hist, dim3(blocks), dim3(TPB), 0, s, vote_status, n, res, np, bins);
+}
+
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
                      const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red, hlc_result* out,
                      hipStream_t s) {

@@ -397,9 +397,9 @@ HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
 // entries (b1, b2) arrive by LDS-DMA -- global_load_lds_dwordx4, 5 pieces of 16 B per lane, 1 KiB
 // per wave-instruction, no VGPR destination -- issued right after the previous window's additions,
 // so the gathers' latency hides behind 5 doublings with no registers held in flight.  Measured
-// neutral (91.17 vs 91.13 M votes/s, profiles/r03_ab_glds.txt): the gathers' latency is already
-// hidden by the other waves; what the table costs is traffic.  RT_SLOT words per
-// entry slot: piece k of lane l at word 256 k + 4 l.
+// 0.8% slower over three alternating rounds (profiles/r03/ab_glds_share_probes.txt): the other
+// waves already hide the gathers' latency; what the table costs is traffic.
+// RT_SLOT words per entry slot: piece k of lane l at word 256 k + 4 l.
 constexpr int RT_SLOT = 5 * 256;
 constexpr int RT_WAVE_WORDS = 2 * RT_SLOT;  // b1 and b2 slots: 10 KiB per wave
 HLC_DEV void glds_entry(const uint32_t* ent, uint32_t* slot) {

@@ -213,6 +213,7 @@ constexpr uint32_t HUGE_MSG = 1u << 20;
 constexpr uint32_t HUGE_MAX = 0x7FFFFFFEu;
 constexpr uint32_t HUGE_ERR = 0xFFFFFF00u;
 constexpr uint32_t HUGE_UNRES = 0xFFu;  // internal marker, never reported (not a prost error code)
+constexpr int HUGE_RESUME_PASSES = 4;     // parallel re-marking passes past long top-level groups
 constexpr uint64_t HUGE_GROUP_SCAN = 256;
 __host__ __device__ __forceinline__ bool is_huge(uint32_t len) { return len > HUGE_MSG && len < HUGE_MAX; }
 
@@ -431,9 +432,31 @@ __global__ void __launch_bounds__(TPB) k_huge_unres(uint32_t len, const uint32_t
     if (mark[p] && next[p] == (HUGE_ERR | HUGE_UNRES)) atomicMin(st + 11, (uint32_t)p);
 }
 
-// From the first unresolved offset on, one lane walks the rest of the top-level fields with
-// unbounded group skips, writing their next[] entries and marks: linear in the message, however
-// many long top-level groups it holds, with no host round trip (a no-op when st[11] is unset).
+// One lane resolves the first unresolved offset on the chain (st[11]) with an unbounded group skip
+// and patches next[] there, so that a fresh set of pointer-jumping rounds continues the chain in
+// parallel past the long group; st[12] = 1 when it did (the rounds of this pass run), else 0.
+__global__ void k_huge_resolve(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len,
+                               uint32_t* __restrict__ next, uint32_t* st) {
+  if (threadIdx.x || blockIdx.x) return;
+  const uint32_t p = st[11];
+  st[12] = 0;
+  if (p == 0xFFFFFFFFu) return;
+  const uint32_t q = huge_parse(wire, base, len, p, false);
+  next[p] = q;
+  st[12] = q < HUGE_ERR ? 1u : 0u;
+}
+
+// J = next for a resumed pass (only when k_huge_resolve patched an offset)
+__global__ void __launch_bounds__(TPB) k_huge_copy_if(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                      uint32_t len, const uint32_t* st) {
+  if (!st[12]) return;
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x)
+    dst[p] = src[p];
+}
+
+// After the bounded resumed passes, one lane walks whatever is left of the top-level fields from
+// the first still-unresolved offset with unbounded group skips, writing their next[] entries and
+// marks: linear in the rest of the message, with no host round trip (a no-op when st[11] is unset).
 __global__ void k_huge_tail(const uint8_t* __restrict__ wire, uint64_t base, uint32_t len, uint32_t* __restrict__ next,
                             uint8_t* __restrict__ mark, const uint32_t* st) {
   if (threadIdx.x || blockIdx.x) return;
@@ -451,7 +474,8 @@ __global__ void k_huge_tail(const uint8_t* __restrict__ wire, uint64_t base, uin
 // One pointer-jumping round: marks J[p] for marked p, J1 = J o J.  Concurrent marks within a round
 // only ever add offsets reachable from the start, so the byte stores need no ordering.
 __global__ void __launch_bounds__(TPB) k_huge_round(const uint32_t* __restrict__ J, uint32_t* __restrict__ J1,
-                                                    uint8_t* mark, uint32_t len) {
+                                                    uint8_t* mark, uint32_t len, const uint32_t* active) {
+  if (active && !*active) return;  // a resumed pass that has nothing to resume
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= len; p += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t j = J[p];
     if (j < len) {
@@ -751,13 +775,27 @@ int launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t 
   HUGE_CHK(hipMemsetAsync(mark, 1, 1, s));
   hipLaunchKernelGGL(k_huge_next, dim3(g), dim3(TPB), 0, s, wire, base, len, next);
   HUGE_CHK(hipMemcpyAsync(save, next, ((size_t)len + 1) * 4, hipMemcpyDeviceToDevice, s));  // the rounds consume it
-  uint32_t* a = next;
-  uint32_t* b = jump;
-  for (uint64_t reach = 1; reach <= len; reach <<= 1) {  // after the round, steps < 2 * reach are marked
-    hipLaunchKernelGGL(k_huge_round, dim3(g), dim3(TPB), 0, s, a, b, mark, len);
-    std::swap(a, b);
+  auto rounds = [&](const uint32_t* active) {
+    uint32_t* a = next;
+    uint32_t* b = jump;
+    for (uint64_t reach = 1; reach <= len; reach <<= 1) {  // after the round, steps < 2 * reach are marked
+      hipLaunchKernelGGL(k_huge_round, dim3(g), dim3(TPB), 0, s, a, b, mark, len, active);
+      std::swap(a, b);
+    }
+  };
+  rounds(nullptr);
+  // A top-level group longer than the bounded skip stops the chain.  Up to HUGE_RESUME_PASSES times:
+  // one lane resolves the first such offset, and a fresh set of rounds (skipped on the device when
+  // there was nothing to resolve) resumes the parallel marking past it -- a long group at the head
+  // of a message no longer hands the rest of it to one lane.  Then one lane finishes whatever is
+  // left (linear).
+  for (int pass = 0; pass < HUGE_RESUME_PASSES; ++pass) {
+    HUGE_CHK(hipMemsetAsync(st + 11, 0xFF, 4, s));
+    hipLaunchKernelGGL(k_huge_unres, dim3(g), dim3(TPB), 0, s, len, save, mark, st);
+    hipLaunchKernelGGL(k_huge_resolve, dim3(1), dim3(64), 0, s, wire, base, len, save, st);
+    hipLaunchKernelGGL(k_huge_copy_if, dim3(g), dim3(TPB), 0, s, save, next, len, st);
+    rounds(st + 12);
   }
-  // a long top-level group on the chain: one lane finishes the chain from there (linear)
   HUGE_CHK(hipMemsetAsync(st + 11, 0xFF, 4, s));
   hipLaunchKernelGGL(k_huge_unres, dim3(g), dim3(TPB), 0, s, len, save, mark, st);
   hipLaunchKernelGGL(k_huge_tail, dim3(1), dim3(64), 0, s, wire, base, len, save, mark, st);

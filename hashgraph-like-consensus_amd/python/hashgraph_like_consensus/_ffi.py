@@ -133,7 +133,7 @@ EXPORTED_SYMBOLS = (
     "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_ctx_take_chain_time", "hlc_consensus_timeout_batch",
     "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
     "hlc_process_votes", "hlc_process_votes_device", "hlc_synth_arena_bytes", "hlc_synth_votes_device",
-    "hlc_synth_byzantine_device",
+    "hlc_synth_byzantine_device", "hlc_outcome_counts_device",
 )
 
 _lib = None
@@ -203,6 +203,8 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_synth_votes_device.restype = c_int
     lib.hlc_synth_byzantine_device.argtypes = [vp, c_uint64, c_uint64, c_uint64, c_uint32, POINTER(hlc_votes), vp, vp]
     lib.hlc_synth_byzantine_device.restype = c_int
+    lib.hlc_outcome_counts_device.argtypes = [vp, vp, c_uint64, vp, c_uint64, vp, vp]
+    lib.hlc_outcome_counts_device.restype = c_int
     lib.hlc_ctx_set_kernel_timing.argtypes = [vp, c_int]
     lib.hlc_ctx_set_kernel_timing.restype = c_int
     lib.hlc_ctx_take_kernel_time.argtypes = [vp, POINTER(ctypes.c_double), u64p, POINTER(ctypes.c_double), u64p]

@@ -248,6 +248,13 @@ class Engine:
             self.ctx, seed, start_proposal, n_proposals, votes_per_proposal, ctypes.byref(dbatch.view),
             c_void_p(kind_ptr), c_void_p(stream_handle) if stream_handle else None))
 
+    def outcome_counts_device(self, status_ptr: int, n_votes: int, results_ptr: int, n_proposals: int,
+                              counts_ptr: int, stream_handle: int = 0) -> None:
+        """hlc_outcome_counts_device: u64[64] histograms (votes by status, proposals by status)."""
+        _ffi.check(self.lib.hlc_outcome_counts_device(
+            self.ctx, c_void_p(status_ptr), n_votes, c_void_p(results_ptr), n_proposals, c_void_p(counts_ptr),
+            c_void_p(stream_handle) if stream_handle else None))
+
     def validate_wire_proposals_device(self, dwire, stream_handle: int = 0) -> None:
         """hlc_validate_wire_proposals_device over a `device.DeviceWire` (wire bytes, message
         extents and scope configs in HBM); results land in dwire.results."""

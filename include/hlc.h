@@ -257,6 +257,14 @@ int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_propo
                            uint8_t* out_vote_status, uint8_t* out_vote_reason,
                            uint8_t* out_recovered);
 
+/* Outcome counters of a validate-many call (what a proposal-sharded run
+ * all-reduces): out_counts[s] = votes whose status byte is s, out_counts[32 + s] = proposals whose
+ * result status is s (s < 32; a larger byte is counted in bin 31).  Device pointers, enqueued on
+ * `stream` (NULL: the context's stream) after zeroing out_counts[0..63]; no host synchronisation. */
+int hlc_outcome_counts_device(hlc_ctx* ctx, const uint8_t* vote_status, uint64_t n_votes,
+                              const hlc_result* results, uint64_t n_proposals, uint64_t* out_counts,
+                              void* stream);
+
 /* Same, but every pointer (inside `votes`, `proposals`, and the outputs) is DEVICE memory
  * of the context's device, and the work is enqueued on `stream` (a hipStream_t, or NULL for
  * the context's stream) without host synchronisation.  Used when inputs are already

@@ -336,3 +336,26 @@ def test_gpu_decode_huge_message_many_long_groups(engine):
         encode_proposal(random_proposal(rnd, max_votes=2)),
     ]
     _check_decode(engine, msgs, _scope(1))
+
+
+def test_gpu_decode_huge_message_long_group_first(engine):
+    """a top-level group longer than the bounded per-offset skip at the START of a huge
+    message used to hand the whole message to one lane.  The chain now resumes in parallel past it
+    (k_huge_resolve + a fresh set of pointer-jumping rounds, up to HUGE_RESUME_PASSES times): a long
+    group at offset 0 followed by 8k vote records, two groups, and four-plus groups (the last ones
+    then taken by the serial tail) all equal the prost oracle."""
+    from wire_fuzz import random_vote
+    from hashgraph_like_consensus.protos import Proposal
+    rnd = random.Random(41)
+    grp = b"\xfb\x01\x0a\x90\x02" + bytes(272) + b"\xfc\x01"
+    votes = [random_vote(rnd) for _ in range(8000)]
+    body = encode_proposal(Proposal(name="lg", proposal_id=5, votes=votes, expected_voters_count=30000,
+                                    timestamp=3, expiration_timestamp=90))
+    msgs = [
+        grp + body,
+        grp + grp + body + b"\x60\x2d",
+        grp * 6 + body,
+        encode_proposal(random_proposal(rnd, max_votes=2)),
+    ]
+    assert all(len(m) > (1 << 20) for m in msgs[:3])
+    _check_decode(engine, msgs, _scope(1))

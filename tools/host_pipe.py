@@ -23,6 +23,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--chunks", default="0,65536,131072,262144")
+    ap.add_argument("--threads", default="4", help="HLC_PIPE_THREADS settings to sweep")
     ap.add_argument("--proposals", type=int, default=10_000)
     a = ap.parse_args()
     import numpy as np
@@ -40,8 +41,12 @@ def main() -> int:
                    + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
     ref = None
     out = []
-    for c in [int(x) for x in a.chunks.split(",")]:
+    settings = [(c, t) for c in [int(x) for x in a.chunks.split(",")] for t in [int(x) for x in a.threads.split(",")]]
+    for c, th in settings:
+        if c == 0 and ref is not None:
+            continue
         os.environ["HLC_PIPE_CHUNK_VOTES"] = str(c)
+        os.environ["HLC_PIPE_THREADS"] = str(th)
         r = eng.validate_proposals(b, d, db.now, want_votes=True)
         if ref is None:
             ref = r
@@ -51,7 +56,7 @@ def main() -> int:
         for _ in range(a.steps):
             eng.validate_proposals(b, d, db.now, want_votes=True)
         el = (time.perf_counter() - t) / a.steps
-        row = {"chunk_votes": c, "ms_per_call": el * 1e3, "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in,
+        row = {"chunk_votes": c, "threads": th, "ms_per_call": el * 1e3, "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in,
                "outputs_equal_one_shot": True}
         print(json.dumps(row), flush=True)
         out.append(row)
