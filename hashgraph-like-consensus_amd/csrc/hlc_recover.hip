@@ -136,6 +136,17 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
     if (lane == 0) base = atomicAdd(ctr, 64ull);
     base = __shfl(base, 0);
     if (base >= n) break;
+#ifdef HLC_REC_PRIO
+    {
+      // A/B variant: the fewer grabs remain after this one, the higher the wave's issue priority,
+      // so waves that started late are not starved by the arbiter's oldest-first order at the end
+      const uint64_t per_round = lanes;  // votes one full round of grabs covers
+      const unsigned left = __builtin_amdgcn_readfirstlane((unsigned)min((uint64_t)3, (n - base) / per_round));
+      if (left == 0) __builtin_amdgcn_s_setprio(3);
+      else if (left == 1) __builtin_amdgcn_s_setprio(2);
+      else if (left == 2) __builtin_amdgcn_s_setprio(1);
+    }
+#endif
     const uint64_t i = base + lane;
     if (i >= n) continue;  // the next grab is past n: the wave leaves together
 #endif
