@@ -161,6 +161,8 @@ struct hlc_ctx {
   uint64_t rec_lanes = 0;
   int rec_force_exact = 0;  // HLC_REC_FORCE_EXACT=1: every vote through the checked chains (tests)
   int serial_stages = 0;    // HLC_SERIAL_STAGES=1: prep + main after the prehash on one stream (A/B, clock probes)
+  int prep_first = 0;       // HLC_PREP_FIRST=1: the prep stage alone on the launch stream before the fork (A/B)
+  int aux_prio = 0;         // HLC_AUX_PRIO=1: the second stream at the device's greatest priority (A/B)
   // hlc_validate_proposals pipeline: two child contexts (own streams and workspace, the parent's
   // fixed-base tables) that take alternate proposal chunks, so one chunk's host->device copy and
   // the next chunk's kernels overlap the previous chunk's kernels (created on first use)
@@ -217,6 +219,16 @@ struct hlc_ctx {
 };
 
 namespace {
+
+// the context's second stream (the recovery's prep / main stages), optionally at the device's
+// greatest stream priority so that its workgroups are dispatched ahead of the prehash's
+hipError_t create_aux(hlc_ctx* c) {
+  if (!c->aux_prio) return hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, greatest);
+}
 
 int activate(hlc_ctx* ctx) {
   HIPCHK(hipSetDevice(ctx->device));
@@ -346,19 +358,27 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     }
     return 0;
   };
+  // HLC_PREP_FIRST=1: the prep stage runs alone on `s` before the fork, so the main stage starts as
+  // soon as it is done and the prehash fills the SIMD slots beside main instead of beside prep
+  const bool prep_first = c->prep_first && !c->serial_stages;
+  hipStream_t prep_s = prep_first ? s : aux;
   if (c->serial_stages) CHK(prehash_and_chain());
-  else {
+  if (!c->serial_stages && !prep_first) {
     HIPCHK(hipEventRecord(c->ev_fork, s));
     HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
   }
-  if (c->timing) HIPCHK(hipEventRecord(p0, aux));
+  if (c->timing) HIPCHK(hipEventRecord(p0, prep_s));
   hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
-                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux);
+                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), prep_s);
   if (c->timing) {
-    HIPCHK(hipEventRecord(p1, aux));
+    HIPCHK(hipEventRecord(p1, prep_s));
     c->rec_prep_ev.emplace_back(p0, p1);
-    HIPCHK(hipEventRecord(r0, aux));
   }
+  if (prep_first) {
+    HIPCHK(hipEventRecord(c->ev_fork, s));
+    HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
+  }
+  if (c->timing) HIPCHK(hipEventRecord(r0, aux));
   hlc::launch_recover_main(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, c->rec_scratch.as<uint32_t>(),
                            c->rec_lanes, c->rec_work.as<uint32_t>(), aux, c->rec_force_exact);
   if (!c->serial_stages) {
@@ -631,8 +651,10 @@ int make_child(hlc_ctx* parent, hlc_ctx** out) {
   c->device = parent->device;
   c->rec_force_exact = parent->rec_force_exact;
   c->serial_stages = parent->serial_stages;
+  c->prep_first = parent->prep_first;
+  c->aux_prio = parent->aux_prio;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      create_aux(c) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess) {
@@ -893,8 +915,10 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
   c->device = device;
   if (const char* fx = std::getenv("HLC_REC_FORCE_EXACT")) c->rec_force_exact = std::atoi(fx) != 0;
   if (const char* ss = std::getenv("HLC_SERIAL_STAGES")) c->serial_stages = std::atoi(ss) != 0;
+  if (const char* pf = std::getenv("HLC_PREP_FIRST")) c->prep_first = std::atoi(pf) != 0;
+  if (const char* ap = std::getenv("HLC_AUX_PRIO")) c->aux_prio = std::atoi(ap) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      create_aux(c) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -306,6 +306,42 @@ HLC_HD void fe29_sqr_ref(fe29& r, const fe29& a) {
   for (int i = 0; i < 9; ++i) r.v[i] = o[i];
 }
 
+// r = a b + c e (mod p) with ONE split / fold / carry pass for the sum: both products accumulate
+// into the same 64-bit columns, so every column must hold eighteen products:
+// sum_i a_i b_(k-i) + c_i e_(k-i) + carry-in + folds < 2^64 (e.g. a normalised, b < 2^30.6, c < 2^30.01,
+// e normalised: 9 (2^59.6 + 2^59.02) < 2^63.5).  r normalised.  (C++ reference of fe29_muladd_asm.)
+HLC_HD void fe29_muladd_ref(fe29& r, const fe29& a, const fe29& b, const fe29& c, const fe29& e) {
+  uint32_t H[9];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 9; k <= 16; ++k) {
+#pragma unroll
+    for (int i = k - 8; i <= 8; ++i) {
+      acc = mad29(a.v[i], b.v[k - i], acc);
+      acc = mad29(c.v[i], e.v[k - i], acc);
+    }
+    H[k - 9] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  H[8] = (uint32_t)acc;
+  uint32_t o[9];
+  acc = 0;
+#pragma unroll
+  for (int j = 0; j <= 8; ++j) {
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      acc = mad29(a.v[i], b.v[j - i], acc);
+      acc = mad29(c.v[i], e.v[j - i], acc);
+    }
+    FE29_LOW_FOLD(j, acc, H);
+    o[j] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  fe29_top(o, acc, H[8]);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = o[i];
+}
+
 #if defined(__HIPCC__)
 }  // namespace hlc
 #include "hlc_fe29_asm.hpp"
@@ -332,6 +368,13 @@ HLC_HD void fe29_sqr(fe29& r, const fe29& a) {
   fe29_sqr_asm(r.v, a.v);
 #else
   fe29_sqr_ref(r, a);
+#endif
+}
+HLC_HD void fe29_muladd(fe29& r, const fe29& a, const fe29& b, const fe29& c, const fe29& e) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe29_muladd_asm(r.v, a.v, b.v, c.v, e.v);
+#else
+  fe29_muladd_ref(r, a, b, c, e);
 #endif
 }
 // two independent products in one interleaved schedule (two dependency chains in flight per wave)

@@ -65,8 +65,9 @@ HLC_HD void gej29_double(gej29& r, const gej29& a) {
 }
 
 // r = a + b, b affine (madd-2007-bl: 8M + 3S, four carry steps).  Z3 = 2 Z1 H as one product;
-// I = 4 HH stays lazy (it only multiplies normalised values); 2V and 2 Y1 J fold into 128p-offset
-// subtractions.  r may alias a.  With zr != nullptr, *zr = Z3 / Z1 = 2H (the R-table build).
+// I = 4 HH stays lazy (it only multiplies normalised values); 2V folds into a 128p-offset
+// subtraction; Y3 = R (V - X3) - 2 Y1 J is one sum of two products (fe29_muladd, with -J carried
+// to normalised form) with a single reduction.  r may alias a.  With zr != nullptr, *zr = Z3 / Z1 = 2H (the R-table build).
 // EXACT = true handles the exceptional cases (a == b: doubling; a == -b: infinity) here.
 // EXACT = false (the hot chains) does NOT test for them: H == 0 gives Z3 == 0, every later Z
 // stays 0 (each step multiplies Z), and the caller tests the chain's final Z once per vote and
@@ -106,10 +107,16 @@ HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullp
   fe29_sqr(x3, rr);
   fe29_sub_b2c(x3, x3, j, v);      // X3 = R^2 - J - 2V
   fe29_sub_lazy(t, v, x3);         // V - X3, lazy: multiplies the normalised R
+#ifdef HLC_MADD_TWO_REDUCTIONS     // A/B: the two products reduced separately, then subtracted
   fe29_mul(y3, rr, t);
   fe29_add(t, a.y, a.y);
   fe29_mul(y1j, t, j);             // 2 Y1 J
   fe29_sub(y3, y3, y1j);           // Y3 = R (V - X3) - 2 Y1 J
+#else
+  fe29_neg(y1j, j);                // -J, normalised
+  fe29_add(h2, a.y, a.y);          // 2 Y1 (h2 is dead here)
+  fe29_muladd(y3, rr, t, h2, y1j); // Y3 = R (V - X3) + 2 Y1 (-J): one reduction for both products
+#endif
   r.x = x3;
   r.y = y3;
   r.z = z3;

@@ -181,7 +181,9 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
 }
 
 #ifndef HLC_COMB_MIN_WAVES
-#define HLC_COMB_MIN_WAVES 2  // launch-bounds floor; 200 VGPRs, runs at 2 waves, no spills (3 and 4 spill 124 / 284 B per lane)
+// launch-bounds floor.  With u2 R read back only after the comb chain (rec_comb29) the kernel takes
+// 142 VGPRs and runs at 3 waves per SIMD with no spills (it held 200 at 2 waves while u2 R stayed live)
+#define HLC_COMB_MIN_WAVES 2
 #endif
 // ---- comb: after the prehash, one lane per vote at full occupancy: u1 = -z / r, u1 G by the comb
 // (12 mixed additions from the HBM table), Q = u2 R + u1 G.  Votes the pre-checks rejected keep
@@ -201,10 +203,7 @@ __global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_comb(uint64_t n
   bool neg_g;
   fe_from_digest(z, z_digest + 8 * i);
   rec_u1(z, rec + i, n, u1, neg_g);
-  load_fe_ws(qx, q + i, n);
-  load_fe_ws(qy, q + (size_t)8 * n + i, n);
-  load_fe_ws(qz, q + (size_t)16 * n + i, n);
-  const int code = rec_comb29(u1, neg_g, m == MST_INF, qx, qy, qz, gcomb, force_exact != 0);
+  const int code = rec_comb29(u1, neg_g, m == MST_INF, q + i, n, qx, qy, qz, gcomb, force_exact != 0);
   state[i] = code != SCHEME_NONE ? (uint8_t)(1 + code) : REC_PENDING;
   if (code != SCHEME_NONE) return;
   store_fe_ws(qx, q + i, n);

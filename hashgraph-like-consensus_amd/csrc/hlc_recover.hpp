@@ -582,15 +582,20 @@ HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx,
 }
 
 // second half: Q = (u2 R, from rec_u2r29) + u1 G; Q in 8 x 32 limbs.  SCHEME_NONE or SCHEME_INFINITY.
-HLC_DEV int rec_comb29(const fe& u1, bool neg_g, bool inf, fe& qx, fe& qy, fe& qz, const uint32_t* gcomb,
-                       bool force_exact) {
+// u2 R (word-major at qin, stride words apart) is read only after the comb, so that its 24 words
+// are not live across the comb's chain (register pressure: k_rec_main runs this in its tail).
+HLC_DEV int rec_comb29(const fe& u1, bool neg_g, bool inf, const uint32_t* qin, size_t stride, fe& qx, fe& qy, fe& qz,
+                       const uint32_t* gcomb, bool force_exact) {
   gej29 acc, ag;
+  comb_mul_g29<false>(ag, u1, neg_g, gcomb);
+  if (force_exact || fe29_is_zero_modp(ag.z)) comb_mul_g29<true>(ag, u1, neg_g, gcomb);
+  load_fe_ws(qx, qin, stride);
+  load_fe_ws(qy, qin + 8 * stride, stride);
+  load_fe_ws(qz, qin + 16 * stride, stride);
   acc.inf = inf;
   fe29_from32(acc.x, qx.v);
   fe29_from32(acc.y, qy.v);
   fe29_from32(acc.z, qz.v);
-  comb_mul_g29<false>(ag, u1, neg_g, gcomb);
-  if (force_exact || fe29_is_zero_modp(ag.z)) comb_mul_g29<true>(ag, u1, neg_g, gcomb);
   gej29_add(acc, acc, ag);
   if (acc.inf) return SCHEME_INFINITY;
   fe29_to32(qx.v, acc.x);

@@ -225,6 +225,22 @@ def test_sub2_sub_b2c(checked):
         assert val(o3[k]) % P == (va - vb - 2 * v3) % P
 
 
+def test_muladd_at_bounds(checked):
+    """fe29_muladd (a b + c e, one reduction for both products) at the operand bounds of its use in
+    the mixed addition's Y3 = R (V - X3) + 2 Y1 (-J): a normalised, b a lazy difference (< 2^30.59),
+    c a lazy doubling (< 2^30.01), e normalised -- every limb at its maximum included."""
+    rnd = random.Random(61)
+    n = 3000
+    a, e = nrm_limbs(rnd, n), nrm_limbs(rnd, n)
+    b, c = limbs(rnd, n, int(2**30.59)), limbs(rnd, n, 2**30 + 2**19)
+    a[0], e[0] = 2**29 + 2**18 - 1, 2**29 + 2**18 - 1
+    b[0], c[0] = int(2**30.59) - 1, 2**30 + 2**19 - 1
+    o = run(checked, 15, a, np.concatenate([b, c, e]))
+    check_normalised(o, 1, 1, rest=0)
+    for k in range(n):
+        assert val(o[k]) % P == (val(a[k]) * val(b[k]) + val(c[k]) * val(e[k])) % P, k
+
+
 def jac(x, y, z, inf=0):
     w = np.zeros(28, np.uint32)
     w[0:9], w[9:18], w[18:27], w[27] = x, y, z, inf

@@ -37,15 +37,19 @@ def column(em, prods, acc, first_zero, sd):
         em(f"v_mad_u64_u32 {acc}, {sd}, {x}, {y}, {addend}")
 
 
-def gen(square, tag="", base=0):
+def gen(square, tag="", base=0, dual=False):
     """One product's instruction list.  tag prefixes the operand names, base the fixed registers
-    (v[base .. base+5]) so that two independent products can be interleaved (gen_dual)."""
+    (v[base .. base+5]) so that two independent products can be interleaved (gen_dual).
+    dual: a*b + c*e in one column schedule (both products accumulate into the same 64-bit columns,
+    one split / fold / carry pass for the sum)."""
     em = Em()
     A = lambda i: f"%[{tag}a{i}]"
     B = (lambda i: f"%[{tag}a{i}]") if square else (lambda i: f"%[{tag}b{i}]")
     D = lambda i: f"%[{tag}d{i}]"    # doubled limbs (squaring), computed by the compiler before the asm
     H = lambda k: f"%[{tag}h{k}]"    # H_{9+k}, k = 0..7 (compiler-allocated); H_17 stays in acc1.lo
     R = lambda j: f"%[{tag}r{j}]"
+    C = lambda i: f"%[{tag}c{i}]"    # dual: the second product's operands
+    E = lambda i: f"%[{tag}e{i}]"
     v = lambda k: f"v{base + k}"
     acc1, acc2, tt = f"v[{base}:{base + 1}]", f"v[{base + 2}:{base + 3}]", f"v[{base + 4}:{base + 5}]"
     sd = f"%[{tag}sd]"
@@ -63,6 +67,8 @@ def gen(square, tag="", base=0):
                     out.append((A(i), A(i)))
             else:
                 out.append((A(i), B(j)))
+                if dual:
+                    out.append((C(i), E(j)))
         return out
 
     # The high columns (9..16) and the low columns (0..8) are two independent mad chains until the
@@ -187,6 +193,26 @@ def emit_dual(name, sq1, sq2):
     return "".join(o)
 
 
+def emit_muladd(name):
+    """r = a b + c e (mod p): one column schedule for the sum of two products (hlc_fe29.hpp
+    fe29_muladd_ref is the same arithmetic)."""
+    lines = gen(False, dual=True)
+    o = [f"// {len(lines)} instructions\n__device__ __forceinline__ void {name}(uint32_t r[9], const uint32_t a[9], "
+         "const uint32_t b[9], const uint32_t c[9], const uint32_t e[9]) {\n"]
+    o.append("  uint64_t sd;\n  uint32_t h[8];\n")
+    o.append("  asm volatile(\n")
+    o.append(block(lines) + "\n")
+    outs = [f'[r{j}] "=&v"(r[{j}])' for j in range(9)] + [f'[h{k}] "=&v"(h[{k}])' for k in range(8)]
+    outs += ['[sd] "=&s"(sd)']
+    ins = [f'[{x}{i}] "v"({x}[{i}])' for x in "abce" for i in range(9)]
+    ins += ['[kfl] "s"(31264u)', '[kfh] "s"(256u)', '[kf00] "s"(256u * 31264u)', '[kf01] "s"(65536u)']
+    clob = ", ".join(f'"v{i}"' for i in range(6))
+    o.append("      : " + ", ".join(outs) + "\n")
+    o.append("      : " + ", ".join(ins) + "\n")
+    o.append("      : " + clob + ");\n}\n\n")
+    return "".join(o)
+
+
 def main():
     mul = gen(False)
     sqr = gen(True)
@@ -195,7 +221,9 @@ def main():
             + emit("fe29_mul_sb_asm", False, mul, b_sgpr=True)
             + "// two independent products interleaved (x = a b, y = c d / x = a^2, y = c^2 / x = a b, y = c^2)\n"
             + emit_dual("fe29_mul2_asm", False, False) + emit_dual("fe29_sqr2_asm", True, True)
-            + emit_dual("fe29_mulsqr_asm", False, True) + "}  // namespace hlc\n")
+            + emit_dual("fe29_mulsqr_asm", False, True)
+            + "// sum of two products with one reduction (r = a b + c e)\n" + emit_muladd("fe29_muladd_asm")
+            + "}  // namespace hlc\n")
     sys.stdout.write(text)
 
 
