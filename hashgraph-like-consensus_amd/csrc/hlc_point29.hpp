@@ -40,27 +40,39 @@ HLC_HD void gej29_set_ge(gej29& r, const ge29& a) {
   r.inf = 0;
 }
 
-// dbl-2009-l (a = 0) arranged for lazy reduction: 3M + 4S and three carry steps (one more
-// product than the textbook 2M + 5S, ~110 fewer instructions).  D = 4 X B is ONE product of the
-// doubled operands (2X)(2B), C4 = 4C = (2B)^2, so X3 = F - 2D and Y3 = E (D - X3) - 2 C4 are
-// each one 128p-offset subtraction of two normalised values.  (secp256k1 has prime order: no
-// point with y = 0.)  r may alias a.
+// dbl-2009-l (a = 0) arranged for lazy reduction: 3M + 3S and three carry steps.  D = 4 X B is ONE
+// product of the doubled operands (2X)(2B), so X3 = F - 2D is one 128p-offset subtraction of two
+// normalised values; Y3 = E (D - X3) - 2 (2B)^2 is one sum of two products with a single reduction
+// (fe29_muladd: E (D - X3) + 4B (-2B)), so (2B)^2 is never reduced on its own.  (secp256k1 has
+// prime order: no point with y = 0.)  r may alias a.
 HLC_HD void gej29_double(gej29& r, const gej29& a) {
-  fe29 A, B, X2, B2, D, C4, E, F, Z2, t, M;
+  fe29 A, B, X2, B2, D, E, F, Z2, t;
   fe29_sqr(A, a.x);
   fe29_sqr(B, a.y);
   fe29_add(X2, a.x, a.x);
   fe29_add(B2, B, B);
   fe29_mul(D, X2, B2);          // 4 X B            (2^30.01 x 2^30.01 operands)
-  fe29_sqr(C4, B2);             // 4 Y^4
   fe29_mul_small(E, A, 3);      // 3 X^2, normalised: it is squared next
   fe29_sqr(F, E);
   fe29_add(Z2, a.z, a.z);
   fe29_mul(r.z, a.y, Z2);       // Z3 = 2 Y Z
   fe29_sub2(r.x, F, D, D);      // X3 = F - 2D
   fe29_sub_lazy(t, D, r.x);     // D - X3, lazy: multiplies the normalised E
+#ifdef HLC_DBL_SQR_C4           // A/B: C4 = (2B)^2 squared and subtracted after a separate product
+  fe29 C4, M;
+  fe29_sqr(C4, B2);             // 4 Y^4
   fe29_mul(M, E, t);
   fe29_sub2(r.y, M, C4, C4);    // Y3 = E (D - X3) - 8 Y^4
+#else
+  // Y3 = E (D - X3) - 2 (2B)^2 = E t + 4B (-2B): one sum of two products, one reduction
+  // (fe29_muladd).  -2B is carried to normalised form; 4B stays lazy (< 2^31.01).  Column bound:
+  // 9 (2^29.01 2^30.59 + 2^31.01 2^29.01) < 2^63.98.  (-4B against 2B would need 4B <= 128p's
+  // limb 8, 2^31 - 5, which a normalised B at its limb-8 maximum exceeds.)
+  fe29 nb, b4;
+  fe29_neg(nb, B2);
+  fe29_add(b4, B2, B2);
+  fe29_muladd(r.y, E, t, b4, nb);
+#endif
   r.inf = a.inf;
 }
 

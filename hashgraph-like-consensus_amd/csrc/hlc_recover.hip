@@ -13,12 +13,14 @@ namespace {
 #endif
 constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
 #ifndef HLC_REC_MIN_WAVES
-// __launch_bounds__ minimum waves per SIMD for k_rec_main: a floor for the register allocator, not
-// the occupancy it reaches.  With 2 the kernel takes 166 VGPRs and so RUNS at 3 waves per SIMD (no
-// spills); 3 beats a grid capped at 2 by 5-6% and a forced 4 (spills) by 2%
-// (profiles/r02_ab_main_waves_split.txt).  The grid is sized from the occupancy API
+// __launch_bounds__ minimum waves per SIMD for k_rec_main: a ceiling on the registers the allocator
+// may take (512 / waves, in steps of 8).  3 waves beat a grid capped at 2 by 5-6% and a forced 4
+// (spills) by 2% (profiles/r02_ab_main_waves_split.txt).  Left to itself (a floor of 2) the
+// allocator takes 174 VGPRs since the doubling's Y3 became one sum of two products (fe29_muladd),
+// one step past 3 waves; with the floor at 3 it fits 168, spilling two 8-byte values that are
+// stored once and reloaded outside the chains.  The grid is sized from the occupancy API
 // (recover_grid_lanes), so it follows whatever the build reaches.
-#define HLC_REC_MIN_WAVES 2
+#define HLC_REC_MIN_WAVES 3
 #endif
 
 // ---- prep: parse + batched r^-1 + scalars (REC_BATCH votes per lane, one safegcd) ----
