@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -163,10 +164,10 @@ struct hlc_ctx {
   int serial_stages = 0;    // HLC_SERIAL_STAGES=1: prep + main after the prehash on one stream (A/B, clock probes)
   int prep_first = 0;       // HLC_PREP_FIRST=1: the prep stage alone on the launch stream before the fork (A/B)
   int aux_prio = 0;         // HLC_AUX_PRIO=1: the second stream at the device's greatest priority (A/B)
-  // hlc_validate_proposals pipeline: two child contexts (own streams and workspace, the parent's
-  // fixed-base tables) that take alternate proposal chunks, so one chunk's host->device copy and
-  // the next chunk's kernels overlap the previous chunk's kernels (created on first use)
-  hlc_ctx* pipe[2] = {nullptr, nullptr};
+  // hlc_validate_proposals pipeline: up to four child contexts (own streams and workspace, the
+  // parent's fixed-base tables) that take proposal chunks in turn, so one chunk's host->device copy
+  // and the next chunks' kernels overlap the previous chunks' kernels (created on first use)
+  hlc_ctx* pipe[4] = {nullptr, nullptr, nullptr, nullptr};
   std::unique_ptr<HostPool> pool;  // the parent's staging workers (HLC_PIPE_THREADS)
   // a pipeline child's staging: page-locked inputs / outputs, one device input buffer, the event
   // after its chunk's output copy, and which chunk it holds
@@ -700,22 +701,77 @@ int pipe_threads() {
   return std::max(1, std::min(t, 64));
 }
 
+// Child contexts of the pipeline, i.e. chunks in flight (HLC_PIPE_DEPTH, default 3, 2..4).
+int pipe_depth() {
+  const char* e = std::getenv("HLC_PIPE_DEPTH");
+  const int d = e ? std::atoi(e) : 3;
+  return std::max(2, std::min(d, 4));
+}
+
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // hlc_validate_proposals over host buffers, pipelined: the proposals are cut into chunks of about
 // pipe_chunk_votes() votes (contiguous proposal ranges whose vote ranges are disjoint and in order --
 // the layout of prost-decoded / packed batches; any other layout returns *used = false and takes the
-// one-shot path).  Chunk k runs on child context pipe[k % 2] (own streams and workspace):
-//   host   : wait for the child's previous chunk (k-2) and copy its outputs out of page-locked
+// one-shot path).  Chunk k runs on child context pipe[k % D] (own streams and workspace; D =
+// pipe_depth(), 3 by default):
+//   host   : wait for the child's previous chunk (k-D) and copy its outputs out of page-locked
 //            memory; check chunk k's fields and copy its SoA slices, proposals and arena span into
 //            the child's page-locked staging buffer (the pool's threads);
 //   device : one H2D DMA of the staging buffer, the validate-many kernels, the outputs' D2H into
 //            page-locked memory, an event -- all asynchronous on the child's stream.
-// So while the host stages chunk k, the device runs chunk k-1 (and chunk k-2's tail): copies,
-// checks and kernels overlap, and the two children's grids fill each other's tails.
+// So while the host stages chunk k, the device runs chunks k-D+1 .. k-1: copies, checks and kernels
+// overlap, and the children's grids fill each other's tails.  With D = 2 the host had to wait for
+// chunk k-2 before staging chunk k, and the device ran dry at every pair boundary (HLC_PIPE_TRACE:
+// ~0.4 ms idle per 131k votes); D = 3 keeps a staged chunk queued behind the two running ones.
+// HLC_PIPE_TRACE=1: one JSON line per pipelined call on stderr -- per chunk the host phases (wait for
+// the child's previous chunk, field checks, staging copies, enqueue) and the device spans (H2D, kernels,
+// D2H) from timing events, all in ms from the call's start (tools/host_pipe.py --trace)
+struct PipeTrace {
+  using clk = std::chrono::steady_clock;
+  bool on = false;
+  clk::time_point t0;
+  hipEvent_t e0 = nullptr;
+  struct Row {
+    double wait0, wait1, check1, stage1, enq1;
+    hipEvent_t a, b, c, d;  // before H2D, after H2D, after the kernels, after D2H
+  };
+  std::vector<Row> rows;
+  double ms(clk::time_point t) const { return std::chrono::duration<double, std::milli>(t - t0).count(); }
+  hipEvent_t ev(hipStream_t s) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) == hipSuccess) (void)hipEventRecord(e, s);
+    return e;
+  }
+  void print(uint64_t n, size_t chunks) {
+    (void)hipDeviceSynchronize();
+    auto el = [&](hipEvent_t e) {
+      float f = -1;
+      if (e0 && e) (void)hipEventElapsedTime(&f, e0, e);
+      return (double)f;
+    };
+    std::fprintf(stderr, "HLC_PIPE_TRACE {\"votes\": %llu, \"chunks\": %zu, \"host_ms\": %.3f, \"rows\": [",
+                 (unsigned long long)n, chunks, ms(clk::now()));
+    for (size_t k = 0; k < rows.size(); ++k) {
+      const Row& r = rows[k];
+      std::fprintf(stderr,
+                   "%s{\"wait\": [%.3f, %.3f], \"check_end\": %.3f, \"stage_end\": %.3f, \"enq_end\": %.3f, "
+                   "\"h2d\": [%.3f, %.3f], \"kern_end\": %.3f, \"d2h_end\": %.3f}",
+                   k ? ", " : "", r.wait0, r.wait1, r.check1, r.stage1, r.enq1, el(r.a), el(r.b), el(r.c), el(r.d));
+    }
+    std::fprintf(stderr, "]}\n");
+    for (auto& r : rows)
+      for (hipEvent_t e : {r.a, r.b, r.c, r.d})
+        if (e) (void)hipEventDestroy(e);
+    if (e0) (void)hipEventDestroy(e0);
+  }
+};
+
 int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
                        hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec, bool* used) {
   *used = false;
+  PipeTrace tr;
+  if (const char* e = std::getenv("HLC_PIPE_TRACE")) tr.on = std::atoi(e) != 0;
   const uint64_t target = pipe_chunk_votes(), n = v->n;
   if (!target || n < 2 * target || np < 2) return 0;
   std::vector<Chunk> ch;
@@ -741,11 +797,17 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
   for (size_t k = 1; k < ch.size(); ++k)
     if (ch[k].v0 < ch[k - 1].v1) return 0;  // interleaved vote ranges: one-shot path
   if (ch.size() < 2) return 0;
-  for (int k = 0; k < 2; ++k)
+  const int depth = pipe_depth();
+  for (int k = 0; k < depth; ++k)
     if (!c->pipe[k]) CHK(make_child(c, &c->pipe[k]));
   if (!c->pool || c->pool->parts() != pipe_threads()) c->pool.reset(new HostPool(pipe_threads() - 1));
   HostPool& pool = *c->pool;
   *used = true;
+  if (tr.on) {
+    tr.t0 = PipeTrace::clk::now();
+    (void)hipEventCreate(&tr.e0);
+    (void)hipEventRecord(tr.e0, c->pipe[0]->stream);
+  }
 
   // output layout in a child's pin_out: results | status | reason | recovered
   auto out_layout = [&](uint64_t nv, uint64_t npk, size_t o[4]) {
@@ -769,15 +831,19 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     return 0;
   };
   auto drain = [&]() {
-    for (int k = 0; k < 2; ++k) {
-      (void)hipStreamSynchronize(c->pipe[k]->stream);
-      c->pipe[k]->busy = false;
+    for (hlc_ctx* p : c->pipe) {
+      if (!p) continue;
+      (void)hipStreamSynchronize(p->stream);
+      p->busy = false;
     }
   };
   std::vector<hlc_proposal> cp;
   for (size_t k = 0; k < ch.size(); ++k) {
-    hlc_ctx* w = c->pipe[k & 1];
+    hlc_ctx* w = c->pipe[k % depth];
+    PipeTrace::Row trow{};
+    if (tr.on) trow.wait0 = tr.ms(PipeTrace::clk::now());
     CHK(copy_out(w));  // its previous chunk (k - 2): also frees its staging buffers
+    if (tr.on) trow.wait1 = tr.ms(PipeTrace::clk::now());
     const Chunk& q = ch[k];
     const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
     // field checks of the chunk's votes and of the uncovered votes before it (the one-shot path's
@@ -815,6 +881,7 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
       a_hi = std::max(a_hi, hi[t]);
     }
     if (a_lo == UINT64_MAX) a_lo = a_hi = 0;
+    if (tr.on) trow.check1 = tr.ms(PipeTrace::clk::now());
     // input layout: vote_id | proposal_id | timestamp | vote | field_off | field_len | props | arena
     size_t o[9];
     o[0] = 0;
@@ -846,7 +913,12 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
       if (c1 > c0) std::memcpy(w->pin_in.at(o[7] + c0), v->bytes + a_lo + c0, c1 - c0);
     });
     hipStream_t s = w->stream;
+    if (tr.on) {
+      trow.stage1 = tr.ms(PipeTrace::clk::now());
+      trow.a = tr.ev(s);
+    }
     HIPCHK(hipMemcpyAsync(w->dev_in.p, w->pin_in.p, o[8], hipMemcpyHostToDevice, s));
+    if (tr.on) trow.b = tr.ev(s);
     uint8_t* d = w->dev_in.as<uint8_t>();
     hlc_votes dv;
     dv.n = nv;
@@ -865,6 +937,7 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     CHK(validate_device(w, &dv, reinterpret_cast<const hlc_proposal*>(d + o[6]), npk, now, w->out_res.as<hlc_result>(),
                         w->out_status.as<uint8_t>(), w->out_reason.as<uint8_t>(),
                         out_rec ? w->out_rec.as<uint8_t>() : nullptr, s));
+    if (tr.on) trow.c = tr.ev(s);
     if (npk) HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[0]), w->out_res.p, npk * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
     if (nv) {
       HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[1]), w->out_status.p, nv, hipMemcpyDeviceToHost, s));
@@ -872,13 +945,19 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
       if (out_rec) HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[3]), w->out_rec.p, nv * 20, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipEventRecord(w->ev_done, s));
+    if (tr.on) {
+      trow.d = tr.ev(s);
+      trow.enq1 = tr.ms(PipeTrace::clk::now());
+      tr.rows.push_back(trow);
+    }
     w->busy = true;
     w->chunk_p0 = q.p0;
     w->chunk_p1 = q.p1;
     w->chunk_v0 = q.v0;
     w->chunk_v1 = q.v1;
   }
-  for (size_t k = ch.size(); k < ch.size() + 2; ++k) CHK(copy_out(c->pipe[k & 1]));
+  for (size_t k = ch.size(); k < ch.size() + depth; ++k) CHK(copy_out(c->pipe[k % depth]));
+  if (tr.on) tr.print(n, ch.size());
   // votes between the chunks' ranges are covered by no proposal: not evaluated (as the one-shot path)
   uint64_t prev = 0;
   for (size_t k = 0; k <= ch.size(); ++k) {

@@ -5,7 +5,8 @@ The pipeline chunk size is read from HLC_PIPE_CHUNK_VOTES on every call (0 = one
 setting: outputs equal the one-shot outputs bit for bit, then --steps calls are timed (host buffers
 in, per-vote statuses + per-proposal results out, blocking).
 
-    python tools/host_pipe.py --steps 10 --chunks 0,65536,131072,262144
+    python tools/host_pipe.py --steps 10 --chunks 0,65536,131072,262144 --depths 2,3,4
+    (HLC_PIPE_TRACE=1 in the environment adds the per-chunk timeline of every call on stderr)
 """
 from __future__ import annotations
 
@@ -24,6 +25,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--chunks", default="0,65536,131072,262144")
     ap.add_argument("--threads", default="4", help="HLC_PIPE_THREADS settings to sweep")
+    ap.add_argument("--depths", default="3", help="HLC_PIPE_DEPTH settings to sweep (child contexts in flight)")
     ap.add_argument("--proposals", type=int, default=10_000)
     a = ap.parse_args()
     import numpy as np
@@ -41,12 +43,14 @@ def main() -> int:
                    + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
     ref = None
     out = []
-    settings = [(c, t) for c in [int(x) for x in a.chunks.split(",")] for t in [int(x) for x in a.threads.split(",")]]
-    for c, th in settings:
+    settings = [(c, t, dp) for c in [int(x) for x in a.chunks.split(",")] for t in [int(x) for x in a.threads.split(",")]
+                for dp in [int(x) for x in a.depths.split(",")]]
+    for c, th, dp in settings:
         if c == 0 and ref is not None:
             continue
         os.environ["HLC_PIPE_CHUNK_VOTES"] = str(c)
         os.environ["HLC_PIPE_THREADS"] = str(th)
+        os.environ["HLC_PIPE_DEPTH"] = str(dp)
         r = eng.validate_proposals(b, d, db.now, want_votes=True)
         if ref is None:
             ref = r
@@ -56,7 +60,7 @@ def main() -> int:
         for _ in range(a.steps):
             eng.validate_proposals(b, d, db.now, want_votes=True)
         el = (time.perf_counter() - t) / a.steps
-        row = {"chunk_votes": c, "threads": th, "ms_per_call": el * 1e3, "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in,
+        row = {"chunk_votes": c, "threads": th, "depth": dp, "ms_per_call": el * 1e3, "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in,
                "outputs_equal_one_shot": True}
         print(json.dumps(row), flush=True)
         out.append(row)
