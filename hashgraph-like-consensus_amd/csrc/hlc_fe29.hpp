@@ -342,6 +342,47 @@ HLC_HD void fe29_muladd_ref(fe29& r, const fe29& a, const fe29& b, const fe29& c
   for (int i = 0; i < 9; ++i) r.v[i] = o[i];
 }
 
+// r = a b + f or a^2 + f (mod p) for a nine-limb addend f (limbs < 2^32; in practice 128p minus
+// normalised values, i.e. a subtraction that follows the product): f_j joins low column j before
+// its split, so the product and the subtraction share one reduction.  Operand contract of mul / sqr;
+// r normalised.  (C++ references of fe29_mul_add_asm / fe29_sqr_add_asm.)
+HLC_HD void fe29_mul_add_ref(fe29& r, const fe29& a, const fe29& b, const uint32_t f[9], bool square) {
+  uint32_t H[9];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 9; k <= 16; ++k) {
+#pragma unroll
+    for (int i = k - 8; i <= 8; ++i) acc = mad29(a.v[i], square ? a.v[k - i] : b.v[k - i], acc);
+    H[k - 9] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  H[8] = (uint32_t)acc;
+  uint32_t o[9];
+  acc = 0;
+#pragma unroll
+  for (int j = 0; j <= 8; ++j) {
+#pragma unroll
+    for (int i = 0; i <= j; ++i) acc = mad29(a.v[i], square ? a.v[j - i] : b.v[j - i], acc);
+    acc = mad29(f[j], 1u, acc);
+    FE29_LOW_FOLD(j, acc, H);
+    o[j] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  fe29_top(o, acc, H[8]);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = o[i];
+}
+
+// the addend of "... - b - c" after a product: f = 128p - b - c limbwise, NO carry (b_i + c_i <= 128p's
+// limbs, as for fe29_sub2; c may be zero)
+HLC_HD void fe29_neg_addend(uint32_t f[9], const fe29& b, const fe29& c) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    FE29_CHECK((uint64_t)b.v[i] + c.v[i] <= k29(i));
+    f[i] = k29(i) - b.v[i] - c.v[i];
+  }
+}
+
 #if defined(__HIPCC__)
 }  // namespace hlc
 #include "hlc_fe29_asm.hpp"
@@ -375,6 +416,20 @@ HLC_HD void fe29_muladd(fe29& r, const fe29& a, const fe29& b, const fe29& c, co
   fe29_muladd_asm(r.v, a.v, b.v, c.v, e.v);
 #else
   fe29_muladd_ref(r, a, b, c, e);
+#endif
+}
+HLC_HD void fe29_mul_add(fe29& r, const fe29& a, const fe29& b, const uint32_t f[9]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe29_mul_add_asm(r.v, a.v, b.v, f);
+#else
+  fe29_mul_add_ref(r, a, b, f, false);
+#endif
+}
+HLC_HD void fe29_sqr_add(fe29& r, const fe29& a, const uint32_t f[9]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fe29_sqr_add_asm(r.v, a.v, f);
+#else
+  fe29_mul_add_ref(r, a, a, f, true);
 #endif
 }
 // two independent products in one interleaved schedule (two dependency chains in flight per wave)

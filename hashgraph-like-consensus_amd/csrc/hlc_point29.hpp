@@ -46,17 +46,26 @@ HLC_HD void gej29_set_ge(gej29& r, const ge29& a) {
 // (fe29_muladd: E (D - X3) + 4B (-2B)), so (2B)^2 is never reduced on its own.  (secp256k1 has
 // prime order: no point with y = 0.)  r may alias a.
 HLC_HD void gej29_double(gej29& r, const gej29& a) {
-  fe29 A, B, X2, B2, D, E, F, Z2, t;
+  fe29 A, B, X2, B2, D, E, Z2, t;
   fe29_sqr(A, a.x);
   fe29_sqr(B, a.y);
   fe29_add(X2, a.x, a.x);
   fe29_add(B2, B, B);
   fe29_mul(D, X2, B2);          // 4 X B            (2^30.01 x 2^30.01 operands)
   fe29_mul_small(E, A, 3);      // 3 X^2, normalised: it is squared next
-  fe29_sqr(F, E);
   fe29_add(Z2, a.z, a.z);
   fe29_mul(r.z, a.y, Z2);       // Z3 = 2 Y Z
+#ifdef HLC_FUSED_SUB_OFF        // A/B: F = E^2 reduced, then a carried subtraction
+  fe29 F;
+  fe29_sqr(F, E);
   fe29_sub2(r.x, F, D, D);      // X3 = F - 2D
+#else
+  {
+    uint32_t f[9];
+    fe29_neg_addend(f, D, D);
+    fe29_sqr_add(r.x, E, f);    // X3 = E^2 + (128p - 2D): one reduction
+  }
+#endif
   fe29_sub_lazy(t, D, r.x);     // D - X3, lazy: multiplies the normalised E
 #ifdef HLC_DBL_SQR_C4           // A/B: C4 = (2B)^2 squared and subtracted after a separate product
   fe29 C4, M;
@@ -92,10 +101,18 @@ HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullp
   }
   fe29 z1z1, u2, s2, h, rr, hh, i4, j, v, h2, z3, x3, t, y3, y1j;
   fe29_sqr(z1z1, a.z);
+#ifdef HLC_FUSED_SUB_OFF
   fe29_mul(u2, b.x, z1z1);
+  fe29_sub(h, u2, a.x);
+#else
+  {
+    uint32_t f[9];
+    fe29_neg_addend(f, a.x, fe29{});
+    fe29_mul_add(h, b.x, z1z1, f);  // H = U2 - X1 = x2 Z1^2 + (128p - X1): one reduction
+  }
+#endif
   fe29_mul(s2, b.y, a.z);
   fe29_mul(s2, s2, z1z1);
-  fe29_sub(h, u2, a.x);
   fe29_sub_lazy(rr, s2, a.y);      // S2 - Y1, lazy
   if (EXACT && fe29_is_zero_modp(h)) {
     fe29_norm(rr);
@@ -116,8 +133,20 @@ HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullp
   fe29_shl(i4, hh, 2);             // I = 4 HH, lazy (< 2^31.01)
   fe29_mul(j, h, i4);              // J = H I
   fe29_mul(v, a.x, i4);            // V = X1 I
+#ifdef HLC_FUSED_SUB_OFF
   fe29_sqr(x3, rr);
   fe29_sub_b2c(x3, x3, j, v);      // X3 = R^2 - J - 2V
+#else
+  {
+    uint32_t f[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      FE29_CHECK((uint64_t)j.v[i] + 2ull * v.v[i] <= k29(i));
+      f[i] = k29(i) - j.v[i] - v.v[i] - v.v[i];
+    }
+    fe29_sqr_add(x3, rr, f);       // X3 = R^2 + (128p - J - 2V): one reduction
+  }
+#endif
   fe29_sub_lazy(t, v, x3);         // V - X3, lazy: multiplies the normalised R
 #ifdef HLC_MADD_TWO_REDUCTIONS     // A/B: the two products reduced separately, then subtracted
   fe29_mul(y3, rr, t);
@@ -147,19 +176,25 @@ HLC_HD void gej29_madd_zr(gej29& a, const ge29& b, fe29& zr) { gej29_madd<false>
 // (2i+1) R = (2i-1) R + 2R with b = 2R; needs a != +-b (distinct, non-opposite multiples of a
 // point of prime order).
 HLC_HD void gej29_zaddu(ge29& a, ge29& b, fe29& zr) {
-  fe29 A, B, C, u, D, t, E, X3, Y3;
+  fe29 A, B, C, u, t, E, X3, Y3;
   fe29_sub(zr, a.x, b.x);          // X2 - X1 (normalised: squared next)
   fe29_sqr(A, zr);
   fe29_mul(B, b.x, A);             // b.x in the new frame
   fe29_mul(C, a.x, A);
   fe29_sub(u, a.y, b.y);           // Y2 - Y1
-  fe29_sqr(D, u);
   fe29_sub_lazy(t, C, B);
   fe29_mul(E, b.y, t);             // b.y in the new frame
-  fe29_sub2(X3, D, B, C);          // X3 = (Y2 - Y1)^2 - B - C
+  {
+    uint32_t f[9];
+    fe29_neg_addend(f, B, C);
+    fe29_sqr_add(X3, u, f);        // X3 = (Y2 - Y1)^2 - B - C, one reduction
+  }
   fe29_sub_lazy(t, B, X3);
-  fe29_mul(Y3, u, t);
-  fe29_sub(Y3, Y3, E);             // Y3 = (Y2 - Y1)(B - X3) - E
+  {
+    uint32_t f[9];
+    fe29_neg_addend(f, E, fe29{});
+    fe29_mul_add(Y3, u, t, f);     // Y3 = (Y2 - Y1)(B - X3) - E, one reduction
+  }
   a.x = X3;
   a.y = Y3;
   b.x = B;

@@ -37,11 +37,14 @@ def column(em, prods, acc, first_zero, sd):
         em(f"v_mad_u64_u32 {acc}, {sd}, {x}, {y}, {addend}")
 
 
-def gen(square, tag="", base=0, dual=False):
+def gen(square, tag="", base=0, dual=False, plus=False):
     """One product's instruction list.  tag prefixes the operand names, base the fixed registers
     (v[base .. base+5]) so that two independent products can be interleaved (gen_dual).
     dual: a*b + c*e in one column schedule (both products accumulate into the same 64-bit columns,
-    one split / fold / carry pass for the sum)."""
+    one split / fold / carry pass for the sum).
+    plus: a*b + f for a nine-limb f (limbs < 2^32, e.g. 128p - c): f_j enters low column j as one
+    more v_mad_u64_u32 by the inline constant 1, so a product and a following subtraction share
+    one reduction (no separate carry pass)."""
     em = Em()
     A = lambda i: f"%[{tag}a{i}]"
     B = (lambda i: f"%[{tag}a{i}]") if square else (lambda i: f"%[{tag}b{i}]")
@@ -50,6 +53,7 @@ def gen(square, tag="", base=0, dual=False):
     R = lambda j: f"%[{tag}r{j}]"
     C = lambda i: f"%[{tag}c{i}]"    # dual: the second product's operands
     E = lambda i: f"%[{tag}e{i}]"
+    F = lambda j: f"%[{tag}f{j}]"    # addend limbs
     v = lambda k: f"v{base + k}"
     acc1, acc2, tt = f"v[{base}:{base + 1}]", f"v[{base + 2}:{base + 3}]", f"v[{base + 4}:{base + 5}]"
     sd = f"%[{tag}sd]"
@@ -92,6 +96,8 @@ def gen(square, tag="", base=0, dual=False):
             else:
                 addend = "0" if (t == 0 and q == 0) else acc2
                 em(f"v_mad_u64_u32 {acc2}, {sd}, {x}, {y}, {addend}")
+        if plus:
+            em(f"v_mad_u64_u32 {acc2}, {sd}, {F(t)}, 1, {acc2}")
         if t <= 7:
             em(f"v_and_b32 {H(t)}, 0x1fffffff, {v(0)}")
             em(f"v_lshrrev_b64 {acc1}, 29, {acc1}")   # after t = 7: H_17 in v0
@@ -213,6 +219,30 @@ def emit_muladd(name):
     return "".join(o)
 
 
+def emit_addend(name, square):
+    """r = a b + f or a^2 + f (mod p) for an addend f of nine limbs < 2^32 (hlc_fe29.hpp
+    fe29_mul_add_ref / fe29_sqr_add_ref are the same arithmetic)."""
+    lines = gen(square, plus=True)
+    sig = "uint32_t r[9], const uint32_t a[9]" + ("" if square else ", const uint32_t b[9]") + ", const uint32_t f[9]"
+    o = [f"// {len(lines)} instructions\n__device__ __forceinline__ void {name}({sig}) {{\n"]
+    o.append("  uint64_t sd;\n  uint32_t h[8];\n")
+    if square:
+        o.append("  uint32_t d[8];\n#pragma unroll\n  for (int i = 0; i < 8; ++i) d[i] = a[i] << 1;\n")
+    o.append("  asm volatile(\n")
+    o.append(block(lines) + "\n")
+    outs = [f'[r{j}] "=&v"(r[{j}])' for j in range(9)] + [f'[h{k}] "=&v"(h[{k}])' for k in range(8)]
+    outs += ['[sd] "=&s"(sd)']
+    ins = [f'[a{i}] "v"(a[{i}])' for i in range(9)]
+    ins += [f'[d{i}] "v"(d[{i}])' for i in range(8)] if square else [f'[b{i}] "v"(b[{i}])' for i in range(9)]
+    ins += [f'[f{i}] "v"(f[{i}])' for i in range(9)]
+    ins += ['[kfl] "s"(31264u)', '[kfh] "s"(256u)', '[kf00] "s"(256u * 31264u)', '[kf01] "s"(65536u)']
+    clob = ", ".join(f'"v{i}"' for i in range(6))
+    o.append("      : " + ", ".join(outs) + "\n")
+    o.append("      : " + ", ".join(ins) + "\n")
+    o.append("      : " + clob + ");\n}\n\n")
+    return "".join(o)
+
+
 def main():
     mul = gen(False)
     sqr = gen(True)
@@ -223,6 +253,8 @@ def main():
             + emit_dual("fe29_mul2_asm", False, False) + emit_dual("fe29_sqr2_asm", True, True)
             + emit_dual("fe29_mulsqr_asm", False, True)
             + "// sum of two products with one reduction (r = a b + c e)\n" + emit_muladd("fe29_muladd_asm")
+            + "// a product / square plus a nine-limb addend with one reduction (r = a b + f, r = a^2 + f)\n"
+            + emit_addend("fe29_mul_add_asm", False) + emit_addend("fe29_sqr_add_asm", True)
             + "}  // namespace hlc\n")
     sys.stdout.write(text)
 
