@@ -336,17 +336,39 @@ HLC_DEV void rec_u1(const fe& zraw, const uint32_t* rec, size_t stride, fe& u1, 
 }
 
 // ---- main stage helpers over the 29-bit field layer ----
+// A/B variants (timing only): -DHLC_TAB_NT_STORE / -DHLC_TAB_NT_LOAD mark the R-table traffic
+// non-temporal (nt), to see whether the table's cache allocation is what costs the clock (§4.1)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+HLC_DEV void tab_st(uint4* p, uint4 v) {
+#ifdef HLC_TAB_NT_STORE
+  const u32x4_t w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+#else
+  *p = v;
+#endif
+}
+HLC_DEV uint4 tab_ld(const uint4* p) {
+#ifdef HLC_TAB_NT_LOAD
+  const u32x4_t w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(w.x, w.y, w.z, w.w);
+#else
+  return *p;
+#endif
+}
+#define HLC_TAB_ST(p, v) tab_st((p), (v))
+#define HLC_TAB_LD(p) tab_ld(p)
 HLC_DEV void store_ge29_tab(const fe29& x, const fe29& y, uint32_t* t) {
   uint4* p = reinterpret_cast<uint4*>(t);
-  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-  p[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-  p[2] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
-  p[3] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
-  p[4] = make_uint4(y.v[7], y.v[8], 0u, 0u);
+  HLC_TAB_ST(p + 0, make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]));
+  HLC_TAB_ST(p + 1, make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]));
+  HLC_TAB_ST(p + 2, make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]));
+  HLC_TAB_ST(p + 3, make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]));
+  HLC_TAB_ST(p + 4, make_uint4(y.v[7], y.v[8], 0u, 0u));
 }
 HLC_DEV void load_ge29_tab(ge29& g, const uint32_t* t) {
   const uint4* p = reinterpret_cast<const uint4*>(t);
-  const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+  const uint4 a = HLC_TAB_LD(p + 0), b = HLC_TAB_LD(p + 1), c = HLC_TAB_LD(p + 2), d = HLC_TAB_LD(p + 3),
+              e = HLC_TAB_LD(p + 4);
   g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
   g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
   g.x.v[8] = c.x; g.y.v[0] = c.y; g.y.v[1] = c.z; g.y.v[2] = c.w;
