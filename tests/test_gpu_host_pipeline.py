@@ -1,5 +1,5 @@
-"""The pipelined host-buffer entry (hlc_validate_proposals cut into proposal chunks that alternate
-between two child contexts, hlc_api.cpp validate_pipelined) equals the one-shot path and the C
+"""The pipelined host-buffer entry (hlc_validate_proposals cut into proposal chunks that take turns
+on 2-4 child contexts, HLC_PIPE_DEPTH; hlc_api.cpp validate_pipelined) equals the one-shot path and the C
 oracle bit for bit: per-proposal results, per-vote statuses, scheme reasons and recovered
 addresses, on a Byzantine batch; also with empty proposals, votes no proposal covers (gaps between
 chunks: status 0xFF), a batch whose proposal ranges are out of order (the one-shot fallback), and
@@ -17,12 +17,15 @@ from helpers import oracle_workload
 pytestmark = pytest.mark.gpu
 
 
-def _run(engine, batch, desc, now, chunk):
+def _run(engine, batch, desc, now, chunk, depth=None):
     os.environ["HLC_PIPE_CHUNK_VOTES"] = str(chunk)
+    if depth is not None:
+        os.environ["HLC_PIPE_DEPTH"] = str(depth)
     try:
         return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
     finally:
         os.environ.pop("HLC_PIPE_CHUNK_VOTES", None)
+        os.environ.pop("HLC_PIPE_DEPTH", None)
 
 
 @pytest.fixture(scope="module")
@@ -32,11 +35,11 @@ def byz():
     return b, d, w.now
 
 
-@pytest.mark.parametrize("chunk", [100, 240, 333])
-def test_gpu_pipeline_equals_one_shot_and_oracle(engine, byz, chunk):
+@pytest.mark.parametrize("chunk,depth", [(100, 3), (240, 3), (333, 3), (100, 2), (100, 4)])
+def test_gpu_pipeline_equals_one_shot_and_oracle(engine, byz, chunk, depth):
     b, d, now = byz
     one = _run(engine, b, d, now, 0)
-    pip = _run(engine, b, d, now, chunk)
+    pip = _run(engine, b, d, now, chunk, depth)
     for x, y in zip(one, pip):
         assert np.array_equal(x, y)
     cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
