@@ -23,16 +23,45 @@ __constant__ static const uint64_t KECCAK_RC[24] = {
     0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
     0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
 
-HLC_DEV uint64_t rol64(uint64_t x, int n) { return n == 0 ? x : ((x << n) | (x >> (64 - n))); }
+// 64-bit rotate on the two 32-bit halves: two v_alignbit_b32 (the compiler's own lowering of the
+// shift-or form costs two 64-bit shifts and two ORs per rotation); n is a compile-time constant
+HLC_DEV uint64_t rol64(uint64_t x, int n) {
+  if (n == 0) return x;
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n >= 32) {
+    const uint32_t t = lo;
+    lo = hi;
+    hi = t;
+    n -= 32;
+    if (n == 0) return ((uint64_t)hi << 32) | lo;
+  }
+  const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - n);
+  const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - n);
+  return ((uint64_t)nhi << 32) | nlo;
+}
+
+// gfx950 three-input bitwise ops (v_bitop3_b32, truth table indexed by a*4 + b*2 + c) on the two
+// halves of a 64-bit lane: a ^ b ^ c (0x96) and keccak's chi a ^ (~b & c) (0xD2), one instruction
+// per half where the shift-free lowering took two
+HLC_DEV uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+  return ((uint64_t)hi << 32) | lo;
+}
+HLC_DEV uint64_t chi64(uint64_t a, uint64_t b, uint64_t c) {
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xD2);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xD2);
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // In-place keccak-f[1600]; a[x + 5y].
 HLC_DEV void keccak_f1600(uint64_t a[25]) {
   for (int round = 0; round < 24; ++round) {
-    uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20];
-    uint64_t c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];
-    uint64_t c2 = a[2] ^ a[7] ^ a[12] ^ a[17] ^ a[22];
-    uint64_t c3 = a[3] ^ a[8] ^ a[13] ^ a[18] ^ a[23];
-    uint64_t c4 = a[4] ^ a[9] ^ a[14] ^ a[19] ^ a[24];
+    uint64_t c0 = xor3_64(xor3_64(a[0], a[5], a[10]), a[15], a[20]);
+    uint64_t c1 = xor3_64(xor3_64(a[1], a[6], a[11]), a[16], a[21]);
+    uint64_t c2 = xor3_64(xor3_64(a[2], a[7], a[12]), a[17], a[22]);
+    uint64_t c3 = xor3_64(xor3_64(a[3], a[8], a[13]), a[18], a[23]);
+    uint64_t c4 = xor3_64(xor3_64(a[4], a[9], a[14]), a[19], a[24]);
     uint64_t d0 = c4 ^ rol64(c1, 1), d1 = c0 ^ rol64(c2, 1), d2 = c1 ^ rol64(c3, 1);
     uint64_t d3 = c2 ^ rol64(c4, 1), d4 = c3 ^ rol64(c0, 1);
     // theta + rho + pi into b[]
@@ -66,11 +95,11 @@ HLC_DEV void keccak_f1600(uint64_t a[25]) {
 #pragma unroll
     for (int y = 0; y < 25; y += 5) {
       uint64_t b0 = b[y], b1 = b[y + 1], b2 = b[y + 2], b3 = b[y + 3], b4 = b[y + 4];
-      a[y] = b0 ^ (~b1 & b2);
-      a[y + 1] = b1 ^ (~b2 & b3);
-      a[y + 2] = b2 ^ (~b3 & b4);
-      a[y + 3] = b3 ^ (~b4 & b0);
-      a[y + 4] = b4 ^ (~b0 & b1);
+      a[y] = chi64(b0, b1, b2);
+      a[y + 1] = chi64(b1, b2, b3);
+      a[y + 2] = chi64(b2, b3, b4);
+      a[y + 3] = chi64(b3, b4, b0);
+      a[y + 4] = chi64(b4, b0, b1);
     }
     a[0] ^= KECCAK_RC[round];
   }
