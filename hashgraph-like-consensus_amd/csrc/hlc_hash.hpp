@@ -116,6 +116,7 @@ __constant__ static const uint32_t SHA256_K[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 HLC_DEV uint32_t ror32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+HLC_DEV uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 
 HLC_DEV void sha256_init(uint32_t h[8]) {
   h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
@@ -130,15 +131,15 @@ HLC_DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
     for (int j = 0; j < 16; ++j) {
       if (r > 0) {
         uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        uint32_t s0 = ror32(w15, 7) ^ ror32(w15, 18) ^ (w15 >> 3);
-        uint32_t s1 = ror32(w2, 17) ^ ror32(w2, 19) ^ (w2 >> 10);
+        uint32_t s0 = xor3_32(ror32(w15, 7), ror32(w15, 18), w15 >> 3);
+        uint32_t s1 = xor3_32(ror32(w2, 17), ror32(w2, 19), w2 >> 10);
         w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
       }
-      uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
-      uint32_t ch = (e & f) ^ (~e & g);
+      uint32_t S1 = xor3_32(ror32(e, 6), ror32(e, 11), ror32(e, 25));
+      uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);    // e ? f : g
       uint32_t t1 = hh + S1 + ch + SHA256_K[r + j] + w[j];
-      uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
-      uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+      uint32_t S0 = xor3_32(ror32(a, 2), ror32(a, 13), ror32(a, 22));
+      uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);    // majority
       uint32_t t2 = S0 + mj;
       hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
