@@ -86,8 +86,30 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
     sc_mont_mul(rinv, prev, cur);  // r_k^-1
     sc_mont_mul(cur, cur, r);      // acc_{k-1}^-1
+#ifndef HLC_PREP_SPLIT
     rec_prep_scalars(s, rinv, parity, rec + i, n);
+#else  // A/B: the per-vote scalar work in k_rec_scalars at full occupancy (measured -0.9%, not kept)
+    store_fe_ws(rinv, rec + (size_t)REC_RINV * n + i, n);  // k_rec_scalars takes it from here
+#endif
   }
+}
+
+// ---- A/B variant -DHLC_PREP_SPLIT: prep's second half as one lane per vote at full occupancy
+// (u2 = s / r, the GLV split of u2 and its regular digits for every vote k_rec_prep inverted r for)
+// instead of inside k_rec_prep's eight-vote sequence at 1.2 waves/SIMD.  Measured -0.9%
+// (profiles/r03/ab_prep_split.txt): the latency-bound prep shares its window with the prehash, so a
+// shorter prep only hands slots from the prehash to k_rec_main sooner. ----
+__global__ void __launch_bounds__(256) k_rec_scalars(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off,
+                                                     size_t off_stride, const uint32_t* sig_len, size_t len_stride,
+                                                     uint32_t* rec) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe r, s, rinv;
+  int parity, code;
+  if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code) || code != SCHEME_NONE)
+    return;  // flags already hold the skip / scheme code
+  load_fe_ws(rinv, rec + (size_t)REC_RINV * n + i, n);
+  rec_prep_scalars(s, rinv, parity, rec + i, n);
 }
 
 // ---- main: decompress + u2 R, one vote per lane at a time (persistent grid) ----
@@ -426,6 +448,10 @@ void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
   const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
   hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, bytes, sig_off, off_stride, sig_len,
                      len_stride, b.rec, b.pfx, b.ctr);
+#ifdef HLC_PREP_SPLIT
+  hipLaunchKernelGGL(k_rec_scalars, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, bytes, sig_off, off_stride,
+                     sig_len, len_stride, b.rec);
+#endif
 }
 
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
