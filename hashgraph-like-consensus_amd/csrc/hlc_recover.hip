@@ -235,7 +235,11 @@ __global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_comb(uint64_t n
   store_fe_ws(qz, q + (size_t)16 * n + i, n);
 }
 
-// ---- final: batched Z^-1 (one safegcd per REC_BATCH votes) and affine Q, then (k_rec_addr, one
+#ifndef HLC_FIN_BATCH
+#define HLC_FIN_BATCH REC_BATCH
+#endif
+constexpr int FIN_BATCH = HLC_FIN_BATCH;  // votes per lane (one inversion) in k_rec_final
+// ---- final: batched Z^-1 (one safegcd per FIN_BATCH votes) and affine Q, then (k_rec_addr, one
 // lane per vote at full occupancy) keccak of X || Y and the owner compare.  Split in two because
 // the eight keccak-f of a lane's batch made k_rec_final one long dependent chain per lane at ~1.2
 // waves/SIMD (latency-bound); the address stage runs 8x as many waves. ----
@@ -246,7 +250,7 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, 
   fe acc;
   fe_set(acc, 1);
 #pragma unroll 1
-  for (int k = 0; k < REC_BATCH; ++k) {
+  for (int k = 0; k < FIN_BATCH; ++k) {
     const uint64_t i = t + (uint64_t)k * L;
     if (i >= n) break;
     if ((pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
@@ -258,7 +262,7 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, 
   fe cur;
   fe_inv(cur, acc);
 #pragma unroll 1
-  for (int k = REC_BATCH - 1; k >= 0; --k) {
+  for (int k = FIN_BATCH - 1; k >= 0; --k) {
     const uint64_t i = t + (uint64_t)k * L;
     if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
     fe x, y, z, prev, zi, zi2, zi3;
@@ -404,8 +408,8 @@ inline unsigned blocks_for(uint64_t n, int tpb) { return (unsigned)((n + tpb - 1
 uint64_t recover_scratch_words() { return SCRATCH_WORDS; }
 
 uint64_t recover_work_words(uint64_t n) {
-  const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH;
-  return n * (uint64_t)(REC_WORDS + Q_WORDS) + L * REC_BATCH * 8 + (n + 3) / 4 + 64;
+  const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH, Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
+  return n * (uint64_t)(REC_WORDS + Q_WORDS) + std::max(L * REC_BATCH, Lf * FIN_BATCH) * 8 + (n + 3) / 4 + 64;
 }
 
 uint64_t recover_grid_lanes() {
@@ -434,7 +438,8 @@ RecBufs rec_bufs(uint64_t n, uint32_t* work) {
   b.q = b.rec + n * (uint64_t)REC_WORDS;
   b.pfx = b.q + n * (uint64_t)Q_WORDS;
   b.L = (n + REC_BATCH - 1) / REC_BATCH;
-  b.mst = reinterpret_cast<uint8_t*>(b.pfx + b.L * REC_BATCH * 8);  // n bytes
+  const uint64_t Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
+  b.mst = reinterpret_cast<uint8_t*>(b.pfx + std::max(b.L * REC_BATCH, Lf * FIN_BATCH) * 8);  // n bytes
   // k_rec_main's work counter: 8-byte aligned inside the 64-word tail of recover_work_words(n)
   b.ctr = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(b.mst + n) + 7) & ~uintptr_t(7));
   return b;
@@ -470,11 +475,12 @@ void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_dig
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact) {
   if (!n) return;
   const RecBufs b = rec_bufs(n, work);
-  const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
+  const uint64_t Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
+  const unsigned fb = (unsigned)((Lf + PREP_TPB - 1) / PREP_TPB);
   const unsigned vb = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(k_rec_comb, dim3(vb), dim3(256), 0, s, n, pre, z_digest, gcomb, verify_out, b.rec, b.q, b.mst,
                      force_exact);
-  hipLaunchKernelGGL(k_rec_final, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, pre, verify_out, b.q, b.pfx);
+  hipLaunchKernelGGL(k_rec_final, dim3(fb), dim3(PREP_TPB), 0, s, n, Lf, pre, verify_out, b.q, b.pfx);
   hipLaunchKernelGGL(k_rec_addr, dim3(vb), dim3(256), 0, s, n, pre, bytes, id_off, off_stride, verify_out, b.q,
                      addr_out);
 }
