@@ -760,11 +760,18 @@ struct PipeTrace {
                    k ? ", " : "", r.wait0, r.wait1, r.check1, r.stage1, r.enq1, el(r.a), el(r.b), el(r.c), el(r.d));
     }
     std::fprintf(stderr, "]}\n");
+    release();
+  }
+  // also on an early error return of the traced call
+  void release() {
     for (auto& r : rows)
       for (hipEvent_t e : {r.a, r.b, r.c, r.d})
         if (e) (void)hipEventDestroy(e);
+    rows.clear();
     if (e0) (void)hipEventDestroy(e0);
+    e0 = nullptr;
   }
+  ~PipeTrace() { release(); }
 };
 
 int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,

@@ -99,6 +99,7 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
 // instead of inside k_rec_prep's eight-vote sequence at 1.2 waves/SIMD.  Measured -0.9%
 // (profiles/r03/ab_prep_split.txt): the latency-bound prep shares its window with the prehash, so a
 // shorter prep only hands slots from the prehash to k_rec_main sooner. ----
+#ifdef HLC_PREP_SPLIT
 __global__ void __launch_bounds__(256) k_rec_scalars(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off,
                                                      size_t off_stride, const uint32_t* sig_len, size_t len_stride,
                                                      uint32_t* rec) {
@@ -111,6 +112,7 @@ __global__ void __launch_bounds__(256) k_rec_scalars(uint64_t n, const uint8_t* 
   load_fe_ws(rinv, rec + (size_t)REC_RINV * n + i, n);
   rec_prep_scalars(s, rinv, parity, rec + i, n);
 }
+#endif
 
 // ---- main: decompress + u2 R, one vote per lane at a time (persistent grid) ----
 // Needs only the prep stage's records and the signatures, not the prehash: it runs beside the
