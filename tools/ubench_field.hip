@@ -420,6 +420,30 @@ __global__ void k_check29(uint32_t* bad, int rounds) {
     fe29_mul2(x2, a, b, y2, b, a);
     fe29_mul_ref(xr, a, b);
     for (int i = 0; i < 9; ++i) d |= (x2.v[i] ^ xr.v[i]) | (y2.v[i] ^ xr.v[i]);
+    // round 3: sum of two products (operands < 2^29: 18 products per column stay < 2^64) and a
+    // product / square plus a 32-bit-limb addend
+    fe29 c, e;
+    uint32_t f[9];
+    for (int i = 0; i < 9; ++i) {
+      const uint32_t hc = hash32(t * 71u + r * 613u + i + 200), he = hash32(t * 53u + r * 389u + i + 300);
+      c.v[i] = mode == 0 ? M29 - (hc & 3u) : hc & M29;
+      e.v[i] = mode <= 1 ? M29 - (he & 3u) : he & M29;
+      f[i] = mode == 3 ? 0xFFFFFFFFu - (hc & 7u) : hash32(he + i);
+    }
+    fe29 am, bm;
+    for (int i = 0; i < 9; ++i) {
+      am.v[i] = a.v[i] & M29;
+      bm.v[i] = b.v[i] & M29;
+    }
+    fe29_muladd(x, am, bm, c, e);
+    fe29_muladd_ref(y, am, bm, c, e);
+    for (int i = 0; i < 9; ++i) d |= x.v[i] ^ y.v[i];
+    fe29_mul_add(x, a, b, f);
+    fe29_mul_add_ref(y, a, b, f, false);
+    for (int i = 0; i < 9; ++i) d |= x.v[i] ^ y.v[i];
+    fe29_sqr_add(x, a, f);
+    fe29_mul_add_ref(y, a, a, f, true);
+    for (int i = 0; i < 9; ++i) d |= x.v[i] ^ y.v[i];
     if (d) atomicAdd(bad, 1u);
   }
 }
@@ -519,7 +543,7 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(k_check29, dim3(blocks), dim3(TPB), 0, 0, d, 64);
   uint32_t bad = 0;
   CHECK(hipMemcpy(&bad, d, 4, hipMemcpyDeviceToHost));
-  printf("fe29 asm vs C++ reference: %u mismatching lanes of %d (x64 rounds, mul + sqr)\n", bad, blocks * TPB);
+  printf("fe29 asm vs C++ reference: %u mismatching lanes of %d (x64 rounds, mul + sqr + dual schedules + muladd + mul_add + sqr_add)\n", bad, blocks * TPB);
   CHECK(hipFree(d));
   return bad ? 1 : 0;
 }
