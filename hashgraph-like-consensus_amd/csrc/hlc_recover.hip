@@ -14,13 +14,14 @@ namespace {
 constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
 #ifndef HLC_REC_MIN_WAVES
 // __launch_bounds__ minimum waves per SIMD for k_rec_main: a ceiling on the registers the allocator
-// may take (512 / waves, in steps of 8).  3 waves beat a grid capped at 2 by 5-6% and a forced 4
-// (spills) by 2% (profiles/r02_ab_main_waves_split.txt).  Left to itself (a floor of 2) the
-// allocator takes 174 VGPRs since the doubling's Y3 became one sum of two products (fe29_muladd),
-// one step past 3 waves; with the floor at 3 it fits 168, spilling two 8-byte values that are
-// stored once and reloaded outside the chains.  The grid is sized from the occupancy API
+// may take (512 / waves, in steps of 8).  At 2 the allocator takes 174 VGPRs (no spills) and the
+// kernel RUNS at 2 waves per SIMD; a floor of 3 fits 168 VGPRs with two 8-byte spills outside the
+// chains.  Round 3 (one-reduction sums of products, bitop3 hashes): 2 waves beat 3 by 2.0% on one
+// box (profiles/r03/ab_occupancy_r03.txt) -- 131k lanes' R tables (239 MB) fit the 256 MB Infinity
+// Cache, 197k lanes' (358 MB) do not.  In round 2, before those changes, 3 beat a grid capped at 2
+// by 5-6% (profiles/r02_ab_main_waves_split.txt).  The grid is sized from the occupancy API
 // (recover_grid_lanes), so it follows whatever the build reaches.
-#define HLC_REC_MIN_WAVES 3
+#define HLC_REC_MIN_WAVES 2
 #endif
 
 // ---- prep: parse + batched r^-1 + scalars (REC_BATCH votes per lane, one safegcd) ----
