@@ -139,7 +139,15 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
   const uint64_t tws = tid;
 #endif
   uint32_t* ws = scratch + tws;
-  uint32_t* tab = scratch + (size_t)IL_WORDS * lanes + (size_t)tws * RTAB_WORDS;
+  rtab29 tab;
+  tab.g = scratch + (size_t)IL_WORDS * lanes + (size_t)tws * RTAB_WORDS;
+#if HLC_REC_LDS_ENTRIES > 0
+  static_assert(REC_TPB == RT_LDS_LS, "the LDS table is strided by the block size");
+  __shared__ uint4 s_tab[5 * RT_LDS_N * REC_TPB];
+  tab.l = s_tab + threadIdx.x;
+#else
+  tab.l = nullptr;
+#endif
 #ifdef HLC_REC_GLDS
   // per wave: the LDS-DMA staging slots of the u2 R chain's table gathers (chain_u2r29), 10 KiB
   __shared__ __attribute__((aligned(16))) uint32_t s_rt[REC_TPB / 64][RT_WAVE_WORDS];

@@ -375,6 +375,50 @@ HLC_DEV void load_ge29_tab(ge29& g, const uint32_t* t) {
   g.y.v[3] = d.x; g.y.v[4] = d.y; g.y.v[5] = d.z; g.y.v[6] = d.w;
   g.y.v[7] = e.x; g.y.v[8] = e.y;
 }
+
+// The lane's R table.  HLC_REC_LDS_ENTRIES > 0 (A/B): the first RT_LDS_N entries (multiples 1, 3,
+// ...) live in LDS instead of the workspace -- piece k (16 B) of entry e at l[(5 e + k) * RT_LDS_LS],
+// lane-strided so that a wave's b128 reads are one contiguous KiB -- and only the rest is written to
+// and gathered from the workspace.  At 2 waves per SIMD (512 lanes per CU) 160 KiB of LDS holds 4
+// entries per lane.  Table building and the rewrite into the common frame index entries uniformly;
+// only the chain's gathers branch per lane (a wave issues both the LDS and the global reads, each
+// under its lanes' mask).
+#ifndef HLC_REC_LDS_ENTRIES
+#define HLC_REC_LDS_ENTRIES 0
+#endif
+constexpr int RT_LDS_N = HLC_REC_LDS_ENTRIES;
+constexpr int RT_LDS_LS = 256;  // lanes per block of the kernel that owns the LDS table
+struct rtab29 {
+  uint32_t* g;  // the lane's RTAB_WORDS workspace words
+  uint4* l;     // the lane's first LDS piece (RT_LDS_N > 0)
+  HLC_DEV const uint32_t* gentry(int e) const { return g + RTAB_ENTRY * e; }
+  HLC_DEV void store(int e, const fe29& x, const fe29& y) const {
+    if (RT_LDS_N > 0 && e < RT_LDS_N) {
+      uint4* p = l + 5 * RT_LDS_LS * e;
+      p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+      p[RT_LDS_LS] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+      p[2 * RT_LDS_LS] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
+      p[3 * RT_LDS_LS] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
+      p[4 * RT_LDS_LS] = make_uint4(y.v[7], y.v[8], 0u, 0u);
+    } else {
+      store_ge29_tab(x, y, g + RTAB_ENTRY * e);
+    }
+  }
+  HLC_DEV void load(ge29& q, int e) const {
+    if (RT_LDS_N > 0 && e < RT_LDS_N) {
+      const uint4* p = l + 5 * RT_LDS_LS * e;
+      const uint4 a = p[0], b = p[RT_LDS_LS], c = p[2 * RT_LDS_LS], d = p[3 * RT_LDS_LS], f = p[4 * RT_LDS_LS];
+      q.x.v[0] = a.x; q.x.v[1] = a.y; q.x.v[2] = a.z; q.x.v[3] = a.w;
+      q.x.v[4] = b.x; q.x.v[5] = b.y; q.x.v[6] = b.z; q.x.v[7] = b.w;
+      q.x.v[8] = c.x; q.y.v[0] = c.y; q.y.v[1] = c.z; q.y.v[2] = c.w;
+      q.y.v[3] = d.x; q.y.v[4] = d.y; q.y.v[5] = d.z; q.y.v[6] = d.w;
+      q.y.v[7] = f.x; q.y.v[8] = f.y;
+    } else {
+      load_ge29_tab(q, g + RTAB_ENTRY * e);
+    }
+  }
+};
+
 HLC_DEV void store_fe29_ws(const fe29& x, uint32_t* ws, size_t stride) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) ws[(size_t)i * stride] = x.v[i];
@@ -443,7 +487,7 @@ HLC_DEV void wait_glds() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // regular signed digits of the GLV halves b1, b2 (b2 against lambda R = (beta x, y)).
 // lds: this wave's RT_WAVE_WORDS staging words (HLC_REC_GLDS only).
 template <bool EXACT>
-HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const uint32_t* tab, const fe29& zg,
+HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const rtab29& tab, const fe29& zg,
                          uint32_t* lds) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
@@ -456,11 +500,13 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
   auto word_at = [&](int win, int k) { return dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride]; };
   auto digit_at = [&](int win, int k) { return digit16(word_at(win, k), win & 1); };
 #ifdef HLC_PROBE_HOT_GATHER
-  auto entry_of = [&](int d) { return tab; };  // timing probe only (wrong results): no table traffic
+  auto index_of = [&](int d) { return 0; };  // timing probe only (wrong results): no table traffic
 #else
-  auto entry_of = [&](int d) { return tab + RTAB_ENTRY * (((d < 0 ? -d : d) - 1) >> 1); };
+  auto index_of = [&](int d) { return ((d < 0 ? -d : d) - 1) >> 1; };
 #endif
+  auto entry_of = [&](int d) { return tab.gentry(index_of(d)); };
 #ifdef HLC_REC_GLDS
+  static_assert(RT_LDS_N == 0, "the LDS-DMA staging variant gathers every entry from the workspace");
   const unsigned lane = threadIdx.x & 63u;
   uint32_t* s1 = lds;
   uint32_t* s2 = lds + RT_SLOT;
@@ -504,15 +550,15 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
     if (win != M_R - 1) {
 #pragma unroll 1
       for (int q = 0; q < W_R - 1; ++q) gej29_double(acc, acc);
-      load_ge29_tab(g, entry_of(d));
+      tab.load(g, index_of(d));
       gej29_double(acc, acc);
     } else {
-      load_ge29_tab(g, entry_of(d));
+      tab.load(g, index_of(d));
     }
     // the b2 entry is loaded before the b1 addition: its gather latency hides behind that addition
     const int d2 = digit_at(win, 1);
     ge29 g2;
-    load_ge29_tab(g2, entry_of(d2));
+    tab.load(g2, index_of(d2));
     fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 1) != 0));
     gej29_madd<EXACT>(acc, acc, g);
     g = g2;
@@ -526,7 +572,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
   for (int k = 0; k < 2; ++k) {
     if (((skews >> k) & 1) == 0) continue;
     ge29 g;
-    load_ge29_tab(g, tab);
+    tab.load(g, 0);
     if (k == 1) fe29_mul_uniform(g.x, g.x, beta);
     fe29_cneg_lazy(g.y, g.y, ((negs >> k) & 1) == 0);
     gej29_madd<EXACT>(acc, acc, g);
@@ -541,7 +587,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const u
 // when its own Z comes out zero (the unchecked chain is exact whenever its Z is non-zero, so this
 // is the combined stage's test split per chain).
 HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz, bool& inf,
-                      uint32_t* ws, size_t ws_stride, uint32_t* tab, bool force_exact, uint32_t* lds) {
+                      uint32_t* ws, size_t ws_stride, const rtab29& tab, bool force_exact, uint32_t* lds) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int parity = (int)((flags >> 5) & 1u);
   ge29 R;
@@ -569,12 +615,12 @@ HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx,
     ge29 a;
     fe29_mul(a.x, R.x, c2);
     fe29_mul(a.y, R.y, c3);
-    store_ge29_tab(a.x, a.y, tab);
+    tab.store(0, a.x, a.y);
     uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
     for (int i = 1; i < RTAB_N; ++i) {
       fe29 zr;
       gej29_zaddu(a, dp, zr);
-      store_ge29_tab(a.x, a.y, tab + RTAB_ENTRY * i);
+      tab.store(i, a.x, a.y);
       store_fe29_ws(zr, zrws + (size_t)(9 * (i - 1)) * ws_stride, ws_stride);
     }
     fe29 sc;
@@ -586,10 +632,10 @@ HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx,
       fe29_sqr(s2, sc);
       fe29_mul(s3, s2, sc);
       ge29 e;
-      load_ge29_tab(e, tab + RTAB_ENTRY * i);
+      tab.load(e, i);
       fe29_mul(e.x, e.x, s2);
       fe29_mul(e.y, e.y, s3);
-      store_ge29_tab(e.x, e.y, tab + RTAB_ENTRY * i);
+      tab.store(i, e.x, e.y);
     }
     fe29_mul(zg, sc, d.z);
   }
