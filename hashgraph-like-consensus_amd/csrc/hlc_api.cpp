@@ -169,13 +169,25 @@ struct hlc_ctx {
   // and the next chunks' kernels overlap the previous chunks' kernels (created on first use)
   hlc_ctx* pipe[4] = {nullptr, nullptr, nullptr, nullptr};
   std::unique_ptr<HostPool> pool;  // the parent's staging workers (HLC_PIPE_THREADS)
-  // a pipeline child's staging: page-locked inputs / outputs, one device input buffer, the event
-  // after its chunk's output copy, and which chunk it holds
-  PBuf pin_in, pin_out;
-  DBuf dev_in;
-  hipEvent_t ev_done = nullptr;
-  bool busy = false;
-  uint64_t chunk_p0 = 0, chunk_p1 = 0, chunk_v0 = 0, chunk_v1 = 0;
+  // a pipeline child's staging: page-locked inputs, one device input buffer, the event after its
+  // chunk's host->device copy (the page-locked inputs are free again once it has fired)
+  PBuf pin_in;
+  DBuf dev_in, dev_out;  // a chunk's inputs; its outputs as one block (one copy back)
+  hipEvent_t ev_h2d = nullptr;
+  bool h2d_pending = false;
+  // shared-stream pipeline (HLC_PIPE_STREAMS=shared; the default is one stream pair per child): the
+  // children run on the parent's launch stream and their own aux streams, uploads on the parent's
+  // `copy` stream and the prep stages on its `pstage` stream; a child's next upload waits for ev_free
+  // (its previous chunk's kernels and output copies are done), and its prep waits for fork_wait (its
+  // upload) instead of a fork from `s`
+  hipStream_t copy = nullptr, pstage = nullptr;  // (parent) upload stream; prep-stage stream
+  hipStream_t prep_stream = nullptr;             // (child) the prep stage's stream, when not aux
+  bool borrowed_streams = false, pipe_shared = false, used = false;
+  hipEvent_t ev_free = nullptr, fork_wait = nullptr;
+  // the parent's call-wide page-locked outputs (every chunk's results land at their own offsets) and
+  // one completion event per chunk in flight
+  PBuf pipe_out;
+  std::vector<hipEvent_t> pipe_ev;
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
   DBuf in_off2, in_len2, in_off3, in_len3, in_priv, byz_key;
@@ -201,7 +213,9 @@ struct hlc_ctx {
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : rec_prep_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    if (ev_done) (void)hipEventDestroy(ev_done);
+    if (ev_h2d) (void)hipEventDestroy(ev_h2d);
+    if (ev_free) (void)hipEventDestroy(ev_free);
+    for (auto e : pipe_ev) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -362,11 +376,17 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   // HLC_PREP_FIRST=1: the prep stage runs alone on `s` before the fork, so the main stage starts as
   // soon as it is done and the prehash fills the SIMD slots beside main instead of beside prep
   const bool prep_first = c->prep_first && !c->serial_stages;
-  hipStream_t prep_s = prep_first ? s : aux;
+  // (a shared-stream pipeline child runs prep on its parent's prep-stage stream, so that chunk k+1's
+  // prep can start in chunk k's k_rec_main tail)
+  hipStream_t prep_s = prep_first ? s : (c->prep_stream && !c->serial_stages ? c->prep_stream : aux);
   if (c->serial_stages) CHK(prehash_and_chain());
   if (!c->serial_stages && !prep_first) {
-    HIPCHK(hipEventRecord(c->ev_fork, s));
-    HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
+    if (c->fork_wait) {  // shared-stream pipeline child: prep / main need only the chunk's upload
+      HIPCHK(hipStreamWaitEvent(prep_s, c->fork_wait, 0));
+    } else {
+      HIPCHK(hipEventRecord(c->ev_fork, s));
+      HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
+    }
   }
   if (c->timing) HIPCHK(hipEventRecord(p0, prep_s));
   hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
@@ -375,8 +395,8 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     HIPCHK(hipEventRecord(p1, prep_s));
     c->rec_prep_ev.emplace_back(p0, p1);
   }
-  if (prep_first) {
-    HIPCHK(hipEventRecord(c->ev_fork, s));
+  if (prep_s != aux) {  // prep ran on `s` (HLC_PREP_FIRST) or on the prep-stage stream
+    HIPCHK(hipEventRecord(c->ev_fork, prep_s));
     HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
   }
   if (c->timing) HIPCHK(hipEventRecord(r0, aux));
@@ -647,19 +667,29 @@ int stage_votes(hlc_ctx* c, const hlc_votes* v, hlc_votes* dv, hipStream_t s) {
   return 0;
 }
 
-int make_child(hlc_ctx* parent, hlc_ctx** out) {
+int make_child(hlc_ctx* parent, hlc_ctx** out, bool shared) {
   hlc_ctx* c = new hlc_ctx();
   c->device = parent->device;
   c->rec_force_exact = parent->rec_force_exact;
   c->serial_stages = parent->serial_stages;
+  if (const char* e = std::getenv("HLC_PIPE_SERIAL")) c->serial_stages = std::atoi(e) != 0;  // A/B: one stream per child
   c->prep_first = parent->prep_first;
   c->aux_prio = parent->aux_prio;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      create_aux(c) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess) {
-    hipStream_t st = c->stream, ax = c->aux;
+  c->pipe_shared = shared;
+  bool ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_h2d, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_free, hipEventDisableTiming) == hipSuccess;
+  if (ok && shared) {  // the parent's launch stream, an aux stream of its own (consecutive chunks'
+                       // k_rec_main grids overlap: the next one's waves fill the last one's tail)
+    c->stream = parent->stream;
+    c->borrowed_streams = true;
+    ok = create_aux(c) == hipSuccess;
+  } else if (ok) {
+    ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess && create_aux(c) == hipSuccess;
+  }
+  if (!ok) {
+    hipStream_t st = c->borrowed_streams ? nullptr : c->stream, ax = c->aux;
     delete c;
     if (st) (void)hipStreamDestroy(st);
     if (ax) (void)hipStreamDestroy(ax);
@@ -676,12 +706,13 @@ int make_child(hlc_ctx* parent, hlc_ctx** out) {
 
 void destroy_ctx(hlc_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
-  hipStream_t s = ctx->stream, a = ctx->aux;
+  for (hipStream_t x : {ctx->stream, ctx->aux, ctx->copy, ctx->pstage})
+    if (x) (void)hipStreamSynchronize(x);
+  hipStream_t s = ctx->borrowed_streams ? nullptr : ctx->stream, a = ctx->aux, cp = ctx->copy, ps = ctx->pstage;
+  // (a shared-stream child's launch stream belongs to its parent)
   delete ctx;
-  if (s) (void)hipStreamDestroy(s);
-  if (a) (void)hipStreamDestroy(a);
+  for (hipStream_t x : {s, a, cp, ps})
+    if (x) (void)hipStreamDestroy(x);
 }
 
 // Votes per pipeline chunk (HLC_PIPE_CHUNK_VOTES overrides; 0 disables the pipeline).
@@ -701,6 +732,16 @@ int pipe_threads() {
   return std::max(1, std::min(t, 64));
 }
 
+// The pipeline children run each on its own stream pair (default) or all on the parent's streams
+// with a separate upload stream (HLC_PIPE_STREAMS=shared, A/B).  Shared streams avoid the runtime's
+// mapping of many streams onto four hardware queues (rocprofv3 showed one child's prehash queued
+// behind another child's k_rec_main), but they also serialise the chunks' recovery stages: measured
+// slower (profiles/r03/host_pipe_v2.txt).
+bool pipe_shared_streams() {
+  const char* e = std::getenv("HLC_PIPE_STREAMS");
+  return e && std::strcmp(e, "shared") == 0;
+}
+
 // Child contexts of the pipeline, i.e. chunks in flight (HLC_PIPE_DEPTH, default 3, 2..4).
 int pipe_depth() {
   const char* e = std::getenv("HLC_PIPE_DEPTH");
@@ -715,17 +756,19 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // the layout of prost-decoded / packed batches; any other layout returns *used = false and takes the
 // one-shot path).  Chunk k runs on child context pipe[k % D] (own streams and workspace; D =
 // pipe_depth(), 3 by default):
-//   host   : wait for the child's previous chunk (k-D) and copy its outputs out of page-locked
-//            memory; check chunk k's fields and copy its SoA slices, proposals and arena span into
-//            the child's page-locked staging buffer (the pool's threads);
-//   device : one H2D DMA of the staging buffer, the validate-many kernels, the outputs' D2H into
-//            page-locked memory, an event -- all asynchronous on the child's stream.
-// So while the host stages chunk k, the device runs chunks k-D+1 .. k-1: copies, checks and kernels
-// overlap, and the children's grids fill each other's tails.  With D = 2 the host had to wait for
-// chunk k-2 before staging chunk k, and the device ran dry at every pair boundary (HLC_PIPE_TRACE:
-// ~0.4 ms idle per 131k votes); D = 3 keeps a staged chunk queued behind the two running ones.
+//   host   : wait until the child's previous chunk (k-D) has been UPLOADED (its page-locked inputs
+//            are free again; its kernels may still run); check chunk k's fields and copy its SoA
+//            slices, proposals and arena span into the child's page-locked staging buffer (the
+//            pool's threads); after enqueueing, copy out every earlier chunk whose event has fired;
+//   device : one H2D DMA of the staging buffer, the validate-many kernels, the outputs' D2H into the
+//            call-wide page-locked output buffer at the chunk's offsets, an event -- all asynchronous
+//            on the child's stream (stream order keeps chunk k's upload behind chunk k-D's kernels).
+// So the host never waits for a chunk's kernels: it runs up to 2D chunks ahead of the device, and the
+// device finds the next chunk uploaded when it finishes one.  (The round-3 first version waited for
+// chunk k-D's outputs before staging chunk k -- the device then ran dry whenever the host was
+// blocked: HLC_PIPE_TRACE showed ~0.4-1 ms idle gaps.)
 // HLC_PIPE_TRACE=1: one JSON line per pipelined call on stderr -- per chunk the host phases (wait for
-// the child's previous chunk, field checks, staging copies, enqueue) and the device spans (H2D, kernels,
+// the child's inputs, field checks, staging copies, enqueue) and the device spans (H2D, kernels,
 // D2H) from timing events, all in ms from the call's start (tools/host_pipe.py --trace)
 struct PipeTrace {
   using clk = std::chrono::steady_clock;
@@ -733,7 +776,7 @@ struct PipeTrace {
   clk::time_point t0;
   hipEvent_t e0 = nullptr;
   struct Row {
-    double wait0, wait1, check1, stage1, enq1;
+    double wait0, wait1, check1, stage1, h2d1, kern1, enq1;  // host times
     hipEvent_t a, b, c, d;  // before H2D, after H2D, after the kernels, after D2H
   };
   std::vector<Row> rows;
@@ -755,9 +798,10 @@ struct PipeTrace {
     for (size_t k = 0; k < rows.size(); ++k) {
       const Row& r = rows[k];
       std::fprintf(stderr,
-                   "%s{\"wait\": [%.3f, %.3f], \"check_end\": %.3f, \"stage_end\": %.3f, \"enq_end\": %.3f, "
-                   "\"h2d\": [%.3f, %.3f], \"kern_end\": %.3f, \"d2h_end\": %.3f}",
-                   k ? ", " : "", r.wait0, r.wait1, r.check1, r.stage1, r.enq1, el(r.a), el(r.b), el(r.c), el(r.d));
+                   "%s{\"wait\": [%.3f, %.3f], \"check_end\": %.3f, \"stage_end\": %.3f, \"enq_h2d_end\": %.3f, "
+                   "\"enq_kern_end\": %.3f, \"enq_end\": %.3f, \"h2d\": [%.3f, %.3f], \"kern_end\": %.3f, \"d2h_end\": %.3f}",
+                   k ? ", " : "", r.wait0, r.wait1, r.check1, r.stage1, r.h2d1, r.kern1, r.enq1, el(r.a), el(r.b), el(r.c),
+                   el(r.d));
     }
     std::fprintf(stderr, "]}\n");
     release();
@@ -805,8 +849,17 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     if (ch[k].v0 < ch[k - 1].v1) return 0;  // interleaved vote ranges: one-shot path
   if (ch.size() < 2) return 0;
   const int depth = pipe_depth();
+  const bool shared = pipe_shared_streams();
+  for (auto& w : c->pipe)
+    if (w && w->pipe_shared != shared) {
+      destroy_ctx(w);
+      w = nullptr;
+    }
   for (int k = 0; k < depth; ++k)
-    if (!c->pipe[k]) CHK(make_child(c, &c->pipe[k]));
+    if (!c->pipe[k]) CHK(make_child(c, &c->pipe[k], shared));
+  if (shared && !c->copy) HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+  if (shared && !c->pstage) HIPCHK(hipStreamCreateWithFlags(&c->pstage, hipStreamNonBlocking));
+  for (int k = 0; k < depth; ++k) c->pipe[k]->prep_stream = shared ? c->pstage : nullptr;
   if (!c->pool || c->pool->parts() != pipe_threads()) c->pool.reset(new HostPool(pipe_threads() - 1));
   HostPool& pool = *c->pool;
   *used = true;
@@ -816,40 +869,66 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     (void)hipEventRecord(tr.e0, c->pipe[0]->stream);
   }
 
-  // output layout in a child's pin_out: results | status | reason | recovered
-  auto out_layout = [&](uint64_t nv, uint64_t npk, size_t o[4]) {
-    o[0] = 0;
-    o[1] = al256(npk * sizeof(hlc_result));
-    o[2] = o[1] + al256(nv);
-    o[3] = o[2] + al256(nv);
-    return o[3] + (out_rec ? nv * 20 : 0);
+  // call-wide page-locked outputs: one block per chunk, [results | status | reason | recovered],
+  // so each chunk's outputs come back in one copy and no chunk waits for an earlier one's to be
+  // copied out
+  auto blk_layout = [&](const Chunk& q, size_t r[4]) {
+    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
+    r[0] = 0;  // (one spare element each, as the one-shot path's buffers)
+    r[1] = al256((npk + 1) * sizeof(hlc_result));
+    r[2] = r[1] + al256(nv + 1);
+    r[3] = r[2] + al256(nv + 1);
+    return r[3] + (out_rec ? al256(nv * 20 + 20) : 0);
   };
-  auto copy_out = [&](hlc_ctx* w) -> int {
-    if (!w->busy) return 0;
-    HIPCHK(hipEventSynchronize(w->ev_done));
-    w->busy = false;
-    const uint64_t nv = w->chunk_v1 - w->chunk_v0, npk = w->chunk_p1 - w->chunk_p0;
-    size_t o[4];
-    out_layout(nv, npk, o);
-    std::memcpy(out_res + w->chunk_p0, w->pin_out.at(o[0]), npk * sizeof(hlc_result));
-    if (out_st) std::memcpy(out_st + w->chunk_v0, w->pin_out.at(o[1]), nv);
-    if (out_rs) std::memcpy(out_rs + w->chunk_v0, w->pin_out.at(o[2]), nv);
-    if (out_rec) std::memcpy(out_rec + 20 * w->chunk_v0, w->pin_out.at(o[3]), nv * 20);
-    return 0;
+  std::vector<size_t> blk_off(ch.size() + 1, 0);
+  for (size_t k = 0; k < ch.size(); ++k) {
+    size_t r[4];
+    blk_off[k + 1] = blk_off[k] + blk_layout(ch[k], r);
+  }
+  CHK(c->pipe_out.ensure(blk_off[ch.size()] + 16));
+  while (c->pipe_ev.size() < ch.size()) {
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->pipe_ev.push_back(e);
+  }
+  // chunk k's outputs -> the caller's buffers (after its event), on the pool
+  auto copy_out = [&](size_t k) {
+    const Chunk& q = ch[k];
+    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
+    size_t r[4];
+    blk_layout(q, r);
+    const uint8_t* src = c->pipe_out.at(blk_off[k]);
+    pool.run([&](int t, int T) {
+      const uint64_t b0 = npk * t / T, b1 = npk * (t + 1) / T, a0 = nv * t / T, a1 = nv * (t + 1) / T;
+      if (b1 > b0)
+        std::memcpy(out_res + q.p0 + b0, src + r[0] + b0 * sizeof(hlc_result), (b1 - b0) * sizeof(hlc_result));
+      if (a1 > a0) {
+        if (out_st) std::memcpy(out_st + q.v0 + a0, src + r[1] + a0, a1 - a0);
+        if (out_rs) std::memcpy(out_rs + q.v0 + a0, src + r[2] + a0, a1 - a0);
+        if (out_rec) std::memcpy(out_rec + 20 * (q.v0 + a0), src + r[3] + 20 * a0, 20 * (a1 - a0));
+      }
+    });
   };
   auto drain = [&]() {
+    for (hipStream_t x : {c->stream, c->aux, c->copy, c->pstage})
+      if (x) (void)hipStreamSynchronize(x);
     for (hlc_ctx* p : c->pipe) {
       if (!p) continue;
       (void)hipStreamSynchronize(p->stream);
-      p->busy = false;
+      (void)hipStreamSynchronize(p->aux);
+      p->h2d_pending = false;
     }
   };
+  size_t next_out = 0;  // chunks [0, next_out) are in the caller's buffers
   std::vector<hlc_proposal> cp;
   for (size_t k = 0; k < ch.size(); ++k) {
     hlc_ctx* w = c->pipe[k % depth];
     PipeTrace::Row trow{};
     if (tr.on) trow.wait0 = tr.ms(PipeTrace::clk::now());
-    CHK(copy_out(w));  // its previous chunk (k - 2): also frees its staging buffers
+    if (w->h2d_pending) {  // its previous chunk's upload has left the page-locked inputs
+      HIPCHK(hipEventSynchronize(w->ev_h2d));
+      w->h2d_pending = false;
+    }
     if (tr.on) trow.wait1 = tr.ms(PipeTrace::clk::now());
     const Chunk& q = ch[k];
     const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
@@ -902,8 +981,6 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     o[8] = o[7] + (a_hi - a_lo);
     CHK(w->pin_in.ensure(o[8] + 16));
     CHK(w->dev_in.ensure(o[8] + 16));
-    size_t oo[4];
-    CHK(w->pin_out.ensure(out_layout(nv, npk, oo) + 16));
     cp.assign(props + q.p0, props + q.p1);
     for (auto& pr : cp) pr.vote_begin = pr.vote_count ? pr.vote_begin - q.v0 : 0;
     std::memcpy(w->pin_in.at(o[6]), cp.data(), npk * sizeof(hlc_proposal));
@@ -919,13 +996,24 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
       const uint64_t c0 = arena * t / T, c1 = arena * (t + 1) / T;
       if (c1 > c0) std::memcpy(w->pin_in.at(o[7] + c0), v->bytes + a_lo + c0, c1 - c0);
     });
-    hipStream_t s = w->stream;
+    // shared streams: the upload on the parent's copy stream once the child's previous chunk is done
+    // with its device inputs and workspace; the launch stream and (through fork_wait) the aux stream
+    // wait for the upload.  Own streams: all of it in order on the child's stream.
+    hipStream_t s = w->stream, cs = shared ? c->copy : w->stream;
+    if (shared && w->used) HIPCHK(hipStreamWaitEvent(cs, w->ev_free, 0));
     if (tr.on) {
       trow.stage1 = tr.ms(PipeTrace::clk::now());
-      trow.a = tr.ev(s);
+      trow.a = tr.ev(cs);
     }
-    HIPCHK(hipMemcpyAsync(w->dev_in.p, w->pin_in.p, o[8], hipMemcpyHostToDevice, s));
-    if (tr.on) trow.b = tr.ev(s);
+    HIPCHK(hipMemcpyAsync(w->dev_in.p, w->pin_in.p, o[8], hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(w->ev_h2d, cs));
+    w->h2d_pending = true;
+    if (tr.on) trow.b = tr.ev(cs);
+    if (shared) {
+      HIPCHK(hipStreamWaitEvent(s, w->ev_h2d, 0));
+      w->fork_wait = w->ev_h2d;
+    }
+    if (tr.on) trow.h2d1 = tr.ms(PipeTrace::clk::now());
     uint8_t* d = w->dev_in.as<uint8_t>();
     hlc_votes dv;
     dv.n = nv;
@@ -937,33 +1025,36 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     dv.field_len = reinterpret_cast<const uint32_t*>(d + o[5]);
     dv.bytes = d + o[7] - a_lo;  // the field offsets stay absolute: bytes + off lands in the staged span
     dv.bytes_len = a_hi;
-    CHK(w->out_res.ensure(npk * sizeof(hlc_result) + 16));
-    CHK(w->out_status.ensure(nv + 1));
-    CHK(w->out_reason.ensure(nv + 1));
-    if (out_rec) CHK(w->out_rec.ensure(nv * 20 + 20));
-    CHK(validate_device(w, &dv, reinterpret_cast<const hlc_proposal*>(d + o[6]), npk, now, w->out_res.as<hlc_result>(),
-                        w->out_status.as<uint8_t>(), w->out_reason.as<uint8_t>(),
-                        out_rec ? w->out_rec.as<uint8_t>() : nullptr, s));
-    if (tr.on) trow.c = tr.ev(s);
-    if (npk) HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[0]), w->out_res.p, npk * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
-    if (nv) {
-      HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[1]), w->out_status.p, nv, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[2]), w->out_reason.p, nv, hipMemcpyDeviceToHost, s));
-      if (out_rec) HIPCHK(hipMemcpyAsync(w->pin_out.at(oo[3]), w->out_rec.p, nv * 20, hipMemcpyDeviceToHost, s));
+    size_t r[4];
+    const size_t blk = blk_layout(q, r);
+    CHK(w->dev_out.ensure(blk + 16));
+    uint8_t* ob = w->dev_out.as<uint8_t>();
+    CHK(validate_device(w, &dv, reinterpret_cast<const hlc_proposal*>(d + o[6]), npk, now,
+                        reinterpret_cast<hlc_result*>(ob + r[0]), ob + r[1], ob + r[2], out_rec ? ob + r[3] : nullptr,
+                        s));
+    if (tr.on) {
+      trow.c = tr.ev(s);
+      trow.kern1 = tr.ms(PipeTrace::clk::now());
     }
-    HIPCHK(hipEventRecord(w->ev_done, s));
+    HIPCHK(hipMemcpyAsync(c->pipe_out.at(blk_off[k]), ob, blk, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(c->pipe_ev[k], s));
+    if (shared) {
+      HIPCHK(hipEventRecord(w->ev_free, s));
+      w->used = true;
+    }
     if (tr.on) {
       trow.d = tr.ev(s);
       trow.enq1 = tr.ms(PipeTrace::clk::now());
       tr.rows.push_back(trow);
     }
-    w->busy = true;
-    w->chunk_p0 = q.p0;
-    w->chunk_p1 = q.p1;
-    w->chunk_v0 = q.v0;
-    w->chunk_v1 = q.v1;
+    // copy out the chunks that are already done, without waiting for any
+    while (next_out < k && hipEventQuery(c->pipe_ev[next_out]) == hipSuccess) copy_out(next_out++);
   }
-  for (size_t k = ch.size(); k < ch.size() + depth; ++k) CHK(copy_out(c->pipe[k % depth]));
+  for (; next_out < ch.size(); ++next_out) {
+    HIPCHK(hipEventSynchronize(c->pipe_ev[next_out]));
+    copy_out(next_out);
+  }
+  for (int k = 0; k < depth; ++k) c->pipe[k]->h2d_pending = false;  // every chunk has completed
   if (tr.on) tr.print(n, ch.size());
   // votes between the chunks' ranges are covered by no proposal: not evaluated (as the one-shot path)
   uint64_t prev = 0;

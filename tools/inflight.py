@@ -25,6 +25,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--inflight", default="1,2")
+    ap.add_argument("--proposals", type=int, default=10_000, help="64 votes each (2048 = one 131k-vote pipeline chunk)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -34,7 +35,7 @@ def main() -> int:
     from hashgraph_like_consensus.engine import Engine
 
     engines = [Engine(0)]
-    db = DeviceBatch.synthetic(engines[0], 10_000, 64, 64, True, synth.config_seed(2))
+    db = DeviceBatch.synthetic(engines[0], a.proposals, 64, 64, True, synth.config_seed(2))
     torch.cuda.synchronize()
 
     def twin():
@@ -67,7 +68,7 @@ def main() -> int:
             engines[j].validate_proposals_device(batches[j], streams[j].cuda_stream)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        row = {"inflight": k, "steps": a.steps, "ms_per_step": el / a.steps * 1e3, "votes_per_s": db.n * a.steps / el}
+        row = {"votes": db.n, "inflight": k, "steps": a.steps, "ms_per_step": el / a.steps * 1e3, "votes_per_s": db.n * a.steps / el}
         print(json.dumps(row), flush=True)
         out.append(row)
     for e in engines:
