@@ -769,7 +769,7 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // blocked: HLC_PIPE_TRACE showed ~0.4-1 ms idle gaps.)
 // HLC_PIPE_TRACE=1: one JSON line per pipelined call on stderr -- per chunk the host phases (wait for
 // the child's inputs, field checks, staging copies, enqueue) and the device spans (H2D, kernels,
-// D2H) from timing events, all in ms from the call's start (tools/host_pipe.py --trace)
+// D2H) from timing events, all in ms from the call's start (tools/host_pipe.py --print-trace)
 struct PipeTrace {
   using clk = std::chrono::steady_clock;
   bool on = false;

@@ -7,6 +7,7 @@ in, per-vote statuses + per-proposal results out, blocking).
 
     python tools/host_pipe.py --steps 10 --chunks 0,65536,131072,262144 --depths 2,3,4
     (HLC_PIPE_TRACE=1 in the environment adds the per-chunk timeline of every call on stderr)
+    python tools/host_pipe.py --print-trace gpurun_out/trace.txt   (that timeline as a table; no GPU)
 """
 from __future__ import annotations
 
@@ -20,6 +21,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
 
 
+def print_trace(path: str) -> None:
+    """HLC_PIPE_TRACE lines (hlc_api.cpp PipeTrace) as one row per chunk: host phases (wait for the
+    child's inputs, staging end, enqueue ends) | device spans (H2D, kernels end, D2H end), ms."""
+    for line in open(path):
+        if not line.startswith("HLC_PIPE_TRACE "):
+            continue
+        d = json.loads(line[len("HLC_PIPE_TRACE "):])
+        print(f"{d['votes']} votes, {d['chunks']} chunks, host {d['host_ms']:.2f} ms")
+        for r in d["rows"]:
+            print(f"  wait {r['wait'][0]:6.2f}-{r['wait'][1]:6.2f} stage {r['stage_end']:6.2f} "
+                  f"enq {r.get('enq_h2d_end', -1):6.2f}/{r.get('enq_kern_end', -1):6.2f}/{r['enq_end']:6.2f} | "
+                  f"h2d {r['h2d'][0]:6.2f}-{r['h2d'][1]:6.2f} kern_end {r['kern_end']:6.2f} d2h_end {r['d2h_end']:6.2f}")
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
@@ -27,7 +42,11 @@ def main() -> int:
     ap.add_argument("--threads", default="4", help="HLC_PIPE_THREADS settings to sweep")
     ap.add_argument("--depths", default="3", help="HLC_PIPE_DEPTH settings to sweep (child contexts in flight)")
     ap.add_argument("--proposals", type=int, default=10_000)
+    ap.add_argument("--print-trace", default=None, help="print an HLC_PIPE_TRACE log as a table and exit")
     a = ap.parse_args()
+    if a.print_trace:
+        print_trace(a.print_trace)
+        return 0
     import numpy as np
     import torch
 
