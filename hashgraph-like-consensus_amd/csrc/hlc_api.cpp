@@ -725,6 +725,16 @@ struct Chunk {
   uint64_t p0, p1, v0, v1;
 };
 
+// Votes in the pipeline's first chunk (HLC_PIPE_FIRST_CHUNK_VOTES; default: half the chunk size): a
+// smaller first chunk reaches the device sooner (its staging and upload are the call's only
+// un-overlapped host work).  A/B on one box, three rounds (profiles/r03/host_pipe_first_chunk.txt):
+// 65,536 gave 71.2-72.1 M votes/s at depth 3 and 4, 131,072 61.8-71.1 M, 32,768 62.7-68.7 M
+uint64_t pipe_first_chunk_votes(uint64_t target) {
+  const char* e = std::getenv("HLC_PIPE_FIRST_CHUNK_VOTES");
+  const uint64_t f = e ? (uint64_t)std::strtoull(e, nullptr, 10) : target / 2;
+  return f ? std::min(f, target) : target;
+}
+
 // Staging workers of the pipeline (HLC_PIPE_THREADS, default 4, including the calling thread).
 int pipe_threads() {
   const char* e = std::getenv("HLC_PIPE_THREADS");
@@ -829,6 +839,7 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
   {
     Chunk cur{0, 0, UINT64_MAX, 0};
     uint64_t acc = 0;
+    const uint64_t first = pipe_first_chunk_votes(target);
     for (uint64_t p = 0; p < np; ++p) {
       const uint64_t b = props[p].vote_begin, e = b + props[p].vote_count;
       if (props[p].vote_count) {
@@ -837,7 +848,7 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
       }
       acc += props[p].vote_count;
       cur.p1 = p + 1;
-      if (acc >= target || p + 1 == np) {
+      if (acc >= (ch.empty() ? first : target) || p + 1 == np) {
         if (cur.v0 == UINT64_MAX) cur.v0 = cur.v1 = ch.empty() ? 0 : ch.back().v1;
         ch.push_back(cur);
         cur = Chunk{p + 1, p + 1, UINT64_MAX, 0};
