@@ -34,7 +34,8 @@ sys.path.insert(0, os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
 METRIC = "verified votes/sec (ecrecover+chain check) at 1/2/4/8 MI355X vs host CPU"
 # Roofline constants frozen in roofline.json: the recovery is
 # integer-VALU bound (no MFMA); W = 337,280 limb products per vote (canonical 8x32 CIOS
-# ecrecover), peak = 39.3 T limb products/s (v_mad_u64_u32 at quarter rate, 2.4 GHz).
+# ecrecover), peak = 39.3 T limb products/s (v_mad_u64_u32 at half rate: 4 cycles per wave64 against
+# the 2-cycle VALU issue, 2.4 GHz); the VALU issue peak is 78.6 T lane-ops/s.
 with open(os.path.join(ROOT, "roofline.json")) as _f:
     ROOFLINE = json.load(_f)
 W_LIMB_PRODUCTS_PER_VOTE = ROOFLINE["W"]["limb_products_per_vote"]
@@ -630,6 +631,22 @@ def main() -> int:
     counters = ex.summary()  # the last timed step's counters (all-reduced over the ranks at N > 1)
     if not probe:
         assert counters["verified_votes"] == votes_per_step, "all-reduced verified-vote counter != votes processed"
+    gathered_check = None
+    if dist is not None:
+        # the gathered per-proposal rows: every rank's slice of the all_gather equals that rank's own
+        # results, byte for byte; the per-rank verdicts are all-reduced (MIN) so rank 0 reports all
+        pc = torch.tensor([P], dtype=torch.int64, device=coll_dev)
+        pcs = [torch.zeros_like(pc) for _ in range(world)]
+        dist.all_gather(pcs, pc)
+        counts = [int(x.item()) for x in pcs]
+        rows = ex.results(counts)
+        r0 = sum(counts[:rank])
+        mine = np.array_equal(rows[r0:r0 + P].view(np.uint8), db.results_numpy().view(np.uint8))
+        ok = torch.tensor([1 if mine else 0], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        gathered_check = {"rows": int(sum(counts)), "every_rank_slice_equals_local_results": bool(ok.item())}
+        if not probe:
+            assert gathered_check["every_rank_slice_equals_local_results"], "gathered result rows != local results"
 
     value = votes_per_step * args.steps / elapsed
     rec_avg_s = rec_ms / max(rec_n, 1) / 1e3
@@ -672,6 +689,7 @@ def main() -> int:
                 if world > 1 else ""),
         },
         "counters_per_step": counters,
+        **({"gathered_results": gathered_check} if gathered_check is not None else {}),
         "roofline": {
             "bound": "valu",
             "kernel": "recovery: k_rec_prep + k_rec_main (second stream, beside the prehash) + k_rec_comb + k_rec_final + k_rec_addr (HIP-event brackets)",

@@ -420,6 +420,24 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   return 0;
 }
 
+// The device workspace validate_device() needs for up to n votes and np proposals (grown on demand
+// otherwise): hlc_ctx_reserve, and the pipeline's children before their first chunk, so that no
+// buffer is reallocated while a chunk is in flight.
+int reserve_validate(hlc_ctx* c, uint64_t n, uint64_t np) {
+  CHK(ensure_recover_scratch(c));
+  CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
+  CHK(c->kec_dig.ensure(n * 32));
+  for (DBuf* b : {&c->pre, &c->pre_reason, &c->verify, &c->status, &c->reason, &c->chain_code}) CHK(b->ensure(n + 1));
+  CHK(c->vote_prop.ensure(n * 4 + 4));
+  uint64_t cap = 64;
+  while (cap < 2 * n) cap <<= 1;
+  CHK(c->chain_tab.ensure(cap * 4));
+  CHK(c->dup_tab.ensure(cap * 4));
+  CHK(c->red.ensure(np * 16 + 16));
+  CHK(c->flag.ensure(16));
+  return 0;
+}
+
 // Device-resident validate-many (every pointer is device memory).
 int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops, uint64_t np, uint64_t now,
                     hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s) {
@@ -735,6 +753,24 @@ uint64_t pipe_first_chunk_votes(uint64_t target) {
   return f ? std::min(f, target) : target;
 }
 
+// The chunk-size schedule: HLC_PIPE_CHUNKS="a,b,c" gives the votes of chunks 0, 1, 2 and every
+// later chunk takes the last size (A/B of geometric schedules); otherwise the first chunk of
+// pipe_first_chunk_votes() and then `target`.
+std::vector<uint64_t> pipe_schedule(uint64_t target) {
+  std::vector<uint64_t> v;
+  if (const char* e = std::getenv("HLC_PIPE_CHUNKS")) {
+    for (const char* p = e; *p;) {
+      char* end = nullptr;
+      const uint64_t x = std::strtoull(p, &end, 10);
+      if (end == p) break;
+      if (x) v.push_back(x);
+      p = *end == ',' ? end + 1 : end;
+    }
+  }
+  if (v.empty()) v = {pipe_first_chunk_votes(target), target};
+  return v;
+}
+
 // Staging workers of the pipeline (HLC_PIPE_THREADS, default 4, including the calling thread).
 int pipe_threads() {
   const char* e = std::getenv("HLC_PIPE_THREADS");
@@ -839,7 +875,7 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
   {
     Chunk cur{0, 0, UINT64_MAX, 0};
     uint64_t acc = 0;
-    const uint64_t first = pipe_first_chunk_votes(target);
+    const std::vector<uint64_t> sched = pipe_schedule(target);
     for (uint64_t p = 0; p < np; ++p) {
       const uint64_t b = props[p].vote_begin, e = b + props[p].vote_count;
       if (props[p].vote_count) {
@@ -848,7 +884,7 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
       }
       acc += props[p].vote_count;
       cur.p1 = p + 1;
-      if (acc >= (ch.empty() ? first : target) || p + 1 == np) {
+      if (acc >= sched[std::min(ch.size(), sched.size() - 1)] || p + 1 == np) {
         if (cur.v0 == UINT64_MAX) cur.v0 = cur.v1 = ch.empty() ? 0 : ch.back().v1;
         ch.push_back(cur);
         cur = Chunk{p + 1, p + 1, UINT64_MAX, 0};
@@ -869,10 +905,20 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
   for (int k = 0; k < depth; ++k)
     if (!c->pipe[k]) CHK(make_child(c, &c->pipe[k], shared));
   if (shared && !c->copy) HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
-  if (shared && !c->pstage) HIPCHK(hipStreamCreateWithFlags(&c->pstage, hipStreamNonBlocking));
-  for (int k = 0; k < depth; ++k) c->pipe[k]->prep_stream = shared ? c->pstage : nullptr;
+  if (shared && !c->pstage && !(std::getenv("HLC_PIPE_PREP_AUX") && std::atoi(std::getenv("HLC_PIPE_PREP_AUX"))))
+    HIPCHK(hipStreamCreateWithFlags(&c->pstage, hipStreamNonBlocking));
+  const bool prep_aux = std::getenv("HLC_PIPE_PREP_AUX") && std::atoi(std::getenv("HLC_PIPE_PREP_AUX"));  // A/B
+  for (int k = 0; k < depth; ++k) c->pipe[k]->prep_stream = shared && !prep_aux ? c->pstage : nullptr;
   if (!c->pool || c->pool->parts() != pipe_threads()) c->pool.reset(new HostPool(pipe_threads() - 1));
   HostPool& pool = *c->pool;
+  {  // every child's workspace sized for the largest chunk before any chunk is enqueued
+    uint64_t mv = 0, mp = 0;
+    for (const Chunk& q : ch) {
+      mv = std::max(mv, q.v1 - q.v0);
+      mp = std::max(mp, q.p1 - q.p0);
+    }
+    for (int k = 0; k < depth; ++k) CHK(reserve_validate(c->pipe[k], mv, mp));
+  }
   *used = true;
   if (tr.on) {
     tr.t0 = PipeTrace::clk::now();
@@ -990,6 +1036,13 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     o[6] = o[5] + al256(nv * 4 * HLC_NFIELDS);
     o[7] = o[6] + al256(npk * sizeof(hlc_proposal));
     o[8] = o[7] + (a_hi - a_lo);
+    size_t r[4];
+    const size_t blk = blk_layout(q, r);
+    if (o[8] + 16 > w->dev_in.cap || blk + 16 > w->dev_out.cap) {
+      // the child's device buffers grow: its previous chunk must be done with them first
+      HIPCHK(hipStreamSynchronize(w->stream));
+      HIPCHK(hipStreamSynchronize(w->aux));
+    }
     CHK(w->pin_in.ensure(o[8] + 16));
     CHK(w->dev_in.ensure(o[8] + 16));
     cp.assign(props + q.p0, props + q.p1);
@@ -1036,8 +1089,6 @@ int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props
     dv.field_len = reinterpret_cast<const uint32_t*>(d + o[5]);
     dv.bytes = d + o[7] - a_lo;  // the field offsets stay absolute: bytes + off lands in the staged span
     dv.bytes_len = a_hi;
-    size_t r[4];
-    const size_t blk = blk_layout(q, r);
     CHK(w->dev_out.ensure(blk + 16));
     uint8_t* ob = w->dev_out.as<uint8_t>();
     CHK(validate_device(w, &dv, reinterpret_cast<const hlc_proposal*>(d + o[6]), npk, now,
@@ -1153,20 +1204,11 @@ int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, ui
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
   const uint64_t n = max_votes;
-  CHK(ensure_recover_scratch(ctx));
-  CHK(ctx->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
+  CHK(reserve_validate(ctx, n, max_proposals));
   for (DBuf* b : {&ctx->sha_sz, &ctx->sha_off, &ctx->kec_sz, &ctx->kec_off}) CHK(b->ensure(n * 8));
-  for (DBuf* b : {&ctx->sha_dig, &ctx->kec_dig}) CHK(b->ensure(n * 32));
-  for (DBuf* b : {&ctx->pre, &ctx->pre_reason, &ctx->verify, &ctx->status, &ctx->reason, &ctx->chain_code})
-    CHK(b->ensure(n + 1));
-  CHK(ctx->vote_prop.ensure(n * 4 + 4));
+  CHK(ctx->sha_dig.ensure(n * 32));
   CHK(ctx->sha_buf.ensure(n * 128 + max_bytes + 64));
   CHK(ctx->kec_buf.ensure(n * 272 + max_bytes + 136));
-  uint64_t cap = 64;
-  while (cap < 2 * n) cap <<= 1;
-  CHK(ctx->chain_tab.ensure(cap * 4));
-  CHK(ctx->dup_tab.ensure(cap * 4));
-  CHK(ctx->red.ensure(max_proposals * 16 + 16));
   return 0;
 }
 

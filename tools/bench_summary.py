@@ -1,0 +1,30 @@
+"""One line per bench.py JSON file: the headline and every secondary leg it carries (no GPU)."""
+import json
+import sys
+
+
+def main() -> None:
+    for path in sys.argv[1:]:
+        for line in open(path):
+            line = line.strip()
+            if not line.startswith("{"):
+                continue
+            d = json.loads(line)
+            parts = [f"{path}: {d['value'] / 1e6:.1f} M votes/s", f"{d['ms_per_step']:.3f} ms/step", f"N={d['n_gpus']}"]
+            rf = d.get("roofline", {})
+            if rf.get("kernel_ms_avg"):
+                parts.append(f"rec {rf['kernel_ms_avg']:.3f} ms frac {rf['frac']:.3f}")
+            for k in ("wire", "end_to_end", "stream", "config3", "config5"):
+                if k in d:
+                    parts.append(f"{k} {d[k]['value'] / 1e6:.1f} M")
+            if "cpu_baseline" in d:
+                parts.append(f"cpu {d['cpu_baseline']['value'] / 1e3:.1f} k")
+            if "gathered_results" in d:
+                parts.append(f"gathered {d['gathered_results']}")
+            if "counters_per_step" in d:
+                parts.append(f"verified {d['counters_per_step']['verified_votes']}")
+            print(", ".join(parts))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,76 @@
+#!/bin/bash
+# One GPU-box session as a list of steps, run in order; the first failing step ends the call.
+#   bash tools/gpu.sh TAG step [step ...]          (outputs under gpurun_out/, named by TAG)
+# Steps:
+#   tests      the whole -m gpu suite (one process, per-test timeouts)
+#   quick      parity subset (test_gpu_parity + test_gpu_scenarios, no config 3)
+#   ptest      pytest $PTEST -m gpu (a subset of the suite)
+#   smoke      __graft_entry__.smoke()
+#   bench      the driver's command: bench.py --gpus 1 --steps 20 --warmup 5 (every leg)
+#   qbench     headline leg only, 5 steps
+#   n2         N = 2 dry run of the sharded bench (gloo, both ranks on GPU 0): config-4 shards
+#   pipe       tools/host_pipe.py sweep, arguments from $PIPE_ARGS
+#   pipetrace  rocprofv3 kernel + memory-copy trace of one host-buffer setting ($PIPE_ARGS)
+#   verify     tools/verify_latency.py (hlc_eth_verify_batch at the C ABI)
+#   profile    tools/profile.sh TAG (kernel trace + PMC passes of the headline leg)
+#   ab         tools/ab.sh $AB_VARIANTS (alternating A/B of lib/variants builds)
+#   clock      tools/clock_probe.py $CLOCK_ARGS (in-kernel shader clock of k_rec_main)
+set -o pipefail
+TAG=$1
+shift
+mkdir -p gpurun_out
+O=gpurun_out
+LEGS="--no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e"
+fail() { echo "step $1 failed"; tail -30 "$2"; exit 1; }
+for step in "$@"; do
+  case $step in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --durations=15 --timeout 200 --timeout-method thread \
+      > $O/gpu_tests_$TAG.log 2>&1 || fail tests $O/gpu_tests_$TAG.log
+    tail -2 $O/gpu_tests_$TAG.log ;;
+  quick)
+    timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scenarios.py -m gpu -x -q \
+      --timeout 120 --timeout-method thread -k "not config3" > $O/quick_$TAG.log 2>&1 || fail quick $O/quick_$TAG.log
+    tail -1 $O/quick_$TAG.log ;;
+  ptest)
+    timeout -k 10 600 python -u -m pytest $PTEST -m gpu -x -v --timeout 200 --timeout-method thread \
+      > $O/ptest_$TAG.log 2>&1 || fail ptest $O/ptest_$TAG.log
+    tail -2 $O/ptest_$TAG.log ;;
+  smoke)
+    timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 || fail smoke $O/smoke_$TAG.log
+    tail -1 $O/smoke_$TAG.log ;;
+  bench)
+    timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_$TAG.json 2> $O/bench_$TAG.err || fail bench $O/bench_$TAG.err
+    python tools/bench_summary.py $O/bench_$TAG.json ;;
+  qbench)
+    timeout -k 10 200 python bench.py --steps 5 --warmup 2 $LEGS > $O/qbench_$TAG.json 2> $O/qbench_$TAG.err || fail qbench $O/qbench_$TAG.err
+    python tools/bench_summary.py $O/qbench_$TAG.json ;;
+  n2)
+    HLC_BENCH_BACKEND=gloo HLC_BENCH_SAME_GPU=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --config 4 --proposals 20000 \
+      --steps 5 --warmup 2 > $O/n2_$TAG.json 2> $O/n2_$TAG.err || fail n2 $O/n2_$TAG.err
+    python tools/bench_summary.py $O/n2_$TAG.json ;;
+  pipe)
+    timeout -k 10 500 python tools/host_pipe.py $PIPE_ARGS > $O/pipe_$TAG.txt 2> $O/pipe_$TAG.err || fail pipe $O/pipe_$TAG.err
+    cat $O/pipe_$TAG.txt ;;
+  pipetrace)
+    OUT=$PWD/$O/pipetrace_$TAG
+    mkdir -p $OUT
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d $OUT -o run -- python3 $OLDPWD/tools/host_pipe.py $PIPE_ARGS > $OUT/out.txt 2> $OUT/err.txt) \
+      || fail pipetrace $OUT/err.txt
+    cat $OUT/out.txt ;;
+  verify)
+    timeout -k 10 400 python tools/verify_latency.py $VERIFY_ARGS > $O/verify_$TAG.txt 2> $O/verify_$TAG.err || fail verify $O/verify_$TAG.err
+    cat $O/verify_$TAG.txt ;;
+  profile)
+    bash tools/profile.sh $TAG || exit 1 ;;
+  ab)
+    bash tools/ab.sh $AB_VARIANTS || exit 1 ;;
+  clock)
+    timeout -k 10 300 python tools/clock_probe.py $CLOCK_ARGS > $O/clock_$TAG.txt 2> $O/clock_$TAG.err || fail clock $O/clock_$TAG.err
+    tail -20 $O/clock_$TAG.txt ;;
+  *)
+    echo "unknown step $step"; exit 2 ;;
+  esac
+done

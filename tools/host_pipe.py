@@ -42,6 +42,10 @@ def main() -> int:
     ap.add_argument("--threads", default="4", help="HLC_PIPE_THREADS settings to sweep")
     ap.add_argument("--depths", default="3", help="HLC_PIPE_DEPTH settings to sweep (child contexts in flight)")
     ap.add_argument("--proposals", type=int, default=10_000)
+    ap.add_argument("--schedules", default="", help="';'- or '/'-separated HLC_PIPE_CHUNKS schedules (votes of chunks 0, 1, "
+                    "...; the last size repeats), each run at every depth / thread setting; replaces --chunks")
+    ap.add_argument("--streams", default="own", help="HLC_PIPE_STREAMS settings to sweep (own, shared)")
+    ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
     ap.add_argument("--print-trace", default=None, help="print an HLC_PIPE_TRACE log as a table and exit")
     a = ap.parse_args()
     if a.print_trace:
@@ -62,11 +66,18 @@ def main() -> int:
                    + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
     ref = None
     out = []
-    settings = [(c, t, dp) for c in [int(x) for x in a.chunks.split(",")] for t in [int(x) for x in a.threads.split(",")]
-                for dp in [int(x) for x in a.depths.split(",")]]
-    for c, th, dp in settings:
+    chunks = [("0", 0)] + [(x, 65536) for x in a.schedules.replace("/", ";").split(";") if x] if a.schedules else \
+        [("", int(x)) for x in a.chunks.split(",")]
+    settings = [(sc, c, t, dp, sm) for sc, c in chunks for t in [int(x) for x in a.threads.split(",")]
+                for dp in [int(x) for x in a.depths.split(",")] for sm in a.streams.split(",")] * max(1, a.rounds)
+    for sched, c, th, dp, sm in settings:
+        os.environ["HLC_PIPE_STREAMS"] = sm
         if c == 0 and ref is not None:
             continue
+        if sched and sched != "0":
+            os.environ["HLC_PIPE_CHUNKS"] = sched
+        else:
+            os.environ.pop("HLC_PIPE_CHUNKS", None)
         os.environ["HLC_PIPE_CHUNK_VOTES"] = str(c)
         os.environ["HLC_PIPE_THREADS"] = str(th)
         os.environ["HLC_PIPE_DEPTH"] = str(dp)
@@ -79,7 +90,7 @@ def main() -> int:
         for _ in range(a.steps):
             eng.validate_proposals(b, d, db.now, want_votes=True)
         el = (time.perf_counter() - t) / a.steps
-        row = {"chunk_votes": c, "threads": th, "depth": dp, "ms_per_call": el * 1e3, "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in,
+        row = {"chunk_votes": c, "schedule": sched, "threads": th, "depth": dp, "streams": sm, "ms_per_call": el * 1e3, "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in,
                "outputs_equal_one_shot": True}
         print(json.dumps(row), flush=True)
         out.append(row)
