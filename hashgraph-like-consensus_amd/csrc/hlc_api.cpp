@@ -44,9 +44,8 @@ int set_err(int code, const std::string& msg) {
 struct DBuf {
   void* p = nullptr;
   size_t cap = 0;
-  bool borrowed = false;  // a pipeline child's view of its parent's fixed-base tables
   ~DBuf() {
-    if (p && !borrowed) (void)hipFree(p);
+    if (p) (void)hipFree(p);
   }
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
@@ -70,7 +69,7 @@ struct DBuf {
   }
 };
 
-// Page-locked host memory (the pipeline's staging buffers: DMA runs asynchronously from it).
+// Page-locked host memory (the host-buffer entries' staging buffers: DMA runs asynchronously from it).
 struct PBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -94,7 +93,7 @@ struct PBuf {
   uint8_t* at(size_t off) const { return static_cast<uint8_t*>(p) + off; }
 };
 
-// A small host worker pool for the pipeline's field checks and staging copies: run(fn) calls
+// A small host worker pool for the host-buffer entries' field checks and staging copies: run(fn) calls
 // fn(part, parts) for every part on the workers and the calling thread and returns when all are done.
 class HostPool {
  public:
@@ -161,33 +160,16 @@ struct hlc_ctx {
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
   int rec_force_exact = 0;  // HLC_REC_FORCE_EXACT=1: every vote through the checked chains (tests)
-  int serial_stages = 0;    // HLC_SERIAL_STAGES=1: prep + main after the prehash on one stream (A/B, clock probes)
-  int prep_first = 0;       // HLC_PREP_FIRST=1: the prep stage alone on the launch stream before the fork (A/B)
-  int aux_prio = 0;         // HLC_AUX_PRIO=1: the second stream at the device's greatest priority (A/B)
-  // hlc_validate_proposals pipeline: up to four child contexts (own streams and workspace, the
-  // parent's fixed-base tables) that take proposal chunks in turn, so one chunk's host->device copy
-  // and the next chunks' kernels overlap the previous chunks' kernels (created on first use)
-  hlc_ctx* pipe[4] = {nullptr, nullptr, nullptr, nullptr};
-  std::unique_ptr<HostPool> pool;  // the parent's staging workers (HLC_PIPE_THREADS)
-  // a pipeline child's staging: page-locked inputs, one device input buffer, the event after its
-  // chunk's host->device copy (the page-locked inputs are free again once it has fired)
-  PBuf pin_in;
-  DBuf dev_in, dev_out;  // a chunk's inputs; its outputs as one block (one copy back)
-  hipEvent_t ev_h2d = nullptr;
-  bool h2d_pending = false;
-  // shared-stream pipeline (HLC_PIPE_STREAMS=shared; the default is one stream pair per child): the
-  // children run on the parent's launch stream and their own aux streams, uploads on the parent's
-  // `copy` stream and the prep stages on its `pstage` stream; a child's next upload waits for ev_free
-  // (its previous chunk's kernels and output copies are done), and its prep waits for fork_wait (its
-  // upload) instead of a fork from `s`
-  hipStream_t copy = nullptr, pstage = nullptr;  // (parent) upload stream; prep-stage stream
-  hipStream_t prep_stream = nullptr;             // (child) the prep stage's stream, when not aux
-  bool borrowed_streams = false, pipe_shared = false, used = false;
-  hipEvent_t ev_free = nullptr, fork_wait = nullptr;
-  // the parent's call-wide page-locked outputs (every chunk's results land at their own offsets) and
-  // one completion event per chunk in flight
-  PBuf pipe_out;
-  std::vector<hipEvent_t> pipe_ev;
+  int serial_stages = 0;    // HLC_SERIAL_STAGES=1: prep + main after the prehash on one stream (clock probes, isolated kernel traces)
+  // hlc_validate_proposals (host buffers): a second recovery slot (stream, per-lane scratch, per-vote
+  // records) so that two k_rec_main grids over the two vote ranges of a call overlap; an upload stream;
+  // the page-locked staging of the inputs and outputs and their device copies (allocated on first use)
+  hipStream_t aux2 = nullptr, copy = nullptr;
+  DBuf rec_scratch2, rec_work2;
+  PBuf pin_in, pin_out;
+  DBuf dev_in, dev_out;
+  hipEvent_t ev_sig[2] = {nullptr, nullptr}, ev_main[2] = {nullptr, nullptr}, ev_rest = nullptr, ev_done = nullptr;
+  std::unique_ptr<HostPool> pool;  // staging workers (HLC_HOST_THREADS)
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
   DBuf in_off2, in_len2, in_off3, in_len3, in_priv, byz_key;
@@ -213,9 +195,8 @@ struct hlc_ctx {
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : rec_prep_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    if (ev_h2d) (void)hipEventDestroy(ev_h2d);
-    if (ev_free) (void)hipEventDestroy(ev_free);
-    for (auto e : pipe_ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_sig[0], ev_sig[1], ev_main[0], ev_main[1], ev_rest, ev_done})
+      if (e) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -235,15 +216,8 @@ struct hlc_ctx {
 
 namespace {
 
-// the context's second stream (the recovery's prep / main stages), optionally at the device's
-// greatest stream priority so that its workgroups are dispatched ahead of the prehash's
-hipError_t create_aux(hlc_ctx* c) {
-  if (!c->aux_prio) return hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
-  int least = 0, greatest = 0;
-  const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-  if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, greatest);
-}
+// the context's second stream (the recovery's prep / main stages)
+hipError_t create_aux(hlc_ctx* c) { return hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking); }
 
 int activate(hlc_ctx* ctx) {
   HIPCHK(hipSetDevice(ctx->device));
@@ -319,6 +293,14 @@ int ensure_fbtab(hlc_ctx* c) {
   return 0;
 }
 
+// A recovery range whose front half (k_rec_prep + k_rec_main over votes [v0, v1), records in `work`)
+// the caller has already enqueued on a stream of its own; `done` fires when that main stage ends.
+struct RecFront {
+  uint64_t v0, v1;
+  uint32_t* work;
+  hipEvent_t done;
+};
+
 // Per-vote validate_vote stage (utils.rs:127-171; plus the proposal_id match of utils.rs:113-115)
 // for votes already mapped to proposals (vote_prop, NO_PROP = skip): fused LDS prehash, the
 // streaming general path for oversize votes (skipped on the device when no vote needs it),
@@ -327,9 +309,11 @@ int ensure_fbtab(hlc_ctx* c) {
 // forked from and joined back into `s`): no host synchronisation.
 // chain_code != nullptr: also the small proposals' chain / duplicate / YES kernel (it needs no
 // vote statuses), on `s` beside the recovery's main stage.
+// fronts != nullptr (hlc_validate_proposals over host buffers): the recovery's front halves are
+// already in flight over those ranges (validate_host); each range's finish waits for its event.
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t np,
                uint64_t now, uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, uint8_t* chain_code,
-               hipStream_t s) {
+               hipStream_t s, const RecFront* fronts = nullptr, int nfronts = 0) {
   const uint64_t n = dv->n;
   CHK(c->pre.ensure(n));
   CHK(c->pre_reason.ensure(n));
@@ -346,7 +330,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   // the measurement of k_rec_main running alone)
   hipStream_t aux = c->serial_stages ? s : c->aux;
   hipEvent_t p0 = nullptr, p1 = nullptr, r0 = nullptr, r1 = nullptr;
-  if (c->timing) {
+  if (c->timing && !fronts) {
     p0 = c->take_event();
     p1 = c->take_event();
     r0 = c->take_event();
@@ -373,31 +357,33 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     }
     return 0;
   };
-  // HLC_PREP_FIRST=1: the prep stage runs alone on `s` before the fork, so the main stage starts as
-  // soon as it is done and the prehash fills the SIMD slots beside main instead of beside prep
-  const bool prep_first = c->prep_first && !c->serial_stages;
-  // (a shared-stream pipeline child runs prep on its parent's prep-stage stream, so that chunk k+1's
-  // prep can start in chunk k's k_rec_main tail)
-  hipStream_t prep_s = prep_first ? s : (c->prep_stream && !c->serial_stages ? c->prep_stream : aux);
-  if (c->serial_stages) CHK(prehash_and_chain());
-  if (!c->serial_stages && !prep_first) {
-    if (c->fork_wait) {  // shared-stream pipeline child: prep / main need only the chunk's upload
-      HIPCHK(hipStreamWaitEvent(prep_s, c->fork_wait, 0));
-    } else {
-      HIPCHK(hipEventRecord(c->ev_fork, s));
-      HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
+  if (fronts) {
+    CHK(prehash_and_chain());
+    for (int k = 0; k < nfronts; ++k) {
+      const RecFront& f = fronts[k];
+      HIPCHK(hipStreamWaitEvent(s, f.done, 0));
+      hlc::launch_recover_finish(f.v1 - f.v0, c->pre.as<uint8_t>() + f.v0, c->kec_dig.as<uint32_t>() + 8 * f.v0,
+                                 dv->bytes, dv->field_off + f.v0 * HLC_NFIELDS + HLC_F_OWNER, HLC_NFIELDS,
+                                 c->gtab.as<uint32_t>(), f.work, c->verify.as<uint8_t>() + f.v0,
+                                 drec ? drec + 20 * f.v0 : nullptr, s, c->rec_force_exact);
     }
+    hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
+                            c->verify.as<uint8_t>(), status, reason, red, s);
+    HIPCHK(hipGetLastError());
+    return 0;
   }
-  if (c->timing) HIPCHK(hipEventRecord(p0, prep_s));
-  hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
-                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), prep_s);
-  if (c->timing) {
-    HIPCHK(hipEventRecord(p1, prep_s));
-    c->rec_prep_ev.emplace_back(p0, p1);
-  }
-  if (prep_s != aux) {  // prep ran on `s` (HLC_PREP_FIRST) or on the prep-stage stream
-    HIPCHK(hipEventRecord(c->ev_fork, prep_s));
+  if (c->serial_stages) {
+    CHK(prehash_and_chain());
+  } else {
+    HIPCHK(hipEventRecord(c->ev_fork, s));
     HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
+  }
+  if (c->timing) HIPCHK(hipEventRecord(p0, aux));
+  hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
+                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux);
+  if (c->timing) {
+    HIPCHK(hipEventRecord(p1, aux));
+    c->rec_prep_ev.emplace_back(p0, p1);
   }
   if (c->timing) HIPCHK(hipEventRecord(r0, aux));
   hlc::launch_recover_main(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, c->rec_scratch.as<uint32_t>(),
@@ -440,7 +426,8 @@ int reserve_validate(hlc_ctx* c, uint64_t n, uint64_t np) {
 
 // Device-resident validate-many (every pointer is device memory).
 int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops, uint64_t np, uint64_t now,
-                    hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s) {
+                    hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s,
+                    const RecFront* fronts = nullptr, int nfronts = 0) {
   const uint64_t n = dv->n;
   if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
   hipEvent_t call0 = nullptr, call1 = nullptr;
@@ -476,7 +463,7 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   // recovery's main stage: k_vote_status reports each proposal's first failing vote)
   if (n)
     CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, np, now, status, reason, drec, c->red.as<uint32_t>(),
-                   c->chain_code.as<uint8_t>(), s));
+                   c->chain_code.as<uint8_t>(), s, fronts, nfronts));
   hipEvent_t ch0 = nullptr, ch1 = nullptr;
   if (c->timing) {  // chain check + duplicate detection + tally (+ k_chain_small's bracket in vote_stage)
     ch0 = c->take_event();
@@ -685,450 +672,305 @@ int stage_votes(hlc_ctx* c, const hlc_votes* v, hlc_votes* dv, hipStream_t s) {
   return 0;
 }
 
-int make_child(hlc_ctx* parent, hlc_ctx** out, bool shared) {
-  hlc_ctx* c = new hlc_ctx();
-  c->device = parent->device;
-  c->rec_force_exact = parent->rec_force_exact;
-  c->serial_stages = parent->serial_stages;
-  if (const char* e = std::getenv("HLC_PIPE_SERIAL")) c->serial_stages = std::atoi(e) != 0;  // A/B: one stream per child
-  c->prep_first = parent->prep_first;
-  c->aux_prio = parent->aux_prio;
-  c->pipe_shared = shared;
-  bool ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&c->ev_h2d, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&c->ev_free, hipEventDisableTiming) == hipSuccess;
-  if (ok && shared) {  // the parent's launch stream, an aux stream of its own (consecutive chunks'
-                       // k_rec_main grids overlap: the next one's waves fill the last one's tail)
-    c->stream = parent->stream;
-    c->borrowed_streams = true;
-    ok = create_aux(c) == hipSuccess;
-  } else if (ok) {
-    ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess && create_aux(c) == hipSuccess;
-  }
-  if (!ok) {
-    hipStream_t st = c->borrowed_streams ? nullptr : c->stream, ax = c->aux;
-    delete c;
-    if (st) (void)hipStreamDestroy(st);
-    if (ax) (void)hipStreamDestroy(ax);
-    return set_err(HLC_EDEVICE, "pipeline stream creation failed");
-  }
-  for (auto pr : {std::make_pair(&c->gtab, &parent->gtab), std::make_pair(&c->fbtab, &parent->fbtab)}) {
-    pr.first->p = pr.second->p;
-    pr.first->cap = pr.second->cap;
-    pr.first->borrowed = true;
-  }
-  *out = c;
-  return 0;
-}
-
 void destroy_ctx(hlc_ctx* ctx) {
   if (!ctx) return;
-  for (hipStream_t x : {ctx->stream, ctx->aux, ctx->copy, ctx->pstage})
+  for (hipStream_t x : {ctx->stream, ctx->aux, ctx->aux2, ctx->copy})
     if (x) (void)hipStreamSynchronize(x);
-  hipStream_t s = ctx->borrowed_streams ? nullptr : ctx->stream, a = ctx->aux, cp = ctx->copy, ps = ctx->pstage;
-  // (a shared-stream child's launch stream belongs to its parent)
+  hipStream_t s = ctx->stream, a = ctx->aux, a2 = ctx->aux2, cp = ctx->copy;
   delete ctx;
-  for (hipStream_t x : {s, a, cp, ps})
+  for (hipStream_t x : {s, a, a2, cp})
     if (x) (void)hipStreamDestroy(x);
-}
-
-// Votes per pipeline chunk (HLC_PIPE_CHUNK_VOTES overrides; 0 disables the pipeline).
-uint64_t pipe_chunk_votes() {
-  const char* e = std::getenv("HLC_PIPE_CHUNK_VOTES");
-  return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)131072;
-}
-
-struct Chunk {
-  uint64_t p0, p1, v0, v1;
-};
-
-// Votes in the pipeline's first chunk (HLC_PIPE_FIRST_CHUNK_VOTES; default: half the chunk size): a
-// smaller first chunk reaches the device sooner (its staging and upload are the call's only
-// un-overlapped host work).  A/B on one box, three rounds (profiles/r03/host_pipe_first_chunk.txt):
-// 65,536 gave 71.2-72.1 M votes/s at depth 3 and 4, 131,072 61.8-71.1 M, 32,768 62.7-68.7 M
-uint64_t pipe_first_chunk_votes(uint64_t target) {
-  const char* e = std::getenv("HLC_PIPE_FIRST_CHUNK_VOTES");
-  const uint64_t f = e ? (uint64_t)std::strtoull(e, nullptr, 10) : target / 2;
-  return f ? std::min(f, target) : target;
-}
-
-// The chunk-size schedule: HLC_PIPE_CHUNKS="a,b,c" gives the votes of chunks 0, 1, 2 and every
-// later chunk takes the last size (A/B of geometric schedules); otherwise the first chunk of
-// pipe_first_chunk_votes() and then `target`.
-std::vector<uint64_t> pipe_schedule(uint64_t target) {
-  std::vector<uint64_t> v;
-  if (const char* e = std::getenv("HLC_PIPE_CHUNKS")) {
-    for (const char* p = e; *p;) {
-      char* end = nullptr;
-      const uint64_t x = std::strtoull(p, &end, 10);
-      if (end == p) break;
-      if (x) v.push_back(x);
-      p = *end == ',' ? end + 1 : end;
-    }
-  }
-  if (v.empty()) v = {pipe_first_chunk_votes(target), target};
-  return v;
-}
-
-// Staging workers of the pipeline (HLC_PIPE_THREADS, default 4, including the calling thread).
-int pipe_threads() {
-  const char* e = std::getenv("HLC_PIPE_THREADS");
-  const int t = e ? std::atoi(e) : 4;
-  return std::max(1, std::min(t, 64));
-}
-
-// The pipeline children run each on its own stream pair (default) or all on the parent's streams
-// with a separate upload stream (HLC_PIPE_STREAMS=shared, A/B).  Shared streams avoid the runtime's
-// mapping of many streams onto four hardware queues (rocprofv3 showed one child's prehash queued
-// behind another child's k_rec_main), but they also serialise the chunks' recovery stages: measured
-// slower (profiles/r03/host_pipe_v2.txt).
-bool pipe_shared_streams() {
-  const char* e = std::getenv("HLC_PIPE_STREAMS");
-  return e && std::strcmp(e, "shared") == 0;
-}
-
-// Child contexts of the pipeline, i.e. chunks in flight (HLC_PIPE_DEPTH, default 3, 2..4).
-int pipe_depth() {
-  const char* e = std::getenv("HLC_PIPE_DEPTH");
-  const int d = e ? std::atoi(e) : 3;
-  return std::max(2, std::min(d, 4));
 }
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// hlc_validate_proposals over host buffers, pipelined: the proposals are cut into chunks of about
-// pipe_chunk_votes() votes (contiguous proposal ranges whose vote ranges are disjoint and in order --
-// the layout of prost-decoded / packed batches; any other layout returns *used = false and takes the
-// one-shot path).  Chunk k runs on child context pipe[k % D] (own streams and workspace; D =
-// pipe_depth(), 3 by default):
-//   host   : wait until the child's previous chunk (k-D) has been UPLOADED (its page-locked inputs
-//            are free again; its kernels may still run); check chunk k's fields and copy its SoA
-//            slices, proposals and arena span into the child's page-locked staging buffer (the
-//            pool's threads); after enqueueing, copy out every earlier chunk whose event has fired;
-//   device : one H2D DMA of the staging buffer, the validate-many kernels, the outputs' D2H into the
-//            call-wide page-locked output buffer at the chunk's offsets, an event -- all asynchronous
-//            on the child's stream (stream order keeps chunk k's upload behind chunk k-D's kernels).
-// So the host never waits for a chunk's kernels: it runs up to 2D chunks ahead of the device, and the
-// device finds the next chunk uploaded when it finishes one.  (The round-3 first version waited for
-// chunk k-D's outputs before staging chunk k -- the device then ran dry whenever the host was
-// blocked: HLC_PIPE_TRACE showed ~0.4-1 ms idle gaps.)
-// HLC_PIPE_TRACE=1: one JSON line per pipelined call on stderr -- per chunk the host phases (wait for
-// the child's inputs, field checks, staging copies, enqueue) and the device spans (H2D, kernels,
-// D2H) from timing events, all in ms from the call's start (tools/host_pipe.py --print-trace)
-struct PipeTrace {
+// Staging workers of the host-buffer entries (HLC_HOST_THREADS, default 8, including the calling thread).
+int host_threads() {
+  const char* e = std::getenv("HLC_HOST_THREADS");
+  const int t = e ? std::atoi(e) : 8;
+  return std::max(1, std::min(t, 64));
+}
+
+// Votes in the first of the two recovery ranges of hlc_validate_proposals (HLC_SPLIT_FIRST_VOTES,
+// default 131072; 0 = one range): the first k_rec_main grid starts once these votes' signatures have
+// landed, the second once the rest have, and fills the first one's tail.
+uint64_t split_first_votes() {
+  const char* e = std::getenv("HLC_SPLIT_FIRST_VOTES");
+  return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)131072;
+}
+
+// Pieces the inputs other than the signatures are staged and uploaded in (HLC_REST_PIECES, default 3):
+// piece k+1 is copied into page-locked memory while piece k's DMA runs.
+int rest_pieces() {
+  const char* e = std::getenv("HLC_REST_PIECES");
+  const int k = e ? std::atoi(e) : 3;
+  return std::max(1, std::min(k, 64));
+}
+
+// The host-buffer entries' streams, events, staging pool and second recovery slot (on first use).
+// The runtime maps a process's streams onto a few hardware queues per priority level
+// (GPU_MAX_HW_QUEUES, 4 on the box), and a marker recorded on a stream that shares its queue with
+// another stream's kernel completes only after that kernel: measured, the upload stream's last event
+// fired when the second k_rec_main ended, 4 ms after its DMA, and the prehash waited for it.  So the
+// upload stream takes the greatest priority and the second recovery stream the least: each draws
+// its queue from a pool of its own, apart from the normal-priority launch / aux streams.
+int host_resources(hlc_ctx* c) {
+  int least = 0, greatest = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  if (!c->copy) HIPCHK(hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, greatest));
+  if (!c->aux2) HIPCHK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, least));
+  for (hipEvent_t* e : {&c->ev_sig[0], &c->ev_sig[1], &c->ev_main[0], &c->ev_main[1], &c->ev_rest, &c->ev_done})
+    if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  if (!c->pool || c->pool->parts() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
+  CHK(ensure_recover_scratch(c));
+  CHK(c->rec_scratch2.ensure(c->rec_lanes * hlc::recover_scratch_words() * sizeof(uint32_t)));
+  return 0;
+}
+
+// HLC_HOST_TRACE=1: one line per hlc_validate_proposals call on stderr -- host phase ends and device
+// event times, ms from the call's start (the device times from an event recorded first on the
+// upload stream)
+struct HostTrace {
   using clk = std::chrono::steady_clock;
   bool on = false;
   clk::time_point t0;
+  std::vector<std::pair<const char*, double>> host;
+  std::vector<std::pair<const char*, hipEvent_t>> dev;
   hipEvent_t e0 = nullptr;
-  struct Row {
-    double wait0, wait1, check1, stage1, h2d1, kern1, enq1;  // host times
-    hipEvent_t a, b, c, d;  // before H2D, after H2D, after the kernels, after D2H
-  };
-  std::vector<Row> rows;
-  double ms(clk::time_point t) const { return std::chrono::duration<double, std::milli>(t - t0).count(); }
-  hipEvent_t ev(hipStream_t s) {
+  void start(hipStream_t s) {
+    if (!on) return;
+    t0 = clk::now();
+    (void)hipEventCreate(&e0);
+    (void)hipEventRecord(e0, s);
+  }
+  void mark(const char* what) {
+    if (on) host.emplace_back(what, std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+  }
+  void ev(const char* what, hipStream_t s) {
+    if (!on) return;
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) == hipSuccess) (void)hipEventRecord(e, s);
-    return e;
-  }
-  void print(uint64_t n, size_t chunks) {
-    (void)hipDeviceSynchronize();
-    auto el = [&](hipEvent_t e) {
-      float f = -1;
-      if (e0 && e) (void)hipEventElapsedTime(&f, e0, e);
-      return (double)f;
-    };
-    std::fprintf(stderr, "HLC_PIPE_TRACE {\"votes\": %llu, \"chunks\": %zu, \"host_ms\": %.3f, \"rows\": [",
-                 (unsigned long long)n, chunks, ms(clk::now()));
-    for (size_t k = 0; k < rows.size(); ++k) {
-      const Row& r = rows[k];
-      std::fprintf(stderr,
-                   "%s{\"wait\": [%.3f, %.3f], \"check_end\": %.3f, \"stage_end\": %.3f, \"enq_h2d_end\": %.3f, "
-                   "\"enq_kern_end\": %.3f, \"enq_end\": %.3f, \"h2d\": [%.3f, %.3f], \"kern_end\": %.3f, \"d2h_end\": %.3f}",
-                   k ? ", " : "", r.wait0, r.wait1, r.check1, r.stage1, r.h2d1, r.kern1, r.enq1, el(r.a), el(r.b), el(r.c),
-                   el(r.d));
+    if (hipEventCreate(&e) == hipSuccess) {
+      (void)hipEventRecord(e, s);
+      dev.emplace_back(what, e);
     }
-    std::fprintf(stderr, "]}\n");
-    release();
   }
-  // also on an early error return of the traced call
-  void release() {
-    for (auto& r : rows)
-      for (hipEvent_t e : {r.a, r.b, r.c, r.d})
-        if (e) (void)hipEventDestroy(e);
-    rows.clear();
+  ~HostTrace() {
+    if (!on) return;
+    (void)hipDeviceSynchronize();
+    std::fprintf(stderr, "HLC_HOST_TRACE {\"host\": {");
+    for (size_t k = 0; k < host.size(); ++k) std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", host[k].first, host[k].second);
+    std::fprintf(stderr, "}, \"device\": {");
+    for (size_t k = 0; k < dev.size(); ++k) {
+      float f = -1;
+      (void)hipEventElapsedTime(&f, e0, dev[k].second);
+      std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", dev[k].first, (double)f);
+      (void)hipEventDestroy(dev[k].second);
+    }
+    std::fprintf(stderr, "}}\n");
     if (e0) (void)hipEventDestroy(e0);
-    e0 = nullptr;
   }
-  ~PipeTrace() { release(); }
 };
 
-int validate_pipelined(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
-                       hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec, bool* used) {
-  *used = false;
-  PipeTrace tr;
-  if (const char* e = std::getenv("HLC_PIPE_TRACE")) tr.on = std::atoi(e) != 0;
-  const uint64_t target = pipe_chunk_votes(), n = v->n;
-  if (!target || n < 2 * target || np < 2) return 0;
-  std::vector<Chunk> ch;
-  {
-    Chunk cur{0, 0, UINT64_MAX, 0};
-    uint64_t acc = 0;
-    const std::vector<uint64_t> sched = pipe_schedule(target);
-    for (uint64_t p = 0; p < np; ++p) {
-      const uint64_t b = props[p].vote_begin, e = b + props[p].vote_count;
-      if (props[p].vote_count) {
-        cur.v0 = std::min(cur.v0, b);
-        cur.v1 = std::max(cur.v1, e);
-      }
-      acc += props[p].vote_count;
-      cur.p1 = p + 1;
-      if (acc >= sched[std::min(ch.size(), sched.size() - 1)] || p + 1 == np) {
-        if (cur.v0 == UINT64_MAX) cur.v0 = cur.v1 = ch.empty() ? 0 : ch.back().v1;
-        ch.push_back(cur);
-        cur = Chunk{p + 1, p + 1, UINT64_MAX, 0};
-        acc = 0;
-      }
-    }
-  }
-  for (size_t k = 1; k < ch.size(); ++k)
-    if (ch[k].v0 < ch[k - 1].v1) return 0;  // interleaved vote ranges: one-shot path
-  if (ch.size() < 2) return 0;
-  const int depth = pipe_depth();
-  const bool shared = pipe_shared_streams();
-  for (auto& w : c->pipe)
-    if (w && w->pipe_shared != shared) {
-      destroy_ctx(w);
-      w = nullptr;
-    }
-  for (int k = 0; k < depth; ++k)
-    if (!c->pipe[k]) CHK(make_child(c, &c->pipe[k], shared));
-  if (shared && !c->copy) HIPCHK(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
-  if (shared && !c->pstage && !(std::getenv("HLC_PIPE_PREP_AUX") && std::atoi(std::getenv("HLC_PIPE_PREP_AUX"))))
-    HIPCHK(hipStreamCreateWithFlags(&c->pstage, hipStreamNonBlocking));
-  const bool prep_aux = std::getenv("HLC_PIPE_PREP_AUX") && std::atoi(std::getenv("HLC_PIPE_PREP_AUX"));  // A/B
-  for (int k = 0; k < depth; ++k) c->pipe[k]->prep_stream = shared && !prep_aux ? c->pstage : nullptr;
-  if (!c->pool || c->pool->parts() != pipe_threads()) c->pool.reset(new HostPool(pipe_threads() - 1));
+// hlc_validate_proposals over host buffers (what INTEGRATION.md's process_incoming_proposals calls).
+// The caller's votes go to the device through page-locked staging on the context's upload stream,
+// ordered by what the kernels need first, so that the VALU-bound recovery starts long before the
+// whole batch has landed:
+//   1. the signatures of votes [0, na), gathered into a dense array (65 B per vote) with their
+//      lengths -> k_rec_prep + k_rec_main over them on the aux stream (recovery slot 1);
+//   2. the signatures of votes [na, n) -> k_rec_prep + k_rec_main over them on the second aux stream
+//      (slot 2: its own per-lane scratch and records), whose waves take the SIMD slots the first
+//      grid's waves free (one k_rec_main tail per call, as in the device-resident call);
+//   3. every other input (SoA arrays, proposals, the byte arena) in rest_pieces() pieces, each copied
+//      into page-locked memory by the host pool while the previous piece's DMA runs -> the prehash,
+//      chain / duplicate / YES kernels on the launch stream, then each range's finish (u1 G, Z^-1,
+//      address) once its main stage is done, the statuses, tables, finalize, and one D2H of every
+//      output into page-locked memory.
+// Every field's (offset, length) is checked on the host pool while it is staged (signatures before
+// their bytes are read); a violation returns HLC_EINVAL before anything reaches the caller's outputs
+// (the device work already enqueued is drained and discarded).  Only stream / event dependencies
+// order the stages: no kernel waits on a flag, so any mapping of the streams onto hardware queues
+// is correct (one that serialises them is only slower).
+int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
+                  hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec) {
+  const uint64_t n = v->n;
+  const uint64_t blen = v->bytes ? v->bytes_len : 0;
+  CHK(host_resources(c));
   HostPool& pool = *c->pool;
-  {  // every child's workspace sized for the largest chunk before any chunk is enqueued
-    uint64_t mv = 0, mp = 0;
-    for (const Chunk& q : ch) {
-      mv = std::max(mv, q.v1 - q.v0);
-      mp = std::max(mp, q.p1 - q.p0);
-    }
-    for (int k = 0; k < depth; ++k) CHK(reserve_validate(c->pipe[k], mv, mp));
-  }
-  *used = true;
-  if (tr.on) {
-    tr.t0 = PipeTrace::clk::now();
-    (void)hipEventCreate(&tr.e0);
-    (void)hipEventRecord(tr.e0, c->pipe[0]->stream);
-  }
-
-  // call-wide page-locked outputs: one block per chunk, [results | status | reason | recovered],
-  // so each chunk's outputs come back in one copy and no chunk waits for an earlier one's to be
-  // copied out
-  auto blk_layout = [&](const Chunk& q, size_t r[4]) {
-    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
-    r[0] = 0;  // (one spare element each, as the one-shot path's buffers)
-    r[1] = al256((npk + 1) * sizeof(hlc_result));
-    r[2] = r[1] + al256(nv + 1);
-    r[3] = r[2] + al256(nv + 1);
-    return r[3] + (out_rec ? al256(nv * 20 + 20) : 0);
-  };
-  std::vector<size_t> blk_off(ch.size() + 1, 0);
-  for (size_t k = 0; k < ch.size(); ++k) {
-    size_t r[4];
-    blk_off[k + 1] = blk_off[k] + blk_layout(ch[k], r);
-  }
-  CHK(c->pipe_out.ensure(blk_off[ch.size()] + 16));
-  while (c->pipe_ev.size() < ch.size()) {
-    hipEvent_t e = nullptr;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->pipe_ev.push_back(e);
-  }
-  // chunk k's outputs -> the caller's buffers (after its event), on the pool
-  auto copy_out = [&](size_t k) {
-    const Chunk& q = ch[k];
-    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
-    size_t r[4];
-    blk_layout(q, r);
-    const uint8_t* src = c->pipe_out.at(blk_off[k]);
-    pool.run([&](int t, int T) {
-      const uint64_t b0 = npk * t / T, b1 = npk * (t + 1) / T, a0 = nv * t / T, a1 = nv * (t + 1) / T;
-      if (b1 > b0)
-        std::memcpy(out_res + q.p0 + b0, src + r[0] + b0 * sizeof(hlc_result), (b1 - b0) * sizeof(hlc_result));
-      if (a1 > a0) {
-        if (out_st) std::memcpy(out_st + q.v0 + a0, src + r[1] + a0, a1 - a0);
-        if (out_rs) std::memcpy(out_rs + q.v0 + a0, src + r[2] + a0, a1 - a0);
-        if (out_rec) std::memcpy(out_rec + 20 * (q.v0 + a0), src + r[3] + 20 * a0, 20 * (a1 - a0));
-      }
-    });
+  HostTrace tr;
+  if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
+  tr.start(c->copy);
+  const uint64_t first = split_first_votes();
+  const uint64_t na = first && n >= 2 * first ? first : n;  // one range when the batch is small
+  const uint64_t nb = n - na;
+  // inputs, page-locked and on the device alike: dense signatures | signature lengths | vote_id |
+  // proposal_id | timestamp | vote | field_off | field_len | proposals | arena
+  size_t o[11];
+  o[0] = 0;
+  o[1] = o[0] + al256(n * 65);
+  o[2] = o[1] + al256(n * 4);
+  o[3] = o[2] + al256(n * 4);
+  o[4] = o[3] + al256(n * 4);
+  o[5] = o[4] + al256(n * 8);
+  o[6] = o[5] + al256(n);
+  o[7] = o[6] + al256(n * 8 * HLC_NFIELDS);
+  o[8] = o[7] + al256(n * 4 * HLC_NFIELDS);
+  o[9] = o[8] + al256(np * sizeof(hlc_proposal));
+  o[10] = o[9] + blen;
+  // outputs: results | status | reason | recovered
+  size_t r[5];
+  r[0] = 0;
+  r[1] = al256((np + 1) * sizeof(hlc_result));
+  r[2] = r[1] + al256(n + 1);
+  r[3] = r[2] + al256(n + 1);
+  r[4] = r[3] + (out_rec ? al256(n * 20 + 20) : 0);
+  CHK(c->pin_in.ensure(o[10] + 16));
+  CHK(c->dev_in.ensure(o[10] + 16));
+  CHK(c->pin_out.ensure(r[4] + 16));
+  CHK(c->dev_out.ensure(r[4] + 16));
+  CHK(reserve_validate(c, n, np));  // slot 1's records are sized for n >= na
+  if (nb) CHK(c->rec_work2.ensure(hlc::recover_work_words(nb) * sizeof(uint32_t)));
+  uint8_t* P = c->pin_in.at(0);
+  uint8_t* D = c->dev_in.as<uint8_t>();
+  auto up = [&](size_t off, size_t len) -> int {
+    if (len) HIPCHK(hipMemcpyAsync(D + off, P + off, len, hipMemcpyHostToDevice, c->copy));
+    return 0;
   };
   auto drain = [&]() {
-    for (hipStream_t x : {c->stream, c->aux, c->copy, c->pstage})
-      if (x) (void)hipStreamSynchronize(x);
-    for (hlc_ctx* p : c->pipe) {
-      if (!p) continue;
-      (void)hipStreamSynchronize(p->stream);
-      (void)hipStreamSynchronize(p->aux);
-      p->h2d_pending = false;
-    }
+    for (hipStream_t x : {c->copy, c->aux, c->aux2, c->stream}) (void)hipStreamSynchronize(x);
   };
-  size_t next_out = 0;  // chunks [0, next_out) are in the caller's buffers
-  std::vector<hlc_proposal> cp;
-  for (size_t k = 0; k < ch.size(); ++k) {
-    hlc_ctx* w = c->pipe[k % depth];
-    PipeTrace::Row trow{};
-    if (tr.on) trow.wait0 = tr.ms(PipeTrace::clk::now());
-    if (w->h2d_pending) {  // its previous chunk's upload has left the page-locked inputs
-      HIPCHK(hipEventSynchronize(w->ev_h2d));
-      w->h2d_pending = false;
-    }
-    if (tr.on) trow.wait1 = tr.ms(PipeTrace::clk::now());
-    const Chunk& q = ch[k];
-    const uint64_t nv = q.v1 - q.v0, npk = q.p1 - q.p0;
-    // field checks of the chunk's votes and of the uncovered votes before it (the one-shot path's
-    // rule), and the arena span of the chunk's votes, on the pool
-    const uint64_t g0 = k ? ch[k - 1].v1 : 0, g1 = k + 1 == ch.size() ? n : q.v1;
-    const int parts = pool.parts();
-    std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
+  const int parts = pool.parts();
+  // signatures of votes [a0, a1) -> the dense array and the length array; false: one lies outside
+  // the arena (its bytes are not read)
+  auto stage_sigs = [&](uint64_t a0, uint64_t a1) -> bool {
     std::vector<int> bad(parts, 0);
     pool.run([&](int t, int T) {
-      const uint64_t a0 = g0 + (g1 - g0) * t / T, a1 = g0 + (g1 - g0) * (t + 1) / T;
-      uint64_t l = UINT64_MAX, h = 0;
-      for (uint64_t i = a0 * HLC_NFIELDS; i < a1 * HLC_NFIELDS; ++i) {
-        const uint64_t off = v->field_off[i], len = v->field_len[i];
-        if (!len) continue;
-        if (!v->bytes || off + len > v->bytes_len || off + len < off) {
+      const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
+      uint8_t* sg = P + o[0];
+      uint32_t* sl = reinterpret_cast<uint32_t*>(P + o[1]);
+      for (uint64_t i = b0; i < b1; ++i) {
+        const uint64_t off = v->field_off[i * HLC_NFIELDS + HLC_F_SIGNATURE];
+        const uint32_t len = v->field_len[i * HLC_NFIELDS + HLC_F_SIGNATURE];
+        sl[i] = len;
+        if (len != 65) continue;  // the prep stage skips it (the pre-checks reject it by length)
+        if (!v->bytes || off + 65 > v->bytes_len || off + 65 < off) {
           bad[t] = 1;
           return;
         }
-        const uint64_t vi = i / HLC_NFIELDS;
-        if (vi >= q.v0 && vi < q.v1) {
-          l = std::min(l, off);
-          h = std::max(h, off + len);
+        std::memcpy(sg + 65 * i, v->bytes + off, 65);
+      }
+    });
+    for (int x : bad)
+      if (x) return false;
+    return true;
+  };
+  uint32_t* work[2] = {c->rec_work.as<uint32_t>(), c->rec_work2.as<uint32_t>()};
+  uint32_t* scratch[2] = {c->rec_scratch.as<uint32_t>(), c->rec_scratch2.as<uint32_t>()};
+  hipStream_t aux[2] = {c->aux, c->aux2};
+  const uint64_t rv0[2] = {0, na}, rv1[2] = {na, n};
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t a0 = rv0[k], m = rv1[k] - rv0[k];
+    if (!m) continue;
+    if (!stage_sigs(a0, a0 + m)) {
+      drain();
+      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+    }
+    tr.mark(k ? "sigs_b_staged" : "sigs_a_staged");
+    CHK(up(o[0] + 65 * a0, 65 * m));
+    CHK(up(o[1] + 4 * a0, 4 * m));
+    HIPCHK(hipEventRecord(c->ev_sig[k], c->copy));
+    tr.ev(k ? "sigs_b_landed" : "sigs_a_landed", c->copy);
+    HIPCHK(hipStreamWaitEvent(aux[k], c->ev_sig[k], 0));
+    const uint8_t* sb = D + o[0] + 65 * a0;
+    const uint32_t* sl = reinterpret_cast<const uint32_t*>(D + o[1]) + a0;
+    hlc::launch_recover_prep(m, sb, nullptr, 0, sl, 1, work[k], aux[k]);
+    hlc::launch_recover_main(m, sb, nullptr, 0, scratch[k], c->rec_lanes, work[k], aux[k], c->rec_force_exact);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_main[k], aux[k]));
+    tr.ev(k ? "main_b_end" : "main_a_end", aux[k]);
+  }
+  // everything else, piece by piece, field checks on the way
+  const int K = rest_pieces();
+  std::vector<int> bad(parts, 0);
+  for (int k = 0; k < K; ++k) {
+    const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K, c0 = blen * k / K, c1 = blen * (k + 1) / K;
+    pool.run([&](int t, int T) {
+      const uint64_t b0 = v0 + (v1 - v0) * t / T, b1 = v0 + (v1 - v0) * (t + 1) / T, m = b1 - b0;
+      if (m) {
+        std::memcpy(P + o[2] + 4 * b0, v->vote_id + b0, 4 * m);
+        std::memcpy(P + o[3] + 4 * b0, v->proposal_id + b0, 4 * m);
+        std::memcpy(P + o[4] + 8 * b0, v->timestamp + b0, 8 * m);
+        std::memcpy(P + o[5] + b0, v->vote + b0, m);
+        std::memcpy(P + o[6] + 8 * HLC_NFIELDS * b0, v->field_off + HLC_NFIELDS * b0, 8 * HLC_NFIELDS * m);
+        std::memcpy(P + o[7] + 4 * HLC_NFIELDS * b0, v->field_len + HLC_NFIELDS * b0, 4 * HLC_NFIELDS * m);
+        for (uint64_t i = b0 * HLC_NFIELDS; i < b1 * HLC_NFIELDS; ++i) {
+          const uint64_t off = v->field_off[i], len = v->field_len[i];
+          if (len && (!v->bytes || off + len > v->bytes_len || off + len < off)) {
+            bad[t] = 1;
+            break;
+          }
         }
       }
-      lo[t] = l;
-      hi[t] = h;
+      const uint64_t d0 = c0 + (c1 - c0) * t / T, d1 = c0 + (c1 - c0) * (t + 1) / T;
+      if (d1 > d0) std::memcpy(P + o[9] + d0, v->bytes + d0, d1 - d0);
+      if (k == 0 && t == 0 && np) std::memcpy(P + o[8], props, np * sizeof(hlc_proposal));
     });
-    uint64_t a_lo = UINT64_MAX, a_hi = 0;
-    for (int t = 0; t < parts; ++t) {
-      if (bad[t]) {
-        drain();
-        return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-      }
-      a_lo = std::min(a_lo, lo[t]);
-      a_hi = std::max(a_hi, hi[t]);
-    }
-    if (a_lo == UINT64_MAX) a_lo = a_hi = 0;
-    if (tr.on) trow.check1 = tr.ms(PipeTrace::clk::now());
-    // input layout: vote_id | proposal_id | timestamp | vote | field_off | field_len | props | arena
-    size_t o[9];
-    o[0] = 0;
-    o[1] = o[0] + al256(nv * 4);
-    o[2] = o[1] + al256(nv * 4);
-    o[3] = o[2] + al256(nv * 8);
-    o[4] = o[3] + al256(nv);
-    o[5] = o[4] + al256(nv * 8 * HLC_NFIELDS);
-    o[6] = o[5] + al256(nv * 4 * HLC_NFIELDS);
-    o[7] = o[6] + al256(npk * sizeof(hlc_proposal));
-    o[8] = o[7] + (a_hi - a_lo);
-    size_t r[4];
-    const size_t blk = blk_layout(q, r);
-    if (o[8] + 16 > w->dev_in.cap || blk + 16 > w->dev_out.cap) {
-      // the child's device buffers grow: its previous chunk must be done with them first
-      HIPCHK(hipStreamSynchronize(w->stream));
-      HIPCHK(hipStreamSynchronize(w->aux));
-    }
-    CHK(w->pin_in.ensure(o[8] + 16));
-    CHK(w->dev_in.ensure(o[8] + 16));
-    cp.assign(props + q.p0, props + q.p1);
-    for (auto& pr : cp) pr.vote_begin = pr.vote_count ? pr.vote_begin - q.v0 : 0;
-    std::memcpy(w->pin_in.at(o[6]), cp.data(), npk * sizeof(hlc_proposal));
-    const uint64_t arena = a_hi - a_lo;
-    pool.run([&](int t, int T) {
-      const uint64_t b0 = q.v0 + nv * t / T, b1 = q.v0 + nv * (t + 1) / T, m = b1 - b0, r = b0 - q.v0;
-      std::memcpy(w->pin_in.at(o[0] + 4 * r), v->vote_id + b0, 4 * m);
-      std::memcpy(w->pin_in.at(o[1] + 4 * r), v->proposal_id + b0, 4 * m);
-      std::memcpy(w->pin_in.at(o[2] + 8 * r), v->timestamp + b0, 8 * m);
-      std::memcpy(w->pin_in.at(o[3] + r), v->vote + b0, m);
-      std::memcpy(w->pin_in.at(o[4] + 8 * HLC_NFIELDS * r), v->field_off + HLC_NFIELDS * b0, 8 * HLC_NFIELDS * m);
-      std::memcpy(w->pin_in.at(o[5] + 4 * HLC_NFIELDS * r), v->field_len + HLC_NFIELDS * b0, 4 * HLC_NFIELDS * m);
-      const uint64_t c0 = arena * t / T, c1 = arena * (t + 1) / T;
-      if (c1 > c0) std::memcpy(w->pin_in.at(o[7] + c0), v->bytes + a_lo + c0, c1 - c0);
-    });
-    // shared streams: the upload on the parent's copy stream once the child's previous chunk is done
-    // with its device inputs and workspace; the launch stream and (through fork_wait) the aux stream
-    // wait for the upload.  Own streams: all of it in order on the child's stream.
-    hipStream_t s = w->stream, cs = shared ? c->copy : w->stream;
-    if (shared && w->used) HIPCHK(hipStreamWaitEvent(cs, w->ev_free, 0));
-    if (tr.on) {
-      trow.stage1 = tr.ms(PipeTrace::clk::now());
-      trow.a = tr.ev(cs);
-    }
-    HIPCHK(hipMemcpyAsync(w->dev_in.p, w->pin_in.p, o[8], hipMemcpyHostToDevice, cs));
-    HIPCHK(hipEventRecord(w->ev_h2d, cs));
-    w->h2d_pending = true;
-    if (tr.on) trow.b = tr.ev(cs);
-    if (shared) {
-      HIPCHK(hipStreamWaitEvent(s, w->ev_h2d, 0));
-      w->fork_wait = w->ev_h2d;
-    }
-    if (tr.on) trow.h2d1 = tr.ms(PipeTrace::clk::now());
-    uint8_t* d = w->dev_in.as<uint8_t>();
-    hlc_votes dv;
-    dv.n = nv;
-    dv.vote_id = reinterpret_cast<const uint32_t*>(d + o[0]);
-    dv.proposal_id = reinterpret_cast<const uint32_t*>(d + o[1]);
-    dv.timestamp = reinterpret_cast<const uint64_t*>(d + o[2]);
-    dv.vote = d + o[3];
-    dv.field_off = reinterpret_cast<const uint64_t*>(d + o[4]);
-    dv.field_len = reinterpret_cast<const uint32_t*>(d + o[5]);
-    dv.bytes = d + o[7] - a_lo;  // the field offsets stay absolute: bytes + off lands in the staged span
-    dv.bytes_len = a_hi;
-    CHK(w->dev_out.ensure(blk + 16));
-    uint8_t* ob = w->dev_out.as<uint8_t>();
-    CHK(validate_device(w, &dv, reinterpret_cast<const hlc_proposal*>(d + o[6]), npk, now,
-                        reinterpret_cast<hlc_result*>(ob + r[0]), ob + r[1], ob + r[2], out_rec ? ob + r[3] : nullptr,
-                        s));
-    if (tr.on) {
-      trow.c = tr.ev(s);
-      trow.kern1 = tr.ms(PipeTrace::clk::now());
-    }
-    HIPCHK(hipMemcpyAsync(c->pipe_out.at(blk_off[k]), ob, blk, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipEventRecord(c->pipe_ev[k], s));
-    if (shared) {
-      HIPCHK(hipEventRecord(w->ev_free, s));
-      w->used = true;
-    }
-    if (tr.on) {
-      trow.d = tr.ev(s);
-      trow.enq1 = tr.ms(PipeTrace::clk::now());
-      tr.rows.push_back(trow);
-    }
-    // copy out the chunks that are already done, without waiting for any
-    while (next_out < k && hipEventQuery(c->pipe_ev[next_out]) == hipSuccess) copy_out(next_out++);
+    CHK(up(o[2] + 4 * v0, 4 * (v1 - v0)));
+    CHK(up(o[3] + 4 * v0, 4 * (v1 - v0)));
+    CHK(up(o[4] + 8 * v0, 8 * (v1 - v0)));
+    CHK(up(o[5] + v0, v1 - v0));
+    CHK(up(o[6] + 8 * HLC_NFIELDS * v0, 8 * HLC_NFIELDS * (v1 - v0)));
+    CHK(up(o[7] + 4 * HLC_NFIELDS * v0, 4 * HLC_NFIELDS * (v1 - v0)));
+    if (k == 0) CHK(up(o[8], np * sizeof(hlc_proposal)));
+    CHK(up(o[9] + c0, c1 - c0));
   }
-  for (; next_out < ch.size(); ++next_out) {
-    HIPCHK(hipEventSynchronize(c->pipe_ev[next_out]));
-    copy_out(next_out);
-  }
-  for (int k = 0; k < depth; ++k) c->pipe[k]->h2d_pending = false;  // every chunk has completed
-  if (tr.on) tr.print(n, ch.size());
-  // votes between the chunks' ranges are covered by no proposal: not evaluated (as the one-shot path)
-  uint64_t prev = 0;
-  for (size_t k = 0; k <= ch.size(); ++k) {
-    const uint64_t g1 = k < ch.size() ? ch[k].v0 : n;
-    if (g1 > prev) {
-      if (out_st) std::memset(out_st + prev, 0xFF, g1 - prev);
-      if (out_rs) std::memset(out_rs + prev, 0, g1 - prev);
-      if (out_rec) std::memset(out_rec + 20 * prev, 0, 20 * (g1 - prev));
+  tr.mark("rest_staged");
+  HIPCHK(hipEventRecord(c->ev_rest, c->copy));
+  tr.ev("rest_landed", c->copy);
+  // the validation on the launch stream, the two recovery ranges joined in by their events
+  hipStream_t s = c->stream;
+  HIPCHK(hipStreamWaitEvent(s, c->ev_rest, 0));
+  hlc_votes dv;
+  dv.n = n;
+  dv.vote_id = reinterpret_cast<const uint32_t*>(D + o[2]);
+  dv.proposal_id = reinterpret_cast<const uint32_t*>(D + o[3]);
+  dv.timestamp = reinterpret_cast<const uint64_t*>(D + o[4]);
+  dv.vote = D + o[5];
+  dv.field_off = reinterpret_cast<const uint64_t*>(D + o[6]);
+  dv.field_len = reinterpret_cast<const uint32_t*>(D + o[7]);
+  dv.bytes = D + o[9];
+  dv.bytes_len = blen;
+  uint8_t* ob = c->dev_out.as<uint8_t>();
+  RecFront fronts[2];
+  int nf = 0;
+  for (int k = 0; k < 2; ++k)
+    if (rv1[k] > rv0[k]) fronts[nf++] = RecFront{rv0[k], rv1[k], work[k], c->ev_main[k]};
+  CHK(validate_device(c, &dv, reinterpret_cast<const hlc_proposal*>(D + o[8]), np, now,
+                      reinterpret_cast<hlc_result*>(ob + r[0]), ob + r[1], ob + r[2], out_rec ? ob + r[3] : nullptr, s,
+                      fronts, nf));
+  tr.ev("kernels_end", s);
+  HIPCHK(hipMemcpyAsync(c->pin_out.p, ob, r[4], hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(c->ev_done, s));
+  tr.ev("outputs_landed", s);
+  tr.mark("enqueued");
+  for (int x : bad) {
+    if (x) {
+      drain();
+      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
     }
-    if (k < ch.size()) prev = std::max(prev, ch[k].v1);
   }
+  HIPCHK(hipEventSynchronize(c->ev_done));
+  tr.mark("device_done");
+  const uint8_t* src = c->pin_out.at(0);
+  pool.run([&](int t, int T) {
+    const uint64_t b0 = np * t / T, b1 = np * (t + 1) / T, a0 = n * t / T, a1 = n * (t + 1) / T;
+    if (b1 > b0) std::memcpy(out_res + b0, src + r[0] + b0 * sizeof(hlc_result), (b1 - b0) * sizeof(hlc_result));
+    if (a1 > a0) {
+      if (out_st) std::memcpy(out_st + a0, src + r[1] + a0, a1 - a0);
+      if (out_rs) std::memcpy(out_rs + a0, src + r[2] + a0, a1 - a0);
+      if (out_rec) std::memcpy(out_rec + 20 * a0, src + r[3] + 20 * a0, 20 * (a1 - a0));
+    }
+  });
+  tr.mark("outputs_copied");
   return 0;
 }
 
@@ -1154,8 +996,6 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
   c->device = device;
   if (const char* fx = std::getenv("HLC_REC_FORCE_EXACT")) c->rec_force_exact = std::atoi(fx) != 0;
   if (const char* ss = std::getenv("HLC_SERIAL_STAGES")) c->serial_stages = std::atoi(ss) != 0;
-  if (const char* pf = std::getenv("HLC_PREP_FIRST")) c->prep_first = std::atoi(pf) != 0;
-  if (const char* ap = std::getenv("HLC_AUX_PRIO")) c->aux_prio = std::atoi(ap) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       create_aux(c) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -1192,10 +1032,6 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
 void hlc_ctx_destroy(hlc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  for (auto& ch : ctx->pipe) {  // children first: they borrow the parent's fixed-base tables
-    destroy_ctx(ch);
-    ch = nullptr;
-  }
   destroy_ctx(ctx);
 }
 
@@ -1320,32 +1156,8 @@ int hlc_validate_proposals(hlc_ctx* ctx, const hlc_votes* votes, const hlc_propo
   if (votes->n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
-  {
-    bool used = false;
-    CHK(validate_pipelined(ctx, votes, proposals, n_proposals, now, out_results, out_vote_status, out_vote_reason,
-                           out_recovered, &used));
-    if (used) return 0;
-  }
-  CHK(check_votes_host(votes));
-  hipStream_t s = ctx->stream;
-  const uint64_t n = votes->n;
-  hlc_votes dv;
-  CHK(stage_votes(ctx, votes, &dv, s));
-  CHK(upload(ctx->in_props, proposals, n_proposals, s));
-  CHK(ctx->out_res.ensure(n_proposals * sizeof(hlc_result) + 16));
-  CHK(ctx->out_status.ensure(n + 1));
-  CHK(ctx->out_reason.ensure(n + 1));
-  if (out_recovered) CHK(ctx->out_rec.ensure(n * 20 + 20));
-  CHK(validate_device(ctx, &dv, ctx->in_props.as<hlc_proposal>(), n_proposals, now, ctx->out_res.as<hlc_result>(),
-                      ctx->out_status.as<uint8_t>(), ctx->out_reason.as<uint8_t>(),
-                      out_recovered ? ctx->out_rec.as<uint8_t>() : nullptr, s));
-  if (n_proposals)
-    HIPCHK(hipMemcpyAsync(out_results, ctx->out_res.p, n_proposals * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
-  if (out_vote_status && n) HIPCHK(hipMemcpyAsync(out_vote_status, ctx->out_status.p, n, hipMemcpyDeviceToHost, s));
-  if (out_vote_reason && n) HIPCHK(hipMemcpyAsync(out_vote_reason, ctx->out_reason.p, n, hipMemcpyDeviceToHost, s));
-  if (out_recovered && n) HIPCHK(hipMemcpyAsync(out_recovered, ctx->out_rec.p, n * 20, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  return 0;
+  return validate_host(ctx, votes, proposals, n_proposals, now, out_results, out_vote_status, out_vote_reason,
+                       out_recovered);
 }
 
 int hlc_decode_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire_len, const uint64_t* msg_off,

@@ -38,10 +38,16 @@ constexpr uint32_t PREP_SKIP = 0xFFu;  // record flags bits 8-15: no 65-byte sig
 // 1 + the scheme code (prep's v / r / s checks, or no point R)
 constexpr uint8_t MST_OK = 0x00, MST_INF = 0xFE, MST_SKIP = 0xFF;
 
+// Vote i's signature: bytes + sig_off[i * off_stride], or (sig_off == nullptr) the dense array the
+// host-buffer entry uploads ahead of the other inputs, 65 bytes per vote at bytes + 65 i.
+HLC_DEV const uint8_t* sig_at(const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride, uint64_t i) {
+  return sig_off ? bytes + sig_off[i * off_stride] : bytes + 65 * i;
+}
+
 HLC_DEV bool prep_sig(const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len,
                       size_t len_stride, uint64_t i, fe& r, fe& s, int& parity, int& code) {
   if (sig_len[i * len_stride] != 65u) return false;  // rejected by the pre-checks (length)
-  const uint8_t* sig = bytes + sig_off[i * off_stride];
+  const uint8_t* sig = sig_at(bytes, sig_off, off_stride, i);
   fe_load_be(r, sig);
   fe_load_be(s, sig + 32);
   code = rec_parse(s, r, sig[64], parity);
@@ -195,7 +201,7 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
     }
     fe r, qx, qy, qz;
     bool inf = false;
-    fe_load_be(r, bytes + sig_off[i * off_stride]);
+    fe_load_be(r, sig_at(bytes, sig_off, off_stride, i));
     const int code = rec_u2r29(r, rec + i, n, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0, lds);
     if (code != SCHEME_NONE) {
       mst[i] = (uint8_t)(1 + code);

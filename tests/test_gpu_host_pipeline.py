@@ -1,9 +1,13 @@
-"""The pipelined host-buffer entry (hlc_validate_proposals cut into proposal chunks that take turns
-on 2-4 child contexts, HLC_PIPE_DEPTH; hlc_api.cpp validate_pipelined) equals the one-shot path and the C
-oracle bit for bit: per-proposal results, per-vote statuses, scheme reasons and recovered
-addresses, on a Byzantine batch; also with empty proposals, votes no proposal covers (gaps between
-chunks: status 0xFF), a batch whose proposal ranges are out of order (the one-shot fallback), and
-an out-of-arena field in a late chunk (HLC_EINVAL, no device access)."""
+"""The host-buffer entry hlc_validate_proposals (hlc_api.cpp validate_host: signatures staged and
+uploaded first as a dense array, the recovery's front half over two vote ranges on two streams, the
+other inputs in pieces behind them) equals the single-range schedule and the C oracle bit for bit:
+per-proposal results, per-vote statuses, scheme reasons and recovered addresses, on a Byzantine
+batch; also with empty proposals, votes no proposal covers (status 0xFF), proposals listed out of
+vote order, and an out-of-arena field -- a signature in the second range or another field in a late
+piece -- which returns HLC_EINVAL with the caller's outputs untouched (the device work already
+enqueued is drained and discarded).  Schedule knobs: HLC_SPLIT_FIRST_VOTES (votes in the first
+range, 0 = one range), HLC_REST_PIECES."""
+import ctypes
 import os
 
 import numpy as np
@@ -12,20 +16,21 @@ import pytest
 import coracle
 from adversarial import byzantine
 from hashgraph_like_consensus import _ffi
+from hashgraph_like_consensus.batch import proposals_ptr, results_ptr
 from helpers import oracle_workload
 
 pytestmark = pytest.mark.gpu
+HLC_EINVAL = -1  # include/hlc.h
 
 
-def _run(engine, batch, desc, now, chunk, depth=None):
-    os.environ["HLC_PIPE_CHUNK_VOTES"] = str(chunk)
-    if depth is not None:
-        os.environ["HLC_PIPE_DEPTH"] = str(depth)
+def _run(engine, batch, desc, now, split, pieces=3):
+    os.environ["HLC_SPLIT_FIRST_VOTES"] = str(split)
+    os.environ["HLC_REST_PIECES"] = str(pieces)
     try:
         return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
     finally:
-        os.environ.pop("HLC_PIPE_CHUNK_VOTES", None)
-        os.environ.pop("HLC_PIPE_DEPTH", None)
+        os.environ.pop("HLC_SPLIT_FIRST_VOTES", None)
+        os.environ.pop("HLC_REST_PIECES", None)
 
 
 @pytest.fixture(scope="module")
@@ -35,48 +40,76 @@ def byz():
     return b, d, w.now
 
 
-@pytest.mark.parametrize("chunk,depth", [(100, 3), (240, 3), (333, 3), (100, 2), (100, 4)])
-def test_gpu_pipeline_equals_one_shot_and_oracle(engine, byz, chunk, depth):
+@pytest.mark.parametrize("split,pieces", [(100, 3), (240, 1), (333, 7), (100, 64), (1, 2), (0, 5)])
+def test_gpu_host_entry_equals_single_range_and_oracle(engine, byz, split, pieces):
     b, d, now = byz
-    one = _run(engine, b, d, now, 0)
-    pip = _run(engine, b, d, now, chunk, depth)
-    for x, y in zip(one, pip):
+    one = _run(engine, b, d, now, 0, 1)
+    got = _run(engine, b, d, now, split, pieces)
+    for x, y in zip(one, got):
         assert np.array_equal(x, y)
     cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
-    assert np.array_equal(pip[0], cres) and np.array_equal(pip[1], cvst)
-    assert np.array_equal(pip[2], cvrs) and np.array_equal(pip[3], crec)
-    assert len({int(s) for s in pip[0]["status"]}) > 3
+    assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
+    assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec)
+    assert len({int(s) for s in got[0]["status"]}) > 3
 
 
-def test_gpu_pipeline_gaps_and_empty_proposals(engine, byz):
+def test_gpu_host_entry_gaps_and_empty_proposals(engine, byz):
     b, d, now = byz
     d2 = d.copy()
     d2["vote_count"][3] = 0            # an empty proposal (StillActive)
     d2["vote_count"][10] -= 5          # its last 5 votes are covered by no proposal
     d2["vote_count"][25] = 0
-    one = _run(engine, b, d2, now, 0)
-    pip = _run(engine, b, d2, now, 100)
-    for x, y in zip(one, pip):
+    one = _run(engine, b, d2, now, 0, 1)
+    got = _run(engine, b, d2, now, 100)
+    for x, y in zip(one, got):
         assert np.array_equal(x, y)
+    cres, cvst, _, _ = coracle.validate_proposals(b, d2, now, threads=8)
+    assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
     gap = int(d2["vote_begin"][10] + d2["vote_count"][10])
-    assert (pip[1][gap:gap + 5] == 0xFF).all()
+    assert (got[1][gap:gap + 5] == 0xFF).all()
 
 
-def test_gpu_pipeline_out_of_order_falls_back(engine, byz):
+def test_gpu_host_entry_out_of_order_proposals(engine, byz):
     b, d, now = byz
-    d2 = d[::-1].copy()  # proposals listed in reverse vote order: chunks would interleave
-    one = _run(engine, b, d2, now, 0)
-    pip = _run(engine, b, d2, now, 100)
-    for x, y in zip(one, pip):
+    d2 = d[::-1].copy()  # proposals listed in reverse vote order
+    one = _run(engine, b, d2, now, 0, 1)
+    got = _run(engine, b, d2, now, 100)
+    for x, y in zip(one, got):
         assert np.array_equal(x, y)
+    cres, _, _, _ = coracle.validate_proposals(b, d2, now, threads=8)
+    assert np.array_equal(got[0], cres)
 
 
-def test_gpu_pipeline_rejects_bad_field_in_late_chunk(engine, byz):
+def _raw_call(engine, batch, desc, now, split):
+    """hlc_validate_proposals through ctypes with outputs pre-filled with 0xAB: -> (rc, outputs)."""
+    n = batch.n
+    res = np.full(desc.shape[0], 0xAB, np.uint8).repeat(16).view(_ffi.RESULT_DTYPE)
+    st = np.full(n, 0xAB, np.uint8)
+    rs = np.full(n, 0xAB, np.uint8)
+    rec = np.full((n, 20), 0xAB, np.uint8)
+    view = batch.view()
+    desc = np.ascontiguousarray(desc)
+    os.environ["HLC_SPLIT_FIRST_VOTES"] = str(split)
+    try:
+        rc = engine.lib.hlc_validate_proposals(engine.ctx, ctypes.byref(view), proposals_ptr(desc), desc.shape[0], now,
+                                               results_ptr(res), _ffi.ptr(st, ctypes.c_uint8),
+                                               _ffi.ptr(rs, ctypes.c_uint8), _ffi.ptr(rec, ctypes.c_uint8))
+    finally:
+        os.environ.pop("HLC_SPLIT_FIRST_VOTES", None)
+    return rc, (res.view(np.uint8), st, rs, rec)
+
+
+@pytest.mark.parametrize("field,where", [(4, "second range"), (2, "late piece"), (0, "late piece")])
+def test_gpu_host_entry_rejects_bad_field_outputs_untouched(engine, byz, field, where):
     b, d, now = byz
     off = b.field_off.copy()
-    off[b.n - 3, 4] = b.arena.size + 10  # signature past the arena, in the last chunk
+    # a vote in the second recovery range and in the last staging piece whose field is non-empty
+    i = max(j for j in range(b.n - 20, b.n) if int(b.field_len[j, field]) > 0)
+    off[i, field] = b.arena.size + 10
     bad = b.__class__(b.vote_id, b.proposal_id, b.timestamp, b.vote, b.arena, off, b.field_len)
-    with pytest.raises(_ffi.HlcError):
-        _run(engine, bad, d, now, 100)
+    rc, outs = _raw_call(engine, bad, d, now, 100)
+    assert rc == HLC_EINVAL, where
+    for o in outs:
+        assert (o == 0xAB).all(), "outputs were written on error"
     ok = _run(engine, b, d, now, 100)  # the context is still usable
-    assert np.array_equal(ok[1], _run(engine, b, d, now, 0)[1])
+    assert np.array_equal(ok[1], _run(engine, b, d, now, 0, 1)[1])
