@@ -771,6 +771,80 @@ struct HostTrace {
   }
 };
 
+// One call's page-locked staging buffer P, its device copy D and the upload stream.
+struct Staging {
+  hlc_ctx* c;
+  uint8_t* P;
+  uint8_t* D;
+  int up(size_t off, size_t len) {
+    if (len) HIPCHK(hipMemcpyAsync(D + off, P + off, len, hipMemcpyHostToDevice, c->copy));
+    return 0;
+  }
+  void drain() {
+    for (hipStream_t x : {c->copy, c->aux, c->aux2, c->stream}) (void)hipStreamSynchronize(x);
+  }
+};
+
+// The recovery's front half of a host-buffer call: the signatures of items [0, na) and [na, n)
+// (sig_off / sig_len with stride `stride`) gathered by the host pool into the dense array at o_sig
+// (65 B per item; zero-filled slots for other lengths) and their lengths at o_len, each range
+// uploaded and its k_rec_prep + k_rec_main enqueued on its own stream (recovery slots 1 and 2) as
+// soon as its DMA is enqueued.  HLC_EINVAL, before its bytes are read, for a 65-byte signature
+// outside the arena.
+int launch_fronts(hlc_ctx* c, Staging& st, HostTrace& tr, uint64_t n, uint64_t na, const uint8_t* bytes,
+                  uint64_t bytes_len, const uint64_t* sig_off, const uint32_t* sig_len, size_t stride, size_t o_sig,
+                  size_t o_len, RecFront fronts[2], int* nf) {
+  HostPool& pool = *c->pool;
+  const int parts = pool.parts();
+  uint32_t* work[2] = {c->rec_work.as<uint32_t>(), c->rec_work2.as<uint32_t>()};
+  uint32_t* scratch[2] = {c->rec_scratch.as<uint32_t>(), c->rec_scratch2.as<uint32_t>()};
+  hipStream_t aux[2] = {c->aux, c->aux2};
+  const uint64_t rv0[2] = {0, na}, rv1[2] = {na, n};
+  *nf = 0;
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t a0 = rv0[k], m = rv1[k] - rv0[k];
+    if (!m) continue;
+    std::vector<int> bad(parts, 0);
+    pool.run([&](int t, int T) {
+      const uint64_t b0 = a0 + m * t / T, b1 = a0 + m * (t + 1) / T;
+      uint8_t* sg = st.P + o_sig;
+      uint32_t* sl = reinterpret_cast<uint32_t*>(st.P + o_len);
+      for (uint64_t i = b0; i < b1; ++i) {
+        const uint64_t off = sig_off[i * stride];
+        const uint32_t len = sig_len[i * stride];
+        sl[i] = len;
+        if (len != 65) continue;  // the prep stage skips it (a length error decided elsewhere)
+        if (!bytes || off + 65 > bytes_len || off + 65 < off) {
+          bad[t] = 1;
+          return;
+        }
+        std::memcpy(sg + 65 * i, bytes + off, 65);
+      }
+    });
+    for (int x : bad) {
+      if (x) {
+        st.drain();
+        return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+      }
+    }
+    tr.mark(k ? "sigs_b_staged" : "sigs_a_staged");
+    CHK(st.up(o_sig + 65 * a0, 65 * m));
+    CHK(st.up(o_len + 4 * a0, 4 * m));
+    HIPCHK(hipEventRecord(c->ev_sig[k], c->copy));
+    tr.ev(k ? "sigs_b_landed" : "sigs_a_landed", c->copy);
+    HIPCHK(hipStreamWaitEvent(aux[k], c->ev_sig[k], 0));
+    const uint8_t* sb = st.D + o_sig + 65 * a0;
+    const uint32_t* sl = reinterpret_cast<const uint32_t*>(st.D + o_len) + a0;
+    hlc::launch_recover_prep(m, sb, nullptr, 0, sl, 1, work[k], aux[k]);
+    hlc::launch_recover_main(m, sb, nullptr, 0, scratch[k], c->rec_lanes, work[k], aux[k], c->rec_force_exact);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_main[k], aux[k]));
+    tr.ev(k ? "main_b_end" : "main_a_end", aux[k]);
+    fronts[(*nf)++] = RecFront{a0, a0 + m, work[k], c->ev_main[k]};
+  }
+  return 0;
+}
+
 // hlc_validate_proposals over host buffers (what INTEGRATION.md's process_incoming_proposals calls).
 // The caller's votes go to the device through page-locked staging on the context's upload stream,
 // ordered by what the kernels need first, so that the VALU-bound recovery starts long before the
@@ -829,65 +903,15 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   CHK(c->dev_out.ensure(r[4] + 16));
   CHK(reserve_validate(c, n, np));  // slot 1's records are sized for n >= na
   if (nb) CHK(c->rec_work2.ensure(hlc::recover_work_words(nb) * sizeof(uint32_t)));
-  uint8_t* P = c->pin_in.at(0);
-  uint8_t* D = c->dev_in.as<uint8_t>();
-  auto up = [&](size_t off, size_t len) -> int {
-    if (len) HIPCHK(hipMemcpyAsync(D + off, P + off, len, hipMemcpyHostToDevice, c->copy));
-    return 0;
-  };
-  auto drain = [&]() {
-    for (hipStream_t x : {c->copy, c->aux, c->aux2, c->stream}) (void)hipStreamSynchronize(x);
-  };
+  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  uint8_t* P = st.P;
+  uint8_t* D = st.D;
+  auto up = [&](size_t off, size_t len) { return st.up(off, len); };
   const int parts = pool.parts();
-  // signatures of votes [a0, a1) -> the dense array and the length array; false: one lies outside
-  // the arena (its bytes are not read)
-  auto stage_sigs = [&](uint64_t a0, uint64_t a1) -> bool {
-    std::vector<int> bad(parts, 0);
-    pool.run([&](int t, int T) {
-      const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
-      uint8_t* sg = P + o[0];
-      uint32_t* sl = reinterpret_cast<uint32_t*>(P + o[1]);
-      for (uint64_t i = b0; i < b1; ++i) {
-        const uint64_t off = v->field_off[i * HLC_NFIELDS + HLC_F_SIGNATURE];
-        const uint32_t len = v->field_len[i * HLC_NFIELDS + HLC_F_SIGNATURE];
-        sl[i] = len;
-        if (len != 65) continue;  // the prep stage skips it (the pre-checks reject it by length)
-        if (!v->bytes || off + 65 > v->bytes_len || off + 65 < off) {
-          bad[t] = 1;
-          return;
-        }
-        std::memcpy(sg + 65 * i, v->bytes + off, 65);
-      }
-    });
-    for (int x : bad)
-      if (x) return false;
-    return true;
-  };
-  uint32_t* work[2] = {c->rec_work.as<uint32_t>(), c->rec_work2.as<uint32_t>()};
-  uint32_t* scratch[2] = {c->rec_scratch.as<uint32_t>(), c->rec_scratch2.as<uint32_t>()};
-  hipStream_t aux[2] = {c->aux, c->aux2};
-  const uint64_t rv0[2] = {0, na}, rv1[2] = {na, n};
-  for (int k = 0; k < 2; ++k) {
-    const uint64_t a0 = rv0[k], m = rv1[k] - rv0[k];
-    if (!m) continue;
-    if (!stage_sigs(a0, a0 + m)) {
-      drain();
-      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-    }
-    tr.mark(k ? "sigs_b_staged" : "sigs_a_staged");
-    CHK(up(o[0] + 65 * a0, 65 * m));
-    CHK(up(o[1] + 4 * a0, 4 * m));
-    HIPCHK(hipEventRecord(c->ev_sig[k], c->copy));
-    tr.ev(k ? "sigs_b_landed" : "sigs_a_landed", c->copy);
-    HIPCHK(hipStreamWaitEvent(aux[k], c->ev_sig[k], 0));
-    const uint8_t* sb = D + o[0] + 65 * a0;
-    const uint32_t* sl = reinterpret_cast<const uint32_t*>(D + o[1]) + a0;
-    hlc::launch_recover_prep(m, sb, nullptr, 0, sl, 1, work[k], aux[k]);
-    hlc::launch_recover_main(m, sb, nullptr, 0, scratch[k], c->rec_lanes, work[k], aux[k], c->rec_force_exact);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev_main[k], aux[k]));
-    tr.ev(k ? "main_b_end" : "main_a_end", aux[k]);
-  }
+  RecFront fronts[2];
+  int nf = 0;
+  CHK(launch_fronts(c, st, tr, n, na, v->bytes, v->bytes_len, v->field_off + HLC_F_SIGNATURE,
+                    v->field_len + HLC_F_SIGNATURE, HLC_NFIELDS, o[0], o[1], fronts, &nf));
   // everything else, piece by piece, field checks on the way
   const int K = rest_pieces();
   std::vector<int> bad(parts, 0);
@@ -940,10 +964,6 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   dv.bytes = D + o[9];
   dv.bytes_len = blen;
   uint8_t* ob = c->dev_out.as<uint8_t>();
-  RecFront fronts[2];
-  int nf = 0;
-  for (int k = 0; k < 2; ++k)
-    if (rv1[k] > rv0[k]) fronts[nf++] = RecFront{rv0[k], rv1[k], work[k], c->ev_main[k]};
   CHK(validate_device(c, &dv, reinterpret_cast<const hlc_proposal*>(D + o[8]), np, now,
                       reinterpret_cast<hlc_result*>(ob + r[0]), ob + r[1], ob + r[2], out_rec ? ob + r[3] : nullptr, s,
                       fronts, nf));
@@ -954,7 +974,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   tr.mark("enqueued");
   for (int x : bad) {
     if (x) {
-      drain();
+      st.drain();
       return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
     }
   }
@@ -968,6 +988,124 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
       if (out_st) std::memcpy(out_st + a0, src + r[1] + a0, a1 - a0);
       if (out_rs) std::memcpy(out_rs + a0, src + r[2] + a0, a1 - a0);
       if (out_rec) std::memcpy(out_rec + 20 * a0, src + r[3] + 20 * a0, 20 * (a1 - a0));
+    }
+  });
+  tr.mark("outputs_copied");
+  return 0;
+}
+
+// hlc_eth_verify_batch over host buffers: the same schedule as validate_host -- the signatures
+// first (dense, two recovery ranges on two streams), then identities, payloads and the arena in
+// pieces, field checks on the way -- with the verify byte stage (length checks + EIP-191 keccak of
+// each payload, k_verify_prehash) on the launch stream, each range's finish after its main stage,
+// one D2H of the statuses (and addresses).  An (offset, length) outside the arena returns
+// HLC_EINVAL before anything reaches the caller's outputs.
+int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len, const uint64_t* id_off,
+                const uint32_t* id_len, const uint64_t* pay_off, const uint32_t* pay_len, const uint64_t* sig_off,
+                const uint32_t* sig_len, uint8_t* out_status, uint8_t* out_addr) {
+  const uint64_t blen = bytes ? bytes_len : 0;
+  CHK(host_resources(c));
+  HostPool& pool = *c->pool;
+  HostTrace tr;
+  if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
+  tr.start(c->copy);
+  const uint64_t first = split_first_votes();
+  const uint64_t na = first && n >= 2 * first ? first : n;
+  // inputs: dense signatures | signature lengths | identity lengths | payload lengths | identity
+  // offsets | payload offsets | arena
+  size_t o[8];
+  o[0] = 0;
+  o[1] = o[0] + al256(n * 65);
+  o[2] = o[1] + al256(n * 4);
+  o[3] = o[2] + al256(n * 4);
+  o[4] = o[3] + al256(n * 4);
+  o[5] = o[4] + al256(n * 8);
+  o[6] = o[5] + al256(n * 8);
+  o[7] = o[6] + blen;
+  const size_t r1 = al256(n + 1), r2 = r1 + (out_addr ? al256(n * 20) : 0);  // statuses | addresses
+  CHK(c->pin_in.ensure(o[7] + 16));
+  CHK(c->dev_in.ensure(o[7] + 16));
+  CHK(c->pin_out.ensure(r2 + 16));
+  CHK(c->dev_out.ensure(r2 + 16));
+  CHK(c->pre.ensure(n + 1));
+  CHK(c->kec_dig.ensure(n * 32 + 32));
+  CHK(c->rec_work.ensure(hlc::recover_work_words(na) * sizeof(uint32_t)));
+  if (n > na) CHK(c->rec_work2.ensure(hlc::recover_work_words(n - na) * sizeof(uint32_t)));
+  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  RecFront fronts[2];
+  int nf = 0;
+  CHK(launch_fronts(c, st, tr, n, na, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], fronts, &nf));
+  const int K = rest_pieces(), parts = pool.parts();
+  std::vector<int> bad(parts, 0);
+  for (int k = 0; k < K; ++k) {
+    const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K, c0 = blen * k / K, c1 = blen * (k + 1) / K;
+    pool.run([&](int t, int T) {
+      const uint64_t b0 = v0 + (v1 - v0) * t / T, b1 = v0 + (v1 - v0) * (t + 1) / T, m = b1 - b0;
+      if (m) {
+        std::memcpy(st.P + o[2] + 4 * b0, id_len + b0, 4 * m);
+        std::memcpy(st.P + o[3] + 4 * b0, pay_len + b0, 4 * m);
+        std::memcpy(st.P + o[4] + 8 * b0, id_off + b0, 8 * m);
+        std::memcpy(st.P + o[5] + 8 * b0, pay_off + b0, 8 * m);
+        for (uint64_t i = b0; i < b1; ++i) {
+          const uint64_t f[3][2] = {{id_off[i], id_len[i]}, {pay_off[i], pay_len[i]}, {sig_off[i], sig_len[i]}};
+          for (const auto& x : f) {
+            if (x[0] + x[1] > bytes_len || x[0] + x[1] < x[0] || (x[1] && !bytes)) {
+              bad[t] = 1;
+              return;
+            }
+          }
+        }
+      }
+      const uint64_t d0 = c0 + (c1 - c0) * t / T, d1 = c0 + (c1 - c0) * (t + 1) / T;
+      if (d1 > d0) std::memcpy(st.P + o[6] + d0, bytes + d0, d1 - d0);
+    });
+    for (int q = 2; q <= 3; ++q) CHK(st.up(o[q] + 4 * v0, 4 * (v1 - v0)));
+    for (int q = 4; q <= 5; ++q) CHK(st.up(o[q] + 8 * v0, 8 * (v1 - v0)));
+    CHK(st.up(o[6] + c0, c1 - c0));
+  }
+  tr.mark("rest_staged");
+  HIPCHK(hipEventRecord(c->ev_rest, c->copy));
+  tr.ev("rest_landed", c->copy);
+  hipStream_t s = c->stream;
+  HIPCHK(hipStreamWaitEvent(s, c->ev_rest, 0));
+  const uint8_t* D = st.D;
+  const uint8_t* dbytes = D + o[6];
+  const uint64_t* did_off = reinterpret_cast<const uint64_t*>(D + o[4]);
+  uint8_t* ob = c->dev_out.as<uint8_t>();
+  uint8_t* dstat = ob;
+  uint8_t* daddr = out_addr ? ob + r1 : nullptr;
+  hlc::launch_verify_prehash(n, dbytes, reinterpret_cast<const uint64_t*>(D + o[5]),
+                             reinterpret_cast<const uint32_t*>(D + o[3]), reinterpret_cast<const uint32_t*>(D + o[1]),
+                             reinterpret_cast<const uint32_t*>(D + o[2]), c->kec_dig.as<uint32_t>(),
+                             c->pre.as<uint8_t>(), dstat, s);
+  if (daddr) HIPCHK(hipMemsetAsync(daddr, 0, n * 20, s));
+  for (int k = 0; k < nf; ++k) {
+    const RecFront& f = fronts[k];
+    HIPCHK(hipStreamWaitEvent(s, f.done, 0));
+    hlc::launch_recover_finish(f.v1 - f.v0, c->pre.as<uint8_t>() + f.v0, c->kec_dig.as<uint32_t>() + 8 * f.v0, dbytes,
+                               did_off + f.v0, 1, c->gtab.as<uint32_t>(), f.work, dstat + f.v0,
+                               daddr ? daddr + 20 * f.v0 : nullptr, s, c->rec_force_exact);
+  }
+  HIPCHK(hipGetLastError());
+  tr.ev("kernels_end", s);
+  HIPCHK(hipMemcpyAsync(c->pin_out.p, ob, r2, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(c->ev_done, s));
+  tr.ev("outputs_landed", s);
+  tr.mark("enqueued");
+  for (int x : bad) {
+    if (x) {
+      st.drain();
+      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
+    }
+  }
+  HIPCHK(hipEventSynchronize(c->ev_done));
+  tr.mark("device_done");
+  const uint8_t* src = c->pin_out.at(0);
+  pool.run([&](int t, int T) {
+    const uint64_t a0 = n * t / T, a1 = n * (t + 1) / T;
+    if (a1 > a0) {
+      std::memcpy(out_status + a0, src + a0, a1 - a0);
+      if (out_addr) std::memcpy(out_addr + 20 * a0, src + r1 + 20 * a0, 20 * (a1 - a0));
     }
   });
   tr.mark("outputs_copied");
@@ -1398,46 +1536,11 @@ int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_
                          const uint64_t* sig_off, const uint32_t* sig_len, uint8_t* out_status, uint8_t* out_addr) {
   if (!ctx || (n && (!id_off || !id_len || !payload_off || !payload_len || !sig_off || !sig_len || !out_status)))
     return set_err(HLC_EINVAL, "NULL argument");
-  for (uint64_t i = 0; i < n; ++i) {
-    if (id_off[i] + id_len[i] > bytes_len || payload_off[i] + payload_len[i] > bytes_len ||
-        sig_off[i] + sig_len[i] > bytes_len)
-      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
-  }
   if (!n) return 0;
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
-  hipStream_t s = ctx->stream;
-  CHK(upload(ctx->in_bytes, bytes, bytes_len, s));
-  CHK(upload(ctx->in_off, id_off, n, s));
-  CHK(upload(ctx->in_len, id_len, n, s));
-  CHK(upload(ctx->in_off2, payload_off, n, s));
-  CHK(upload(ctx->in_len2, payload_len, n, s));
-  CHK(upload(ctx->in_off3, sig_off, n, s));
-  CHK(upload(ctx->in_len3, sig_len, n, s));
-  const uint8_t* dbytes = ctx->in_bytes.as<uint8_t>();
-  CHK(run_prehash(ctx, nullptr, n, hlc::MSG_PAYLOAD, dbytes, ctx->in_off2.as<uint64_t>(), ctx->in_len2.as<uint32_t>(), s));
-  CHK(ctx->pre.ensure(n));
-  CHK(ctx->verify.ensure(n));
-  hlc::launch_verify_pre(n, ctx->in_len3.as<uint32_t>(), ctx->in_len.as<uint32_t>(), ctx->pre.as<uint8_t>(),
-                         ctx->verify.as<uint8_t>(), s);
-  CHK(ensure_recover_scratch(ctx));
-  uint8_t* drec = nullptr;
-  if (out_addr) {
-    CHK(ctx->out_rec.ensure(n * 20 + 20));
-    drec = ctx->out_rec.as<uint8_t>();
-    HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
-  }
-  CHK(ctx->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
-  hlc::launch_recover(n, ctx->pre.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), dbytes, ctx->in_off3.as<uint64_t>(),
-                      ctx->in_off.as<uint64_t>(), 1, ctx->in_len3.as<uint32_t>(), 1, ctx->gtab.as<uint32_t>(),
-                      ctx->rec_scratch.as<uint32_t>(),
-                      ctx->rec_lanes, ctx->rec_work.as<uint32_t>(), ctx->verify.as<uint8_t>(), drec, s,
-                      ctx->rec_force_exact);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(out_status, ctx->verify.p, n, hipMemcpyDeviceToHost, s));
-  if (out_addr) HIPCHK(hipMemcpyAsync(out_addr, drec, n * 20, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  return 0;
+  return verify_host(ctx, n, bytes, bytes_len, id_off, id_len, payload_off, payload_len, sig_off, sig_len, out_status,
+                     out_addr);
 }
 
 int hlc_consensus_timeout_batch(hlc_ctx* ctx, uint64_t n, const hlc_session_tally* sessions, uint8_t* out_state,

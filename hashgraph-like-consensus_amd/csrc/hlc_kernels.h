@@ -41,9 +41,11 @@ void launch_keccak_blocks(uint64_t n, const uint64_t* off, const uint64_t* sz, c
 // exclusive prefix sum of u64 sizes (hipcub); temp == nullptr queries temp_bytes
 hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
                            hipStream_t s);
-// hlc_eth_verify_batch length checks (ethereum.rs:71-82): pre[i] = PRE_PENDING or verify_out set
-void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
-                       uint8_t* verify_out, hipStream_t s);
+// hlc_eth_verify_batch over host-staged items: the length checks (ethereum.rs:71-82) and the
+// EIP-191 keccak of each payload streamed from the arena (dense per-item arrays, stride 1)
+void launch_verify_prehash(uint64_t n, const uint8_t* bytes, const uint64_t* pay_off, const uint32_t* pay_len,
+                           const uint32_t* sig_len, const uint32_t* id_len, uint32_t* kec_dig, uint8_t* pre,
+                           uint8_t* verify_out, hipStream_t s);
 // fused byte stage (sizes + SHA-256 compare + EIP-191 keccak + pre-status) for votes whose
 // messages fit the per-lane LDS window; others get PRE_GENERAL and *general is set non-zero
 void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
@@ -62,11 +64,8 @@ void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop
 // bytes + sig_off[i*stride_f] etc.  verify_out[i]: HLC_VERIFY_TRUE/FALSE or 1+SCHEME.
 // kernels (hlc_recover.hip): k_rec_prep, k_rec_main, k_rec_comb, k_rec_final, k_rec_addr; `work` holds
 // recover_work_words(n) words of per-vote records for the call
-void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
-                    const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* sig_len,
-                    size_t len_stride, const uint32_t* gtab, uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work,
-                    uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0);
-// the same in three parts: the prep stage reads only the signatures (65-byte ones by sig_len) and
+// in three parts: the prep stage reads only the signatures (65-byte ones by sig_len; sig_off == nullptr:
+// a dense array, 65 B per item at bytes + 65 i) and
 // the main stage (u2 R) only the prep records, so a caller may enqueue both on a second stream
 // concurrently with the prehash kernels; the finish (k_rec_comb: u1 G + the addition; k_rec_final;
 // k_rec_addr) once both are done

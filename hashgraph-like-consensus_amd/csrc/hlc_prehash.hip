@@ -1031,24 +1031,90 @@ __global__ void k_clear_if(const uint32_t* flags, uint32_t bit, uint32_t* tab, u
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += stride) tab[k] = EMPTY_SLOT;
 }
 
-__global__ void k_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
-                             uint8_t* verify_out) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// hlc_eth_verify_batch's byte stage over host-staged items, one lane per item: the length checks
+// of EthereumConsensusSigner::verify (signing/ethereum.rs:71-82: the signature's length first, then
+// the identity's) and, for the items that pass, keccak256 of the EIP-191 message of the payload
+// (alloy eip191_hash_message, reached through recover_address_from_msg at ethereum.rs:89):
+// "\x19Ethereum Signed Message:\n" || decimal(len) || payload, absorbed straight from the arena
+// (rate 136, pad 0x01 .. 0x80) -- no message buffer, no size scan, no host round trip.
+__constant__ uint8_t EIP191_PREFIX[26] = {0x19, 'E', 't', 'h', 'e', 'r', 'e', 'u', 'm', ' ', 'S', 'i', 'g',
+                                          'n',  'e', 'd', ' ', 'M', 'e', 's', 's', 'a', 'g', 'e', ':', '\n'};
+
+__global__ void k_verify_prehash(uint64_t n, const uint8_t* bytes, const uint64_t* pay_off, const uint32_t* pay_len,
+                                 const uint32_t* sig_len, const uint32_t* id_len, uint32_t* kec_dig, uint8_t* pre,
+                                 uint8_t* verify_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (sig_len[i] != 65) {
     pre[i] = 0;
     verify_out[i] = 1 + HLC_SCHEME_SIG_LEN;
-  } else if (id_len[i] != 20) {
+    return;
+  }
+  if (id_len[i] != 20) {
     pre[i] = 0;
     verify_out[i] = 1 + HLC_SCHEME_ID_LEN;
-  } else {
-    pre[i] = PRE_PENDING;
+    return;
+  }
+  pre[i] = PRE_PENDING;
+  const uint32_t len = pay_len[i];
+  const uint8_t* p = bytes + pay_off[i];
+  // decimal digits of len, most significant first
+  uint32_t nd = 1;
+  for (uint32_t x = len; x >= 10; x /= 10) ++nd;
+  const uint64_t H = 26 + nd, L = H + len, nb = L / 136 + 1;
+  uint64_t sk[25];
+#pragma unroll
+  for (int q = 0; q < 25; ++q) sk[q] = 0;
+  uint64_t pos = 0;
+  for (uint64_t b = 0; b < nb; ++b) {
+#pragma unroll 1
+    for (int q = 0; q < 17; ++q) {
+      uint64_t w = 0;
+      if (pos >= H && pos + 8 <= L) {  // eight payload bytes
+        const uint8_t* s8 = p + (pos - H);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) w |= (uint64_t)s8[t] << (8 * t);
+        pos += 8;
+      } else {
+#pragma unroll 1
+        for (int t = 0; t < 8; ++t, ++pos) {
+          uint32_t c;
+          if (pos < 26) {
+            c = EIP191_PREFIX[pos];
+          } else if (pos < H) {
+            uint32_t x = len;
+            for (uint64_t k = pos - 26 + 1; k < nd; ++k) x /= 10;
+            c = '0' + x % 10;
+          } else if (pos < L) {
+            c = p[pos - H];
+          } else {
+            c = (pos == L ? 0x01u : 0u) | (pos == nb * 136 - 1 ? 0x80u : 0u);
+          }
+          w |= (uint64_t)c << (8 * t);
+        }
+      }
+      sk[q] ^= w;
+    }
+    keccak_f1600(sk);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    kec_dig[i * 8 + 2 * q] = (uint32_t)sk[q];
+    kec_dig[i * 8 + 2 * q + 1] = (uint32_t)(sk[q] >> 32);
   }
 }
 
 inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB); }
 
 }  // namespace
+
+void launch_verify_prehash(uint64_t n, const uint8_t* bytes, const uint64_t* pay_off, const uint32_t* pay_len,
+                           const uint32_t* sig_len, const uint32_t* id_len, uint32_t* kec_dig, uint8_t* pre,
+                           uint8_t* verify_out, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_verify_prehash, dim3(blocks_for(n)), dim3(TPB), 0, s, n, bytes, pay_off, pay_len, sig_len,
+                       id_len, kec_dig, pre, verify_out);
+}
 
 hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, void* temp, size_t& temp_bytes,
                                  hipStream_t s) {
@@ -1062,10 +1128,6 @@ void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_p
                        n, vote_prop, props, kec_dig, pre, pre_reason, general);
 }
 
-void launch_verify_pre(uint64_t n, const uint32_t* sig_len, const uint32_t* id_len, uint8_t* pre,
-                       uint8_t* verify_out, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_verify_pre, dim3(blocks_for(n)), dim3(TPB), 0, s, n, sig_len, id_len, pre, verify_out);
-}
 
 hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, const uint32_t* field_len, uint32_t* vote_prop,
                                uint64_t nv,

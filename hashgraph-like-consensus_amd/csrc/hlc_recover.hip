@@ -93,33 +93,9 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
     sc_mont_mul(rinv, prev, cur);  // r_k^-1
     sc_mont_mul(cur, cur, r);      // acc_{k-1}^-1
-#ifndef HLC_PREP_SPLIT
     rec_prep_scalars(s, rinv, parity, rec + i, n);
-#else  // A/B: the per-vote scalar work in k_rec_scalars at full occupancy (measured -0.9%, not kept)
-    store_fe_ws(rinv, rec + (size_t)REC_RINV * n + i, n);  // k_rec_scalars takes it from here
-#endif
   }
 }
-
-// ---- A/B variant -DHLC_PREP_SPLIT: prep's second half as one lane per vote at full occupancy
-// (u2 = s / r, the GLV split of u2 and its regular digits for every vote k_rec_prep inverted r for)
-// instead of inside k_rec_prep's eight-vote sequence at 1.2 waves/SIMD.  Measured -0.9%
-// (profiles/r03/ab_prep_split.txt): the latency-bound prep shares its window with the prehash, so a
-// shorter prep only hands slots from the prehash to k_rec_main sooner. ----
-#ifdef HLC_PREP_SPLIT
-__global__ void __launch_bounds__(256) k_rec_scalars(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off,
-                                                     size_t off_stride, const uint32_t* sig_len, size_t len_stride,
-                                                     uint32_t* rec) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  fe r, s, rinv;
-  int parity, code;
-  if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code) || code != SCHEME_NONE)
-    return;  // flags already hold the skip / scheme code
-  load_fe_ws(rinv, rec + (size_t)REC_RINV * n + i, n);
-  rec_prep_scalars(s, rinv, parity, rec + i, n);
-}
-#endif
 
 // ---- main: decompress + u2 R, one vote per lane at a time (persistent grid) ----
 // Needs only the prep stage's records and the signatures, not the prehash: it runs beside the
@@ -136,61 +112,23 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
                                                                      const uint32_t* rec, uint32_t* q, uint8_t* mst,
                                                                      int force_exact, unsigned long long* ctr) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#if defined(HLC_PROBE_SHARE_TABLE)
-  // timing probe only (wrong results): HLC_PROBE_SHARE_TABLE lanes (a power of two) build and gather
-  // ONE shared R table and z-ratio column: 64 keeps the table traffic in L1/L2 (1.8 KB per wave), 2
-  // halves the workspace footprint (358 -> 179 MB, inside the 256 MB Infinity Cache)
-  const uint64_t tws = tid & ~(uint64_t)(HLC_PROBE_SHARE_TABLE - 1);
-#else
-  const uint64_t tws = tid;
-#endif
-  uint32_t* ws = scratch + tws;
+  uint32_t* ws = scratch + tid;
   rtab29 tab;
-  tab.g = scratch + (size_t)IL_WORDS * lanes + (size_t)tws * RTAB_WORDS;
-#if HLC_REC_LDS_ENTRIES > 0
-  static_assert(REC_TPB == RT_LDS_LS, "the LDS table is strided by the block size");
-  __shared__ uint4 s_tab[5 * RT_LDS_N * REC_TPB];
-  tab.l = s_tab + threadIdx.x;
-#else
-  tab.l = nullptr;
-#endif
-#ifdef HLC_REC_GLDS
-  // per wave: the LDS-DMA staging slots of the u2 R chain's table gathers (chain_u2r29), 10 KiB
-  __shared__ __attribute__((aligned(16))) uint32_t s_rt[REC_TPB / 64][RT_WAVE_WORDS];
-  uint32_t* lds = s_rt[threadIdx.x >> 6];
-#else
-  uint32_t* lds = nullptr;
-#endif
+  tab.g = scratch + (size_t)IL_WORDS * lanes + (size_t)tid * RTAB_WORDS;
 #ifdef HLC_CLOCK_PROBE
   // A/B probe (make variant NAME=clk DEFS=-DHLC_CLOCK_PROBE): the shader clock a wave sees under
   // the real kernel = core-clock ticks (clock64) over constant 100 MHz ticks (wall_clock64)
   const uint64_t clk0 = clock64(), wall0 = wall_clock64();
   uint32_t done = 0;
 #endif
-#ifdef HLC_STATIC_STRIDE
-  // A/B variant: the round-1 static assignment (vote tid + k * lanes)
-  for (uint64_t i = tid; i < n; i += lanes) {
-#else
   const unsigned lane = threadIdx.x & 63u;
   for (;;) {
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(ctr, 64ull);
     base = __shfl(base, 0);
     if (base >= n) break;
-#ifdef HLC_REC_PRIO
-    {
-      // A/B variant: the fewer grabs remain after this one, the higher the wave's issue priority,
-      // so waves that started late are not starved by the arbiter's oldest-first order at the end
-      const uint64_t per_round = lanes;  // votes one full round of grabs covers
-      const unsigned left = __builtin_amdgcn_readfirstlane((unsigned)min((uint64_t)3, (n - base) / per_round));
-      if (left == 0) __builtin_amdgcn_s_setprio(3);
-      else if (left == 1) __builtin_amdgcn_s_setprio(2);
-      else if (left == 2) __builtin_amdgcn_s_setprio(1);
-    }
-#endif
     const uint64_t i = base + lane;
     if (i >= n) continue;  // the next grab is past n: the wave leaves together
-#endif
 #ifdef HLC_CLOCK_PROBE
     ++done;
 #endif
@@ -202,7 +140,7 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
     fe r, qx, qy, qz;
     bool inf = false;
     fe_load_be(r, sig_at(bytes, sig_off, off_stride, i));
-    const int code = rec_u2r29(r, rec + i, n, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0, lds);
+    const int code = rec_u2r29(r, rec + i, n, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0);
     if (code != SCHEME_NONE) {
       mst[i] = (uint8_t)(1 + code);
       continue;
@@ -435,10 +373,6 @@ uint64_t recover_grid_lanes() {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_rec_main, REC_TPB, 0) != hipSuccess || per_cu < 1)
     per_cu = 2;
-#ifdef HLC_REC_GRID_WAVES
-  // A/B variant: a smaller persistent grid than the register budget admits (waves per SIMD)
-  per_cu = std::min(per_cu, HLC_REC_GRID_WAVES * 4 * 64 / REC_TPB);
-#endif
   return (uint64_t)cus * (uint64_t)per_cu * REC_TPB;
 }
 
@@ -470,10 +404,6 @@ void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
   const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
   hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, bytes, sig_off, off_stride, sig_len,
                      len_stride, b.rec, b.pfx, b.ctr);
-#ifdef HLC_PREP_SPLIT
-  hipLaunchKernelGGL(k_rec_scalars, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, bytes, sig_off, off_stride,
-                     sig_len, len_stride, b.rec);
-#endif
 }
 
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
@@ -502,14 +432,6 @@ void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_dig
                      addr_out);
 }
 
-void launch_recover(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
-                    const uint64_t* sig_off, const uint64_t* id_off, size_t off_stride, const uint32_t* sig_len,
-                    size_t len_stride, const uint32_t* gcomb, uint32_t* scratch, uint64_t scratch_lanes,
-                    uint32_t* work, uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact) {
-  launch_recover_prep(n, bytes, sig_off, off_stride, sig_len, len_stride, work, s);
-  launch_recover_main(n, bytes, sig_off, off_stride, scratch, scratch_lanes, work, s, force_exact);
-  launch_recover_finish(n, pre, z_digest, bytes, id_off, off_stride, gcomb, work, verify_out, addr_out, s, force_exact);
-}
 
 void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s) {
   const uint64_t total = (uint64_t)GC_WINDOWS * GC_ENTRIES + 1;

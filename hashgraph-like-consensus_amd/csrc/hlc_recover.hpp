@@ -232,9 +232,6 @@ HLC_DEV int comb_digit(fe& x) {
 }
 
 HLC_DEV const uint32_t* comb_entry(const uint32_t* gcomb, int w, int d) {
-#ifdef HLC_PROBE_HOT_GATHER
-  d = 1;  // timing probe only (wrong results): every gather hits one hot entry per window
-#endif
   const int idx = ((d < 0 ? -d : d) - 1) >> 1;
   return gcomb + ((size_t)w * GC_ENTRIES + (size_t)idx) * 16;
 }
@@ -336,39 +333,20 @@ HLC_DEV void rec_u1(const fe& zraw, const uint32_t* rec, size_t stride, fe& u1, 
 }
 
 // ---- main stage helpers over the 29-bit field layer ----
-// A/B variants (timing only): -DHLC_TAB_NT_STORE / -DHLC_TAB_NT_LOAD mark the R-table traffic
-// non-temporal (nt), to see whether the table's cache allocation is what costs the clock (§4.1)
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-HLC_DEV void tab_st(uint4* p, uint4 v) {
-#ifdef HLC_TAB_NT_STORE
-  const u32x4_t w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
-#else
-  *p = v;
-#endif
-}
-HLC_DEV uint4 tab_ld(const uint4* p) {
-#ifdef HLC_TAB_NT_LOAD
-  const u32x4_t w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
-  return make_uint4(w.x, w.y, w.z, w.w);
-#else
-  return *p;
-#endif
-}
-#define HLC_TAB_ST(p, v) tab_st((p), (v))
-#define HLC_TAB_LD(p) tab_ld(p)
+// R-table entries: x, y in 9 x 29-bit limbs + 2 pad words (80 B), five 16-B vector accesses.
+// (Measured and not kept, DESIGN.md §4.1: non-temporal table stores / loads -9 ... -27%; the first
+// entries in LDS -0.2 ... -11.5%; LDS-DMA staging of the gathers one window ahead -0.8%.)
 HLC_DEV void store_ge29_tab(const fe29& x, const fe29& y, uint32_t* t) {
   uint4* p = reinterpret_cast<uint4*>(t);
-  HLC_TAB_ST(p + 0, make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]));
-  HLC_TAB_ST(p + 1, make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]));
-  HLC_TAB_ST(p + 2, make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]));
-  HLC_TAB_ST(p + 3, make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]));
-  HLC_TAB_ST(p + 4, make_uint4(y.v[7], y.v[8], 0u, 0u));
+  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+  p[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+  p[2] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
+  p[3] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
+  p[4] = make_uint4(y.v[7], y.v[8], 0u, 0u);
 }
 HLC_DEV void load_ge29_tab(ge29& g, const uint32_t* t) {
   const uint4* p = reinterpret_cast<const uint4*>(t);
-  const uint4 a = HLC_TAB_LD(p + 0), b = HLC_TAB_LD(p + 1), c = HLC_TAB_LD(p + 2), d = HLC_TAB_LD(p + 3),
-              e = HLC_TAB_LD(p + 4);
+  const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
   g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
   g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
   g.x.v[8] = c.x; g.y.v[0] = c.y; g.y.v[1] = c.z; g.y.v[2] = c.w;
@@ -376,47 +354,11 @@ HLC_DEV void load_ge29_tab(ge29& g, const uint32_t* t) {
   g.y.v[7] = e.x; g.y.v[8] = e.y;
 }
 
-// The lane's R table.  HLC_REC_LDS_ENTRIES > 0 (A/B): the first RT_LDS_N entries (multiples 1, 3,
-// ...) live in LDS instead of the workspace -- piece k (16 B) of entry e at l[(5 e + k) * RT_LDS_LS],
-// lane-strided so that a wave's b128 reads are one contiguous KiB -- and only the rest is written to
-// and gathered from the workspace.  At 2 waves per SIMD (512 lanes per CU) 160 KiB of LDS holds 4
-// entries per lane.  Table building and the rewrite into the common frame index entries uniformly;
-// only the chain's gathers branch per lane (a wave issues both the LDS and the global reads, each
-// under its lanes' mask).
-#ifndef HLC_REC_LDS_ENTRIES
-#define HLC_REC_LDS_ENTRIES 0
-#endif
-constexpr int RT_LDS_N = HLC_REC_LDS_ENTRIES;
-constexpr int RT_LDS_LS = 256;  // lanes per block of the kernel that owns the LDS table
+// The lane's R table: RTAB_N entries in its workspace words.
 struct rtab29 {
   uint32_t* g;  // the lane's RTAB_WORDS workspace words
-  uint4* l;     // the lane's first LDS piece (RT_LDS_N > 0)
-  HLC_DEV const uint32_t* gentry(int e) const { return g + RTAB_ENTRY * e; }
-  HLC_DEV void store(int e, const fe29& x, const fe29& y) const {
-    if (RT_LDS_N > 0 && e < RT_LDS_N) {
-      uint4* p = l + 5 * RT_LDS_LS * e;
-      p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-      p[RT_LDS_LS] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-      p[2 * RT_LDS_LS] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
-      p[3 * RT_LDS_LS] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
-      p[4 * RT_LDS_LS] = make_uint4(y.v[7], y.v[8], 0u, 0u);
-    } else {
-      store_ge29_tab(x, y, g + RTAB_ENTRY * e);
-    }
-  }
-  HLC_DEV void load(ge29& q, int e) const {
-    if (RT_LDS_N > 0 && e < RT_LDS_N) {
-      const uint4* p = l + 5 * RT_LDS_LS * e;
-      const uint4 a = p[0], b = p[RT_LDS_LS], c = p[2 * RT_LDS_LS], d = p[3 * RT_LDS_LS], f = p[4 * RT_LDS_LS];
-      q.x.v[0] = a.x; q.x.v[1] = a.y; q.x.v[2] = a.z; q.x.v[3] = a.w;
-      q.x.v[4] = b.x; q.x.v[5] = b.y; q.x.v[6] = b.z; q.x.v[7] = b.w;
-      q.x.v[8] = c.x; q.y.v[0] = c.y; q.y.v[1] = c.z; q.y.v[2] = c.w;
-      q.y.v[3] = d.x; q.y.v[4] = d.y; q.y.v[5] = d.z; q.y.v[6] = d.w;
-      q.y.v[7] = f.x; q.y.v[8] = f.y;
-    } else {
-      load_ge29_tab(q, g + RTAB_ENTRY * e);
-    }
-  }
+  HLC_DEV void store(int e, const fe29& x, const fe29& y) const { store_ge29_tab(x, y, g + RTAB_ENTRY * e); }
+  HLC_DEV void load(ge29& q, int e) const { load_ge29_tab(q, g + RTAB_ENTRY * e); }
 };
 
 HLC_DEV void store_fe29_ws(const fe29& x, uint32_t* ws, size_t stride) {
@@ -459,36 +401,10 @@ HLC_DEV void comb_mul_g29(gej29& acc, fe k, bool neg, const uint32_t* gcomb) {
   }
 }
 
-// A/B variant -DHLC_REC_GLDS (not the default): LDS staging of the R-table gathers.  A window's two
-// entries (b1, b2) arrive by LDS-DMA -- global_load_lds_dwordx4, 5 pieces of 16 B per lane, 1 KiB
-// per wave-instruction, no VGPR destination -- issued right after the previous window's additions,
-// so the gathers' latency hides behind 5 doublings with no registers held in flight.  Measured
-// 0.8% slower over three alternating rounds (profiles/r03/ab_glds_share_probes.txt): the other
-// waves already hide the gathers' latency; what the table costs is traffic.
-// RT_SLOT words per entry slot: piece k of lane l at word 256 k + 4 l.
-constexpr int RT_SLOT = 5 * 256;
-constexpr int RT_WAVE_WORDS = 2 * RT_SLOT;  // b1 and b2 slots: 10 KiB per wave
-HLC_DEV void glds_entry(const uint32_t* ent, uint32_t* slot) {
-#pragma unroll
-  for (int k = 0; k < 5; ++k) __builtin_amdgcn_global_load_lds((const void*)(ent + 4 * k), (void*)(slot + 256 * k), 16, 0, 0);
-}
-HLC_DEV void lds_entry(ge29& g, const uint32_t* slot, unsigned lane) {
-  const uint4* p = reinterpret_cast<const uint4*>(slot) + lane;
-  const uint4 a = p[0], b = p[64], c = p[128], d = p[192], e = p[256];
-  g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
-  g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
-  g.x.v[8] = c.x; g.y.v[0] = c.y; g.y.v[1] = c.z; g.y.v[2] = c.w;
-  g.y.v[3] = d.x; g.y.v[4] = d.y; g.y.v[5] = d.z; g.y.v[6] = d.w;
-  g.y.v[7] = e.x; g.y.v[8] = e.y;
-}
-HLC_DEV void wait_glds() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 // u2 R over the lane's R table (odd multiples 1..31 of R in one common-Z frame, zg = that Z):
 // regular signed digits of the GLV halves b1, b2 (b2 against lambda R = (beta x, y)).
-// lds: this wave's RT_WAVE_WORDS staging words (HLC_REC_GLDS only).
 template <bool EXACT>
-HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const rtab29& tab, const fe29& zg,
-                         uint32_t* lds) {
+HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const rtab29& tab, const fe29& zg) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int negs = (int)(flags & 3u), skews = (int)((flags >> 2) & 3u);
   fe29 beta;
@@ -499,50 +415,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const r
   // at the same positions (uniform across the wave).
   auto word_at = [&](int win, int k) { return dws[((size_t)(k * DIG_R_WORDS) + (size_t)(win >> 1)) * stride]; };
   auto digit_at = [&](int win, int k) { return digit16(word_at(win, k), win & 1); };
-#ifdef HLC_PROBE_HOT_GATHER
-  auto index_of = [&](int d) { return 0; };  // timing probe only (wrong results): no table traffic
-#else
   auto index_of = [&](int d) { return ((d < 0 ? -d : d) - 1) >> 1; };
-#endif
-  auto entry_of = [&](int d) { return tab.gentry(index_of(d)); };
-#ifdef HLC_REC_GLDS
-  static_assert(RT_LDS_N == 0, "the LDS-DMA staging variant gathers every entry from the workspace");
-  const unsigned lane = threadIdx.x & 63u;
-  uint32_t* s1 = lds;
-  uint32_t* s2 = lds + RT_SLOT;
-  int win = M_R - 1;
-  int d1 = digit_at(win, 0), d2 = digit_at(win, 1);
-  glds_entry(entry_of(d1), s1);
-  glds_entry(entry_of(d2), s2);
-#pragma unroll 1
-  for (;;) {
-    // the next window's digit words: ordinary loads, first used after this window's additions
-    uint32_t n1 = 0, n2 = 0;
-    if (win > 0) {
-      n1 = word_at(win - 1, 0);
-      n2 = word_at(win - 1, 1);
-    }
-    if (win != M_R - 1) {
-#pragma unroll 1
-      for (int q = 0; q < W_R; ++q) gej29_double(acc, acc);
-    }
-    wait_glds();
-    ge29 g;
-    lds_entry(g, s1, lane);
-    fe29_cneg_lazy(g.y, g.y, (d1 < 0) != ((negs & 1) != 0));
-    gej29_madd<EXACT>(acc, acc, g);
-    lds_entry(g, s2, lane);
-    fe29_mul_uniform(g.x, g.x, beta);
-    fe29_cneg_lazy(g.y, g.y, (d2 < 0) != ((negs & 2) != 0));
-    gej29_madd<EXACT>(acc, acc, g);
-    if (win == 0) break;
-    --win;
-    d1 = digit16(n1, win & 1);
-    d2 = digit16(n2, win & 1);
-    glds_entry(entry_of(d1), s1);  // the slots were read above (the additions used them)
-    glds_entry(entry_of(d2), s2);
-  }
-#else
 #pragma unroll 1
   for (int win = M_R - 1; win >= 0; --win) {
     ge29 g;
@@ -567,7 +440,6 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const r
     fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 2) != 0));
     gej29_madd<EXACT>(acc, acc, g);
   }
-#endif
 #pragma unroll 1
   for (int k = 0; k < 2; ++k) {
     if (((skews >> k) & 1) == 0) continue;
@@ -587,7 +459,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const r
 // when its own Z comes out zero (the unchecked chain is exact whenever its Z is non-zero, so this
 // is the combined stage's test split per chain).
 HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx, fe& qy, fe& qz, bool& inf,
-                      uint32_t* ws, size_t ws_stride, const rtab29& tab, bool force_exact, uint32_t* lds) {
+                      uint32_t* ws, size_t ws_stride, const rtab29& tab, bool force_exact) {
   const uint32_t flags = rec[(size_t)REC_FLAGS * stride];
   const int parity = (int)((flags >> 5) & 1u);
   ge29 R;
@@ -640,8 +512,8 @@ HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx,
     fe29_mul(zg, sc, d.z);
   }
   gej29 acc;
-  chain_u2r29<false>(acc, rec, stride, tab, zg, lds);
-  if (force_exact || (!acc.inf && fe29_is_zero_modp(acc.z))) chain_u2r29<true>(acc, rec, stride, tab, zg, lds);
+  chain_u2r29<false>(acc, rec, stride, tab, zg);
+  if (force_exact || (!acc.inf && fe29_is_zero_modp(acc.z))) chain_u2r29<true>(acc, rec, stride, tab, zg);
   inf = acc.inf;
   fe29_to32(qx.v, acc.x);
   fe29_to32(qy.v, acc.y);

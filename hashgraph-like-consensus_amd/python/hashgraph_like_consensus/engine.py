@@ -103,6 +103,25 @@ class Engine:
             _ffi.ptr(st, c_uint8), _ffi.ptr(addr, c_uint8)))
         return st[:n], addr[:n]
 
+    def eth_verify_arrays(self, arena: np.ndarray, id_off: np.ndarray, id_len: np.ndarray, pay_off: np.ndarray,
+                          pay_len: np.ndarray, sig_off: np.ndarray, sig_len: np.ndarray, want_addr: bool = True,
+                          out: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+        """hlc_eth_verify_batch over pre-packed arrays (one byte arena, per-item u64 offsets and u32
+        lengths, contiguous): no per-item Python work.  -> (status[n], recovered[n,20] or None); `out`
+        reuses caller-owned output arrays."""
+        n = int(id_off.shape[0])
+        if out is None:
+            st = np.zeros(max(n, 1), np.uint8)
+            addr = np.zeros((max(n, 1), 20), np.uint8) if want_addr else None
+        else:
+            st, addr = out
+        _ffi.check(self.lib.hlc_eth_verify_batch(
+            self.ctx, n, _ffi.ptr(arena, c_uint8), int(arena.size), _ffi.ptr(id_off, c_uint64),
+            _ffi.ptr(id_len, c_uint32), _ffi.ptr(pay_off, c_uint64), _ffi.ptr(pay_len, c_uint32),
+            _ffi.ptr(sig_off, c_uint64), _ffi.ptr(sig_len, c_uint32), _ffi.ptr(st, c_uint8),
+            _ffi.ptr(addr, c_uint8) if want_addr else None))
+        return st[:n], (addr[:n] if addr is not None else None)
+
     def consensus_timeout_batch(self, sessions: np.ndarray):
         """hlc_consensus_timeout_batch over a SESSION_TALLY_DTYPE array -> (new state u8[n],
         status u8[n]) -- handle_consensus_timeout (service.rs:323-373) per session."""

@@ -13,7 +13,7 @@
 #   pipetrace  rocprofv3 kernel + memory-copy trace of one host-buffer setting ($PIPE_ARGS)
 #   verify     tools/verify_latency.py (hlc_eth_verify_batch at the C ABI)
 #   profile    tools/profile.sh TAG (kernel trace + PMC passes of the headline leg)
-#   ab         tools/ab.sh $AB_VARIANTS (alternating A/B of lib/variants builds)
+#   ab         tools/ab_arms.sh $AB_ARMS (alternating A/B arms: lib/variants builds or env settings)
 #   clock      tools/clock_probe.py $CLOCK_ARGS (in-kernel shader clock of k_rec_main)
 set -o pipefail
 TAG=$1
@@ -66,7 +66,7 @@ for step in "$@"; do
   profile)
     bash tools/profile.sh $TAG || exit 1 ;;
   ab)
-    bash tools/ab.sh $AB_VARIANTS || exit 1 ;;
+    bash tools/ab_arms.sh $AB_ARMS || exit 1 ;;
   clock)
     timeout -k 10 300 python tools/clock_probe.py $CLOCK_ARGS > $O/clock_$TAG.txt 2> $O/clock_$TAG.err || fail clock $O/clock_$TAG.err
     tail -20 $O/clock_$TAG.txt ;;
