@@ -165,10 +165,12 @@ struct hlc_ctx {
   // records) so that two k_rec_main grids over the two vote ranges of a call overlap; an upload stream;
   // the page-locked staging of the inputs and outputs and their device copies (allocated on first use)
   hipStream_t aux2 = nullptr, copy = nullptr;
-  DBuf rec_scratch2, rec_work2;
+  DBuf rec_scratch2;
+  std::vector<std::unique_ptr<DBuf>> rec_works;  // per-vote records of each recovery range but the first
   PBuf pin_in, pin_out;
   DBuf dev_in, dev_out;
-  hipEvent_t ev_sig[2] = {nullptr, nullptr}, ev_main[2] = {nullptr, nullptr}, ev_rest = nullptr, ev_done = nullptr;
+  std::vector<hipEvent_t> ev_sig, ev_main;  // per recovery range: signatures landed, main stage done
+  hipEvent_t ev_rest = nullptr, ev_done = nullptr;
   std::unique_ptr<HostPool> pool;  // staging workers (HLC_HOST_THREADS)
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
@@ -195,7 +197,9 @@ struct hlc_ctx {
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : rec_prep_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    for (hipEvent_t e : {ev_sig[0], ev_sig[1], ev_main[0], ev_main[1], ev_rest, ev_done})
+    for (hipEvent_t e : ev_sig) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_main) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_rest, ev_done})
       if (e) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
@@ -320,7 +324,8 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   CHK(c->verify.ensure(n));
   CHK(c->kec_dig.ensure(n * 32));
   CHK(ensure_recover_scratch(c));
-  CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
+  // (fronts: range 0's records are in flight in rec_work, sized by the caller)
+  if (!fronts) CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   // The recovery's prep stage (signature parse, batched r^-1, GLV digits) and main stage (R, its
   // table, the u2 R chain: ~93% of the recovery) need only the signatures, so they run on the
   // context's aux stream while the prehash kernels (and the small-proposal chain kernel) run on
@@ -691,12 +696,28 @@ int host_threads() {
   return std::max(1, std::min(t, 64));
 }
 
-// Votes in the first of the two recovery ranges of hlc_validate_proposals (HLC_SPLIT_FIRST_VOTES,
-// default 131072; 0 = one range): the first k_rec_main grid starts once these votes' signatures have
-// landed, the second once the rest have, and fills the first one's tail.
-uint64_t split_first_votes() {
-  const char* e = std::getenv("HLC_SPLIT_FIRST_VOTES");
-  return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)131072;
+// The recovery ranges of a host-buffer call of n items (HLC_SPLIT_VOTES="a,b,...", default
+// "131072,196608"; "0" = one range): a range of each listed size while at least twice that many
+// items remain, then one range for the rest.  Range k's k_rec_main grid starts once its signatures
+// have landed; ranges alternate between two streams (and two per-lane scratch buffers), so each
+// range's waves take the SIMD slots the previous range's waves free.
+std::vector<uint64_t> split_ranges(uint64_t n) {
+  std::vector<uint64_t> sizes, b{0};
+  const char* e = std::getenv("HLC_SPLIT_VOTES");
+  const char* p = e ? e : "131072,196608";
+  while (*p) {
+    char* end = nullptr;
+    const uint64_t x = std::strtoull(p, &end, 10);
+    if (end == p) break;
+    sizes.push_back(x);
+    p = *end == ',' ? end + 1 : end;
+  }
+  for (uint64_t x : sizes) {
+    if (!x || b.size() > 7 || n - b.back() < 2 * x) break;
+    b.push_back(b.back() + x);
+  }
+  if (n > b.back() || b.size() == 1) b.push_back(n);
+  return b;  // range k = [b[k], b[k+1])
 }
 
 // Pieces the inputs other than the signatures are staged and uploaded in (HLC_REST_PIECES, default 3):
@@ -719,7 +740,7 @@ int host_resources(hlc_ctx* c) {
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   if (!c->copy) HIPCHK(hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, greatest));
   if (!c->aux2) HIPCHK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, least));
-  for (hipEvent_t* e : {&c->ev_sig[0], &c->ev_sig[1], &c->ev_main[0], &c->ev_main[1], &c->ev_rest, &c->ev_done})
+  for (hipEvent_t* e : {&c->ev_rest, &c->ev_done})
     if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   if (!c->pool || c->pool->parts() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
   CHK(ensure_recover_scratch(c));
@@ -785,25 +806,35 @@ struct Staging {
   }
 };
 
-// The recovery's front half of a host-buffer call: the signatures of items [0, na) and [na, n)
-// (sig_off / sig_len with stride `stride`) gathered by the host pool into the dense array at o_sig
-// (65 B per item; zero-filled slots for other lengths) and their lengths at o_len, each range
-// uploaded and its k_rec_prep + k_rec_main enqueued on its own stream (recovery slots 1 and 2) as
-// soon as its DMA is enqueued.  HLC_EINVAL, before its bytes are read, for a 65-byte signature
-// outside the arena.
-int launch_fronts(hlc_ctx* c, Staging& st, HostTrace& tr, uint64_t n, uint64_t na, const uint8_t* bytes,
-                  uint64_t bytes_len, const uint64_t* sig_off, const uint32_t* sig_len, size_t stride, size_t o_sig,
-                  size_t o_len, RecFront fronts[2], int* nf) {
+// The recovery's front half of a host-buffer call: the signatures of the items of each range of
+// split_ranges(n) (sig_off / sig_len with stride `stride`) gathered by the host pool into the dense
+// array at o_sig (65 B per item; slots of other lengths left as they are) and their lengths at
+// o_len, each range uploaded and its k_rec_prep + k_rec_main enqueued (on the aux streams in turn)
+// as soon as its DMA is enqueued.  Sizes each range's records.  HLC_EINVAL, before its bytes are
+// read, for a 65-byte signature outside the arena.
+int launch_fronts(hlc_ctx* c, Staging& st, HostTrace& tr, uint64_t n, const uint8_t* bytes, uint64_t bytes_len,
+                  const uint64_t* sig_off, const uint32_t* sig_len, size_t stride, size_t o_sig, size_t o_len,
+                  std::vector<RecFront>& fronts) {
   HostPool& pool = *c->pool;
   const int parts = pool.parts();
-  uint32_t* work[2] = {c->rec_work.as<uint32_t>(), c->rec_work2.as<uint32_t>()};
+  const std::vector<uint64_t> rb = split_ranges(n);
+  const size_t R = rb.size() - 1;
+  while (c->rec_works.size() + 1 < R) c->rec_works.emplace_back(new DBuf());
+  while (c->ev_sig.size() < R) {
+    hipEvent_t a = nullptr, b = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    c->ev_sig.push_back(a);
+    HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    c->ev_main.push_back(b);
+  }
   uint32_t* scratch[2] = {c->rec_scratch.as<uint32_t>(), c->rec_scratch2.as<uint32_t>()};
   hipStream_t aux[2] = {c->aux, c->aux2};
-  const uint64_t rv0[2] = {0, na}, rv1[2] = {na, n};
-  *nf = 0;
-  for (int k = 0; k < 2; ++k) {
-    const uint64_t a0 = rv0[k], m = rv1[k] - rv0[k];
+  fronts.clear();
+  for (size_t k = 0; k < R; ++k) {
+    const uint64_t a0 = rb[k], m = rb[k + 1] - rb[k];
     if (!m) continue;
+    DBuf& wb = k == 0 ? c->rec_work : *c->rec_works[k - 1];
+    CHK(wb.ensure(hlc::recover_work_words(m) * sizeof(uint32_t)));
     std::vector<int> bad(parts, 0);
     pool.run([&](int t, int T) {
       const uint64_t b0 = a0 + m * t / T, b1 = a0 + m * (t + 1) / T;
@@ -827,20 +858,21 @@ int launch_fronts(hlc_ctx* c, Staging& st, HostTrace& tr, uint64_t n, uint64_t n
         return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
       }
     }
-    tr.mark(k ? "sigs_b_staged" : "sigs_a_staged");
+    tr.mark("sigs_staged");
     CHK(st.up(o_sig + 65 * a0, 65 * m));
     CHK(st.up(o_len + 4 * a0, 4 * m));
     HIPCHK(hipEventRecord(c->ev_sig[k], c->copy));
-    tr.ev(k ? "sigs_b_landed" : "sigs_a_landed", c->copy);
-    HIPCHK(hipStreamWaitEvent(aux[k], c->ev_sig[k], 0));
+    tr.ev("sigs_landed", c->copy);
+    hipStream_t a = aux[k % 2];
+    HIPCHK(hipStreamWaitEvent(a, c->ev_sig[k], 0));
     const uint8_t* sb = st.D + o_sig + 65 * a0;
     const uint32_t* sl = reinterpret_cast<const uint32_t*>(st.D + o_len) + a0;
-    hlc::launch_recover_prep(m, sb, nullptr, 0, sl, 1, work[k], aux[k]);
-    hlc::launch_recover_main(m, sb, nullptr, 0, scratch[k], c->rec_lanes, work[k], aux[k], c->rec_force_exact);
+    hlc::launch_recover_prep(m, sb, nullptr, 0, sl, 1, wb.as<uint32_t>(), a);
+    hlc::launch_recover_main(m, sb, nullptr, 0, scratch[k % 2], c->rec_lanes, wb.as<uint32_t>(), a, c->rec_force_exact);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev_main[k], aux[k]));
-    tr.ev(k ? "main_b_end" : "main_a_end", aux[k]);
-    fronts[(*nf)++] = RecFront{a0, a0 + m, work[k], c->ev_main[k]};
+    HIPCHK(hipEventRecord(c->ev_main[k], a));
+    tr.ev("main_end", a);
+    fronts.push_back(RecFront{a0, a0 + m, wb.as<uint32_t>(), c->ev_main[k]});
   }
   return 0;
 }
@@ -873,9 +905,6 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   HostTrace tr;
   if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
   tr.start(c->copy);
-  const uint64_t first = split_first_votes();
-  const uint64_t na = first && n >= 2 * first ? first : n;  // one range when the batch is small
-  const uint64_t nb = n - na;
   // inputs, page-locked and on the device alike: dense signatures | signature lengths | vote_id |
   // proposal_id | timestamp | vote | field_off | field_len | proposals | arena
   size_t o[11];
@@ -901,17 +930,15 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   CHK(c->dev_in.ensure(o[10] + 16));
   CHK(c->pin_out.ensure(r[4] + 16));
   CHK(c->dev_out.ensure(r[4] + 16));
-  CHK(reserve_validate(c, n, np));  // slot 1's records are sized for n >= na
-  if (nb) CHK(c->rec_work2.ensure(hlc::recover_work_words(nb) * sizeof(uint32_t)));
+  CHK(reserve_validate(c, n, np));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
   uint8_t* P = st.P;
   uint8_t* D = st.D;
   auto up = [&](size_t off, size_t len) { return st.up(off, len); };
   const int parts = pool.parts();
-  RecFront fronts[2];
-  int nf = 0;
-  CHK(launch_fronts(c, st, tr, n, na, v->bytes, v->bytes_len, v->field_off + HLC_F_SIGNATURE,
-                    v->field_len + HLC_F_SIGNATURE, HLC_NFIELDS, o[0], o[1], fronts, &nf));
+  std::vector<RecFront> fronts;
+  CHK(launch_fronts(c, st, tr, n, v->bytes, v->bytes_len, v->field_off + HLC_F_SIGNATURE,
+                    v->field_len + HLC_F_SIGNATURE, HLC_NFIELDS, o[0], o[1], fronts));
   // everything else, piece by piece, field checks on the way
   const int K = rest_pieces();
   std::vector<int> bad(parts, 0);
@@ -966,7 +993,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   uint8_t* ob = c->dev_out.as<uint8_t>();
   CHK(validate_device(c, &dv, reinterpret_cast<const hlc_proposal*>(D + o[8]), np, now,
                       reinterpret_cast<hlc_result*>(ob + r[0]), ob + r[1], ob + r[2], out_rec ? ob + r[3] : nullptr, s,
-                      fronts, nf));
+                      fronts.data(), (int)fronts.size()));
   tr.ev("kernels_end", s);
   HIPCHK(hipMemcpyAsync(c->pin_out.p, ob, r[4], hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->ev_done, s));
@@ -1009,8 +1036,6 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   HostTrace tr;
   if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
   tr.start(c->copy);
-  const uint64_t first = split_first_votes();
-  const uint64_t na = first && n >= 2 * first ? first : n;
   // inputs: dense signatures | signature lengths | identity lengths | payload lengths | identity
   // offsets | payload offsets | arena
   size_t o[8];
@@ -1029,12 +1054,9 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   CHK(c->dev_out.ensure(r2 + 16));
   CHK(c->pre.ensure(n + 1));
   CHK(c->kec_dig.ensure(n * 32 + 32));
-  CHK(c->rec_work.ensure(hlc::recover_work_words(na) * sizeof(uint32_t)));
-  if (n > na) CHK(c->rec_work2.ensure(hlc::recover_work_words(n - na) * sizeof(uint32_t)));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
-  RecFront fronts[2];
-  int nf = 0;
-  CHK(launch_fronts(c, st, tr, n, na, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], fronts, &nf));
+  std::vector<RecFront> fronts;
+  CHK(launch_fronts(c, st, tr, n, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], fronts));
   const int K = rest_pieces(), parts = pool.parts();
   std::vector<int> bad(parts, 0);
   for (int k = 0; k < K; ++k) {
@@ -1079,8 +1101,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
                              reinterpret_cast<const uint32_t*>(D + o[2]), c->kec_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), dstat, s);
   if (daddr) HIPCHK(hipMemsetAsync(daddr, 0, n * 20, s));
-  for (int k = 0; k < nf; ++k) {
-    const RecFront& f = fronts[k];
+  for (const RecFront& f : fronts) {
     HIPCHK(hipStreamWaitEvent(s, f.done, 0));
     hlc::launch_recover_finish(f.v1 - f.v0, c->pre.as<uint8_t>() + f.v0, c->kec_dig.as<uint32_t>() + 8 * f.v0, dbytes,
                                did_off + f.v0, 1, c->gtab.as<uint32_t>(), f.work, dstat + f.v0,

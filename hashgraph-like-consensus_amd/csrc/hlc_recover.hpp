@@ -57,9 +57,9 @@ constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
 // Per-lane workspace of the main stage (persistent grid):
 //  * lane-interleaved (word w of lane t at w * lanes + t: every lane touches the same word, so
 //    each access is one coalesced 256-B row per wave): the z-ratios of the table build;
-//  * per-lane contiguous R table (RTAB_WORDS words, 64-B entries read by 16-B vector loads):
+//  * per-lane contiguous R table (RTAB_WORDS words, 64-B entries read by four 16-B vector loads):
 //    entries are gathered at lane-dependent indices, so each lane's entry must be one block.
-constexpr int RTAB_ENTRY = 20;                  // words per entry: x, y in 9 x 29-bit limbs + 2 pad (80 B)
+constexpr int RTAB_ENTRY = 16;                  // words per entry: x, y below 2^256 in 8 x 32 bits (64 B)
 constexpr int RTAB_WORDS = RTAB_N * RTAB_ENTRY; // per lane (affine, common-Z frame)
 constexpr int ZR_OFF = 0;                       // z-ratios of the table build (9 limbs each)
 constexpr int IL_WORDS = ZR_OFF + 9 * (RTAB_N - 1);       // interleaved words per lane
@@ -333,32 +333,85 @@ HLC_DEV void rec_u1(const fe& zraw, const uint32_t* rec, size_t stride, fe& u1, 
 }
 
 // ---- main stage helpers over the 29-bit field layer ----
-// R-table entries: x, y in 9 x 29-bit limbs + 2 pad words (80 B), five 16-B vector accesses.
-// (Measured and not kept, DESIGN.md §4.1: non-temporal table stores / loads -9 ... -27%; the first
-// entries in LDS -0.2 ... -11.5%; LDS-DMA staging of the gathers one window ahead -0.8%.)
-HLC_DEV void store_ge29_tab(const fe29& x, const fe29& y, uint32_t* t) {
-  uint4* p = reinterpret_cast<uint4*>(t);
-  p[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
-  p[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
-  p[2] = make_uint4(x.v[8], y.v[0], y.v[1], y.v[2]);
-  p[3] = make_uint4(y.v[3], y.v[4], y.v[5], y.v[6]);
-  p[4] = make_uint4(y.v[7], y.v[8], 0u, 0u);
+// R-table entries of 64 B: one aligned half line per gather.  (Round 3 stored the lazy limbs, 80 B
+// per entry straddling 128-B lines for half of the entries; the 64-B form measured +6.1% on the
+// step, profiles/r04/ab_table64.txt.  Also measured and not kept, DESIGN.md §4.1: non-temporal table
+// stores / loads -9 ... -27%; the first entries in LDS -0.2 ... -11.5%; LDS-DMA staging of the
+// gathers one window ahead -0.8%.)  A stored
+// coordinate (a normalised product: limbs < 2^29, limb 2 < 2^29 + 2^19, value < 2^261) is brought
+// below 2^256 -- its bits at and above 2^256 fold as t (2^32 + 977), one serial carry, a second
+// fold only when that carry reaches bit 256 again (the value was within 2^38 of 2^256) -- and packed
+// into 8 words; a gather unpacks with one v_alignbit + one v_and per limb.
+HLC_DEV void fe29_pack256(uint32_t w[8], const fe29& a) {
+  uint32_t d[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) d[i] = a.v[i];
+  const uint32_t t = d[8] >> 24;
+  d[8] &= 0x00FFFFFFu;
+  d[0] += t * 977u;
+  d[1] += t * 8u;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint32_t x = d[i] + c;
+    c = x >> 29;
+    d[i] = x & M29;
+  }
+  if (d[8] >> 24) {  // bit 256 set again: fold once more (then the value is far below 2^256)
+    d[8] &= 0x00FFFFFFu;
+    d[0] += 977u;
+    d[1] += 8u;
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const uint32_t x = d[i] + c;
+      c = x >> 29;
+      d[i] = x & M29;
+    }
+  }
+  w[0] = d[0] | (d[1] << 29);
+  w[1] = (d[1] >> 3) | (d[2] << 26);
+  w[2] = (d[2] >> 6) | (d[3] << 23);
+  w[3] = (d[3] >> 9) | (d[4] << 20);
+  w[4] = (d[4] >> 12) | (d[5] << 17);
+  w[5] = (d[5] >> 15) | (d[6] << 14);
+  w[6] = (d[6] >> 18) | (d[7] << 11);
+  w[7] = (d[7] >> 21) | (d[8] << 8);
 }
-HLC_DEV void load_ge29_tab(ge29& g, const uint32_t* t) {
+HLC_DEV void fe29_unpack256(fe29& r, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, uint32_t w5,
+                            uint32_t w6, uint32_t w7) {
+  r.v[0] = w0 & M29;
+  r.v[1] = __builtin_amdgcn_alignbit(w1, w0, 29) & M29;
+  r.v[2] = __builtin_amdgcn_alignbit(w2, w1, 26) & M29;
+  r.v[3] = __builtin_amdgcn_alignbit(w3, w2, 23) & M29;
+  r.v[4] = __builtin_amdgcn_alignbit(w4, w3, 20) & M29;
+  r.v[5] = __builtin_amdgcn_alignbit(w5, w4, 17) & M29;
+  r.v[6] = __builtin_amdgcn_alignbit(w6, w5, 14) & M29;
+  r.v[7] = __builtin_amdgcn_alignbit(w7, w6, 11) & M29;
+  r.v[8] = w7 >> 8;
+}
+HLC_DEV void store_ge29_tab64(const fe29& x, const fe29& y, uint32_t* t) {
+  uint32_t a[8], b[8];
+  fe29_pack256(a, x);
+  fe29_pack256(b, y);
+  uint4* p = reinterpret_cast<uint4*>(t);
+  p[0] = make_uint4(a[0], a[1], a[2], a[3]);
+  p[1] = make_uint4(a[4], a[5], a[6], a[7]);
+  p[2] = make_uint4(b[0], b[1], b[2], b[3]);
+  p[3] = make_uint4(b[4], b[5], b[6], b[7]);
+}
+HLC_DEV void load_ge29_tab64(ge29& g, const uint32_t* t) {
   const uint4* p = reinterpret_cast<const uint4*>(t);
-  const uint4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
-  g.x.v[0] = a.x; g.x.v[1] = a.y; g.x.v[2] = a.z; g.x.v[3] = a.w;
-  g.x.v[4] = b.x; g.x.v[5] = b.y; g.x.v[6] = b.z; g.x.v[7] = b.w;
-  g.x.v[8] = c.x; g.y.v[0] = c.y; g.y.v[1] = c.z; g.y.v[2] = c.w;
-  g.y.v[3] = d.x; g.y.v[4] = d.y; g.y.v[5] = d.z; g.y.v[6] = d.w;
-  g.y.v[7] = e.x; g.y.v[8] = e.y;
+  const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+  fe29_unpack256(g.x, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w);
+  fe29_unpack256(g.y, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w);
 }
 
 // The lane's R table: RTAB_N entries in its workspace words.
 struct rtab29 {
   uint32_t* g;  // the lane's RTAB_WORDS workspace words
-  HLC_DEV void store(int e, const fe29& x, const fe29& y) const { store_ge29_tab(x, y, g + RTAB_ENTRY * e); }
-  HLC_DEV void load(ge29& q, int e) const { load_ge29_tab(q, g + RTAB_ENTRY * e); }
+  HLC_DEV void store(int e, const fe29& x, const fe29& y) const { store_ge29_tab64(x, y, g + RTAB_ENTRY * e); }
+  HLC_DEV void load(ge29& q, int e) const { load_ge29_tab64(q, g + RTAB_ENTRY * e); }
 };
 
 HLC_DEV void store_fe29_ws(const fe29& x, uint32_t* ws, size_t stride) {

@@ -5,8 +5,8 @@ per-proposal results, per-vote statuses, scheme reasons and recovered addresses,
 batch; also with empty proposals, votes no proposal covers (status 0xFF), proposals listed out of
 vote order, and an out-of-arena field -- a signature in the second range or another field in a late
 piece -- which returns HLC_EINVAL with the caller's outputs untouched (the device work already
-enqueued is drained and discarded).  Schedule knobs: HLC_SPLIT_FIRST_VOTES (votes in the first
-range, 0 = one range), HLC_REST_PIECES."""
+enqueued is drained and discarded).  Schedule knobs: HLC_SPLIT_VOTES (sizes of the recovery ranges
+before the last, "0" = one range), HLC_REST_PIECES."""
 import ctypes
 import os
 
@@ -24,12 +24,12 @@ HLC_EINVAL = -1  # include/hlc.h
 
 
 def _run(engine, batch, desc, now, split, pieces=3):
-    os.environ["HLC_SPLIT_FIRST_VOTES"] = str(split)
+    os.environ["HLC_SPLIT_VOTES"] = str(split)
     os.environ["HLC_REST_PIECES"] = str(pieces)
     try:
         return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
     finally:
-        os.environ.pop("HLC_SPLIT_FIRST_VOTES", None)
+        os.environ.pop("HLC_SPLIT_VOTES", None)
         os.environ.pop("HLC_REST_PIECES", None)
 
 
@@ -40,7 +40,8 @@ def byz():
     return b, d, w.now
 
 
-@pytest.mark.parametrize("split,pieces", [(100, 3), (240, 1), (333, 7), (100, 64), (1, 2), (0, 5)])
+@pytest.mark.parametrize("split,pieces", [("100", 3), ("240", 1), ("333", 7), ("100", 64), ("1", 2), ("0", 5),
+                                          ("64,128", 3), ("100,150,90", 2)])
 def test_gpu_host_entry_equals_single_range_and_oracle(engine, byz, split, pieces):
     b, d, now = byz
     one = _run(engine, b, d, now, 0, 1)
@@ -89,13 +90,13 @@ def _raw_call(engine, batch, desc, now, split):
     rec = np.full((n, 20), 0xAB, np.uint8)
     view = batch.view()
     desc = np.ascontiguousarray(desc)
-    os.environ["HLC_SPLIT_FIRST_VOTES"] = str(split)
+    os.environ["HLC_SPLIT_VOTES"] = str(split)
     try:
         rc = engine.lib.hlc_validate_proposals(engine.ctx, ctypes.byref(view), proposals_ptr(desc), desc.shape[0], now,
                                                results_ptr(res), _ffi.ptr(st, ctypes.c_uint8),
                                                _ffi.ptr(rs, ctypes.c_uint8), _ffi.ptr(rec, ctypes.c_uint8))
     finally:
-        os.environ.pop("HLC_SPLIT_FIRST_VOTES", None)
+        os.environ.pop("HLC_SPLIT_VOTES", None)
     return rc, (res.view(np.uint8), st, rs, rec)
 
 

@@ -142,20 +142,20 @@ def test_gpu_verify_batch_sizes(engine):
         assert [a.tobytes() for a in addr] == exp_addr[:n], n
 
 
-@pytest.mark.parametrize("split,pieces", [(0, 1), (100, 3), (700, 5), (1, 64)])
+@pytest.mark.parametrize("split,pieces", [("0", 1), ("100", 3), ("700", 5), ("1", 64), ("200,300", 2)])
 def test_gpu_verify_batch_split_schedules(engine, split, pieces):
     """hlc_eth_verify_batch stages the signatures first and recovers them in two ranges on two
-    streams (HLC_SPLIT_FIRST_VOTES items in the first), the identities / payloads / arena in
+    streams in turn (HLC_SPLIT_VOTES: the sizes of the ranges before the last), the identities / payloads / arena in
     HLC_REST_PIECES pieces: every schedule equals the oracle item for item (payloads of 0..299 bytes:
     1-3 digit EIP-191 lengths, 1-3 keccak blocks)."""
     ids, pays, sigs = _mutated_items(1500, 11)
     exp_st, exp_addr = _oracle_verify(ids, pays, sigs)
-    os.environ["HLC_SPLIT_FIRST_VOTES"] = str(split)
+    os.environ["HLC_SPLIT_VOTES"] = str(split)
     os.environ["HLC_REST_PIECES"] = str(pieces)
     try:
         st, addr = engine.eth_verify_batch(ids, pays, sigs)
     finally:
-        os.environ.pop("HLC_SPLIT_FIRST_VOTES", None)
+        os.environ.pop("HLC_SPLIT_VOTES", None)
         os.environ.pop("HLC_REST_PIECES", None)
     assert [int(x) for x in st] == exp_st
     assert [a.tobytes() for a in addr] == exp_addr
@@ -174,13 +174,13 @@ def test_gpu_verify_batch_rejects_out_of_arena_outputs_untouched(engine):
         o[which * n + n - 1] = arena.size + 1
         st = np.full(n, 0xAB, np.uint8)
         addr = np.full((n, 20), 0xAB, np.uint8)
-        os.environ["HLC_SPLIT_FIRST_VOTES"] = "100"
+        os.environ["HLC_SPLIT_VOTES"] = "100"
         try:
             with pytest.raises(_ffi.HlcError):
                 engine.eth_verify_arrays(arena, o[:n], lens[:n], o[n:2 * n], lens[n:2 * n], o[2 * n:], lens[2 * n:],
                                          out=(st, addr))
         finally:
-            os.environ.pop("HLC_SPLIT_FIRST_VOTES", None)
+            os.environ.pop("HLC_SPLIT_VOTES", None)
         assert (st == 0xAB).all() and (addr == 0xAB).all()
     st, addr = engine.eth_verify_arrays(arena, offs[:n], lens[:n], offs[n:2 * n], lens[n:2 * n], offs[2 * n:],
                                         lens[2 * n:])

@@ -14,7 +14,7 @@
 #   verify     tools/verify_latency.py (hlc_eth_verify_batch at the C ABI)
 #   profile    tools/profile.sh TAG (kernel trace + PMC passes of the headline leg)
 #   ab         tools/ab_arms.sh $AB_ARMS (alternating A/B arms: lib/variants builds or env settings)
-#   clock      tools/clock_probe.py $CLOCK_ARGS (in-kernel shader clock of k_rec_main)
+#   clock      tools/clock_probe.py over the HLC_CLOCK_PROBE builds in $CLOCK_VARIANTS, two alternating rounds
 set -o pipefail
 TAG=$1
 shift
@@ -68,8 +68,13 @@ for step in "$@"; do
   ab)
     bash tools/ab_arms.sh $AB_ARMS || exit 1 ;;
   clock)
-    timeout -k 10 300 python tools/clock_probe.py $CLOCK_ARGS > $O/clock_$TAG.txt 2> $O/clock_$TAG.err || fail clock $O/clock_$TAG.err
-    tail -20 $O/clock_$TAG.txt ;;
+    for round in 1 2; do
+      for v in $CLOCK_VARIANTS; do
+        HLC_LIB=$PWD/hashgraph-like-consensus_amd/lib/variants/libhlc_$v.so timeout -k 10 200 python tools/clock_probe.py \
+          run --tag $v > $O/clock_${TAG}_${v}_$round.log 2>&1 || fail clock $O/clock_${TAG}_${v}_$round.log
+      done
+    done
+    python tools/clock_probe.py summarize $O/clock_${TAG}_*.log | tee $O/clock_$TAG.txt ;;
   *)
     echo "unknown step $step"; exit 2 ;;
   esac
