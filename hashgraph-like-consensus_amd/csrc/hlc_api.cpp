@@ -728,6 +728,25 @@ int rest_pieces() {
   return std::max(1, std::min(k, 64));
 }
 
+// Whether [p, p + len) lies in page-locked host memory the device can DMA from directly
+// (hlc_host_alloc, hipHostMalloc or hipHostRegister): then the host-buffer entries upload that array
+// from the caller's memory and skip its staging copy.
+bool is_pinned(const void* p, size_t len) {
+  if (!p || !len) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: clear the sticky error
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost) return false;
+  hipPointerAttribute_t b;  // the last byte in the same allocation
+  if (hipPointerGetAttributes(&b, static_cast<const uint8_t*>(p) + len - 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return b.type == hipMemoryTypeHost;
+}
+
 // The host-buffer entries' streams, events, staging pool and second recovery slot (on first use).
 // The runtime maps a process's streams onto a few hardware queues per priority level
 // (GPU_MAX_HW_QUEUES, 4 on the box), and a marker recorded on a stream that shares its queue with
@@ -755,8 +774,8 @@ struct HostTrace {
   using clk = std::chrono::steady_clock;
   bool on = false;
   clk::time_point t0;
-  std::vector<std::pair<const char*, double>> host;
-  std::vector<std::pair<const char*, hipEvent_t>> dev;
+  std::vector<std::pair<std::string, double>> host;
+  std::vector<std::pair<std::string, hipEvent_t>> dev;
   hipEvent_t e0 = nullptr;
   void start(hipStream_t s) {
     if (!on) return;
@@ -764,10 +783,10 @@ struct HostTrace {
     (void)hipEventCreate(&e0);
     (void)hipEventRecord(e0, s);
   }
-  void mark(const char* what) {
+  void mark(const std::string& what) {
     if (on) host.emplace_back(what, std::chrono::duration<double, std::milli>(clk::now() - t0).count());
   }
-  void ev(const char* what, hipStream_t s) {
+  void ev(const std::string& what, hipStream_t s) {
     if (!on) return;
     hipEvent_t e = nullptr;
     if (hipEventCreate(&e) == hipSuccess) {
@@ -779,12 +798,13 @@ struct HostTrace {
     if (!on) return;
     (void)hipDeviceSynchronize();
     std::fprintf(stderr, "HLC_HOST_TRACE {\"host\": {");
-    for (size_t k = 0; k < host.size(); ++k) std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", host[k].first, host[k].second);
+    for (size_t k = 0; k < host.size(); ++k)
+      std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", host[k].first.c_str(), host[k].second);
     std::fprintf(stderr, "}, \"device\": {");
     for (size_t k = 0; k < dev.size(); ++k) {
       float f = -1;
       (void)hipEventElapsedTime(&f, e0, dev[k].second);
-      std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", dev[k].first, (double)f);
+      std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", dev[k].first.c_str(), (double)f);
       (void)hipEventDestroy(dev[k].second);
     }
     std::fprintf(stderr, "}}\n");
@@ -799,6 +819,11 @@ struct Staging {
   uint8_t* D;
   int up(size_t off, size_t len) {
     if (len) HIPCHK(hipMemcpyAsync(D + off, P + off, len, hipMemcpyHostToDevice, c->copy));
+    return 0;
+  }
+  // len bytes from the caller's page-locked memory straight to D + off (no staging copy)
+  int up_from(size_t off, const void* src, size_t len) {
+    if (len) HIPCHK(hipMemcpyAsync(D + off, src, len, hipMemcpyHostToDevice, c->copy));
     return 0;
   }
   void drain() {
@@ -858,11 +883,11 @@ int launch_fronts(hlc_ctx* c, Staging& st, HostTrace& tr, uint64_t n, const uint
         return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
       }
     }
-    tr.mark("sigs_staged");
+    tr.mark("sigs_staged_" + std::to_string(k));
     CHK(st.up(o_sig + 65 * a0, 65 * m));
     CHK(st.up(o_len + 4 * a0, 4 * m));
     HIPCHK(hipEventRecord(c->ev_sig[k], c->copy));
-    tr.ev("sigs_landed", c->copy);
+    tr.ev("sigs_landed_" + std::to_string(k), c->copy);
     hipStream_t a = aux[k % 2];
     HIPCHK(hipStreamWaitEvent(a, c->ev_sig[k], 0));
     const uint8_t* sb = st.D + o_sig + 65 * a0;
@@ -871,7 +896,7 @@ int launch_fronts(hlc_ctx* c, Staging& st, HostTrace& tr, uint64_t n, const uint
     hlc::launch_recover_main(m, sb, nullptr, 0, scratch[k % 2], c->rec_lanes, wb.as<uint32_t>(), a, c->rec_force_exact);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_main[k], a));
-    tr.ev("main_end", a);
+    tr.ev("main_end_" + std::to_string(k), a);
     fronts.push_back(RecFront{a0, a0 + m, wb.as<uint32_t>(), c->ev_main[k]});
   }
   return 0;
@@ -939,7 +964,22 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   std::vector<RecFront> fronts;
   CHK(launch_fronts(c, st, tr, n, v->bytes, v->bytes_len, v->field_off + HLC_F_SIGNATURE,
                     v->field_len + HLC_F_SIGNATURE, HLC_NFIELDS, o[0], o[1], fronts));
-  // everything else, piece by piece, field checks on the way
+  // everything else, piece by piece, field checks on the way.  An array the caller holds in
+  // page-locked memory goes to the device straight from there; the others through the staging copy.
+  struct Arr {
+    const uint8_t* src;
+    size_t dst, elem;  // staging offset, bytes per vote (0: the proposals)
+    bool pinned;
+  };
+  Arr arr[7] = {{reinterpret_cast<const uint8_t*>(v->vote_id), o[2], 4, false},
+                {reinterpret_cast<const uint8_t*>(v->proposal_id), o[3], 4, false},
+                {reinterpret_cast<const uint8_t*>(v->timestamp), o[4], 8, false},
+                {v->vote, o[5], 1, false},
+                {reinterpret_cast<const uint8_t*>(v->field_off), o[6], 8 * HLC_NFIELDS, false},
+                {reinterpret_cast<const uint8_t*>(v->field_len), o[7], 4 * HLC_NFIELDS, false},
+                {reinterpret_cast<const uint8_t*>(props), o[8], 0, false}};
+  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem ? x.elem * n : np * sizeof(hlc_proposal));
+  const bool arena_pinned = is_pinned(v->bytes, blen);
   const int K = rest_pieces();
   std::vector<int> bad(parts, 0);
   for (int k = 0; k < K; ++k) {
@@ -947,12 +987,8 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
     pool.run([&](int t, int T) {
       const uint64_t b0 = v0 + (v1 - v0) * t / T, b1 = v0 + (v1 - v0) * (t + 1) / T, m = b1 - b0;
       if (m) {
-        std::memcpy(P + o[2] + 4 * b0, v->vote_id + b0, 4 * m);
-        std::memcpy(P + o[3] + 4 * b0, v->proposal_id + b0, 4 * m);
-        std::memcpy(P + o[4] + 8 * b0, v->timestamp + b0, 8 * m);
-        std::memcpy(P + o[5] + b0, v->vote + b0, m);
-        std::memcpy(P + o[6] + 8 * HLC_NFIELDS * b0, v->field_off + HLC_NFIELDS * b0, 8 * HLC_NFIELDS * m);
-        std::memcpy(P + o[7] + 4 * HLC_NFIELDS * b0, v->field_len + HLC_NFIELDS * b0, 4 * HLC_NFIELDS * m);
+        for (const Arr& x : arr)
+          if (x.elem && !x.pinned) std::memcpy(P + x.dst + x.elem * b0, x.src + x.elem * b0, x.elem * m);
         for (uint64_t i = b0 * HLC_NFIELDS; i < b1 * HLC_NFIELDS; ++i) {
           const uint64_t off = v->field_off[i], len = v->field_len[i];
           if (len && (!v->bytes || off + len > v->bytes_len || off + len < off)) {
@@ -962,17 +998,16 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
         }
       }
       const uint64_t d0 = c0 + (c1 - c0) * t / T, d1 = c0 + (c1 - c0) * (t + 1) / T;
-      if (d1 > d0) std::memcpy(P + o[9] + d0, v->bytes + d0, d1 - d0);
-      if (k == 0 && t == 0 && np) std::memcpy(P + o[8], props, np * sizeof(hlc_proposal));
+      if (d1 > d0 && !arena_pinned) std::memcpy(P + o[9] + d0, v->bytes + d0, d1 - d0);
+      if (k == 0 && t == 0 && np && !arr[6].pinned) std::memcpy(P + o[8], props, np * sizeof(hlc_proposal));
     });
-    CHK(up(o[2] + 4 * v0, 4 * (v1 - v0)));
-    CHK(up(o[3] + 4 * v0, 4 * (v1 - v0)));
-    CHK(up(o[4] + 8 * v0, 8 * (v1 - v0)));
-    CHK(up(o[5] + v0, v1 - v0));
-    CHK(up(o[6] + 8 * HLC_NFIELDS * v0, 8 * HLC_NFIELDS * (v1 - v0)));
-    CHK(up(o[7] + 4 * HLC_NFIELDS * v0, 4 * HLC_NFIELDS * (v1 - v0)));
-    if (k == 0) CHK(up(o[8], np * sizeof(hlc_proposal)));
-    CHK(up(o[9] + c0, c1 - c0));
+    for (const Arr& x : arr) {
+      const size_t off = x.elem ? x.elem * v0 : 0, len = x.elem ? x.elem * (v1 - v0) : (k == 0 ? np * sizeof(hlc_proposal) : 0);
+      if (x.pinned) CHK(st.up_from(x.dst + off, x.src + off, len));
+      else CHK(up(x.dst + off, len));
+    }
+    if (arena_pinned) CHK(st.up_from(o[9] + c0, v->bytes + c0, c1 - c0));
+    else CHK(up(o[9] + c0, c1 - c0));
   }
   tr.mark("rest_staged");
   HIPCHK(hipEventRecord(c->ev_rest, c->copy));
@@ -1059,15 +1094,25 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   CHK(launch_fronts(c, st, tr, n, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], fronts));
   const int K = rest_pieces(), parts = pool.parts();
   std::vector<int> bad(parts, 0);
+  // (an array the caller holds in page-locked memory is uploaded from there, with no staging copy)
+  struct Arr {
+    const uint8_t* src;
+    size_t dst, elem;
+    bool pinned;
+  };
+  Arr arr[4] = {{reinterpret_cast<const uint8_t*>(id_len), o[2], 4, false},
+                {reinterpret_cast<const uint8_t*>(pay_len), o[3], 4, false},
+                {reinterpret_cast<const uint8_t*>(id_off), o[4], 8, false},
+                {reinterpret_cast<const uint8_t*>(pay_off), o[5], 8, false}};
+  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
+  const bool arena_pinned = is_pinned(bytes, blen);
   for (int k = 0; k < K; ++k) {
     const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K, c0 = blen * k / K, c1 = blen * (k + 1) / K;
     pool.run([&](int t, int T) {
       const uint64_t b0 = v0 + (v1 - v0) * t / T, b1 = v0 + (v1 - v0) * (t + 1) / T, m = b1 - b0;
       if (m) {
-        std::memcpy(st.P + o[2] + 4 * b0, id_len + b0, 4 * m);
-        std::memcpy(st.P + o[3] + 4 * b0, pay_len + b0, 4 * m);
-        std::memcpy(st.P + o[4] + 8 * b0, id_off + b0, 8 * m);
-        std::memcpy(st.P + o[5] + 8 * b0, pay_off + b0, 8 * m);
+        for (const Arr& x : arr)
+          if (!x.pinned) std::memcpy(st.P + x.dst + x.elem * b0, x.src + x.elem * b0, x.elem * m);
         for (uint64_t i = b0; i < b1; ++i) {
           const uint64_t f[3][2] = {{id_off[i], id_len[i]}, {pay_off[i], pay_len[i]}, {sig_off[i], sig_len[i]}};
           for (const auto& x : f) {
@@ -1079,11 +1124,14 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
         }
       }
       const uint64_t d0 = c0 + (c1 - c0) * t / T, d1 = c0 + (c1 - c0) * (t + 1) / T;
-      if (d1 > d0) std::memcpy(st.P + o[6] + d0, bytes + d0, d1 - d0);
+      if (d1 > d0 && !arena_pinned) std::memcpy(st.P + o[6] + d0, bytes + d0, d1 - d0);
     });
-    for (int q = 2; q <= 3; ++q) CHK(st.up(o[q] + 4 * v0, 4 * (v1 - v0)));
-    for (int q = 4; q <= 5; ++q) CHK(st.up(o[q] + 8 * v0, 8 * (v1 - v0)));
-    CHK(st.up(o[6] + c0, c1 - c0));
+    for (const Arr& x : arr) {
+      if (x.pinned) CHK(st.up_from(x.dst + x.elem * v0, x.src + x.elem * v0, x.elem * (v1 - v0)));
+      else CHK(st.up(x.dst + x.elem * v0, x.elem * (v1 - v0)));
+    }
+    if (arena_pinned) CHK(st.up_from(o[6] + c0, bytes + c0, c1 - c0));
+    else CHK(st.up(o[6] + c0, c1 - c0));
   }
   tr.mark("rest_staged");
   HIPCHK(hipEventRecord(c->ev_rest, c->copy));
@@ -1138,6 +1186,18 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
 extern "C" {
 
 const char* hlc_last_error(void) { return g_err.c_str(); }
+
+int hlc_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return set_err(HLC_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!bytes) return 0;
+  HIPCHK(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  return 0;
+}
+
+void hlc_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
 
 int hlc_abi_version(void) { return HLC_ABI_VERSION; }
 

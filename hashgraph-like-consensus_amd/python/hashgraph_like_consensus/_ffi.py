@@ -133,7 +133,7 @@ EXPORTED_SYMBOLS = (
     "hlc_ctx_set_kernel_timing", "hlc_ctx_take_kernel_time", "hlc_ctx_take_chain_time", "hlc_consensus_timeout_batch",
     "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
     "hlc_process_votes", "hlc_process_votes_device", "hlc_synth_arena_bytes", "hlc_synth_votes_device",
-    "hlc_synth_byzantine_device", "hlc_outcome_counts_device",
+    "hlc_synth_byzantine_device", "hlc_outcome_counts_device", "hlc_host_alloc", "hlc_host_free",
 )
 
 _lib = None
@@ -163,6 +163,10 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_last_error.restype = c_char_p
     lib.hlc_abi_version.argtypes = []
     lib.hlc_abi_version.restype = c_int
+    lib.hlc_host_alloc.argtypes = [c_uint64, POINTER(c_void_p)]
+    lib.hlc_host_alloc.restype = c_int
+    lib.hlc_host_free.argtypes = [c_void_p]
+    lib.hlc_host_free.restype = None
     lib.hlc_compute_vote_hashes.argtypes = [vp, POINTER(hlc_votes), u8p]
     lib.hlc_compute_vote_hashes.restype = c_int
     lib.hlc_eth_verify_batch.argtypes = [vp, c_uint64, u8p, c_uint64, u64p, u32p, u64p, u32p,
@@ -226,3 +230,44 @@ def ptr(arr, ctype):
     if arr is None:
         return None
     return arr.ctypes.data_as(POINTER(ctype))
+
+
+class PinnedArena:
+    """Page-locked host memory from hlc_host_alloc, handed out as numpy arrays (`take`): input
+    arrays built here reach the device without the host-buffer entries' staging copy.  Freed with
+    the object (keep it alive while its arrays are in use)."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        self._lib = load_library()
+        self._p = c_void_p()
+        check(self._lib.hlc_host_alloc(max(int(nbytes), 1), ctypes.byref(self._p)))
+        self.nbytes = int(nbytes)
+        buf = (ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self._p.value)
+        self._u8 = np.frombuffer(buf, dtype=np.uint8)
+        self._used = 0
+
+    def take(self, shape, dtype):
+        """A zeroed array of `shape` / `dtype` carved out of the arena (64-byte aligned)."""
+        import numpy as np
+        dt = np.dtype(dtype)
+        count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+        start = (self._used + 63) & ~63
+        end = start + count * dt.itemsize
+        if end > self.nbytes:
+            raise MemoryError("PinnedArena exhausted")
+        self._used = end
+        a = self._u8[start:end].view(dt).reshape(shape)
+        a[...] = 0
+        return a
+
+    def close(self):
+        if self._p is not None and self._p.value:
+            self._lib.hlc_host_free(self._p)
+        self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -51,6 +51,22 @@ class VoteBatch:
         off, ln = int(self.field_off[i, k]), int(self.field_len[i, k])
         return self.arena[off:off + ln].tobytes()
 
+    def pinned(self) -> "VoteBatch":
+        """The same batch with every array in page-locked memory (hlc_host_alloc, one
+        _ffi.PinnedArena kept alive by the returned batch): hlc_validate_proposals then DMAs the
+        arrays without its staging copy -- the layout an embedder that builds its batches in
+        hlc_host_alloc memory hands over."""
+        arrs = (self.vote_id, self.proposal_id, self.timestamp, self.vote, self.arena, self.field_off, self.field_len)
+        pa = _ffi.PinnedArena(sum(a.nbytes + 64 for a in arrs) + 64)
+        out = []
+        for a in arrs:
+            b = pa.take(a.shape, a.dtype)
+            b[...] = a
+            out.append(b)
+        vb = VoteBatch(*out)
+        vb._pinned = pa
+        return vb
+
 
 def pack_votes(votes: Sequence[Vote]) -> VoteBatch:
     n = len(votes)

@@ -201,16 +201,31 @@ typedef struct hlc_ctx hlc_ctx;
  * state is what the static `Signer::verify` of signing.rs:69 needs).  Every context allocates
  * and builds its fixed-base tables (~40 ms): the u1 G comb of the recovery, 12 x 2^21 affine
  * points = 1.5 GiB of HBM, and the 512 KiB signing comb; HLC_ENOMEM (with hlc_last_error) when
- * they do not fit.  The recovery's per-lane workspace (~360 MB) and the per-vote workspace
- * (~0.5 KB per vote of the largest batch) are allocated on first use (or hlc_ctx_reserve). */
+ * they do not fit.  The recovery's per-lane workspace (~205 MB: one R table of 16 x 64 B plus the
+ * z-ratios per lane of the persistent grid) and the per-vote workspace (~0.5 KB per vote of the
+ * largest batch) are allocated on first use (or hlc_ctx_reserve).
+ * The host-buffer entries (hlc_validate_proposals, hlc_eth_verify_batch) add on their first call:
+ * a second per-lane recovery workspace (~205 MB; their recovery ranges alternate over two streams),
+ * the per-vote records of each recovery range (~0.3 KB per vote), page-locked staging of the
+ * inputs (the call's input bytes + 69 B per vote of dense signatures) and of the outputs, and a
+ * device copy of each; all are kept for later calls of the same or smaller size. */
 int hlc_ctx_create(int device, hlc_ctx** out);
 void hlc_ctx_destroy(hlc_ctx* ctx);
-/* Pre-sizes the validate-many workspace (hlc_validate_proposals[_device] up to these sizes then
- * allocates nothing).  The wire-decode and streaming paths grow their own workspace on first
- * use and keep it for later calls of the same or smaller size. */
+/* Pre-sizes the device-resident validate-many workspace (hlc_validate_proposals_device up to these
+ * sizes then allocates nothing; the host-buffer entries still add what hlc_ctx_create lists).  The
+ * wire-decode and streaming paths grow their own workspace on first use and keep it for later
+ * calls of the same or smaller size. */
 int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, uint64_t max_bytes);
 const char* hlc_last_error(void);
 int hlc_abi_version(void);
+
+/* Page-locked host memory (hipHostMalloc): input arrays a caller builds in it (the SoA arrays,
+ * the byte arena, the proposals; identities / payloads / signatures of hlc_eth_verify_batch) are
+ * DMA'd to the device straight from there by the host-buffer entries, with no staging copy (any
+ * array may be page-locked or not; the library checks each one per call).  hlc_host_free releases
+ * it.  Not tied to a context. */
+int hlc_host_alloc(uint64_t bytes, void** out);
+void hlc_host_free(void* p);
 
 /* ---- Measurement hooks (bench.py roofline): HIP events on the launch stream ------ */
 /* enable != 0: every validate-many call records hipEvents around the signature-recovery

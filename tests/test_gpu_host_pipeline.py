@@ -114,3 +114,22 @@ def test_gpu_host_entry_rejects_bad_field_outputs_untouched(engine, byz, field, 
         assert (o == 0xAB).all(), "outputs were written on error"
     ok = _run(engine, b, d, now, 100)  # the context is still usable
     assert np.array_equal(ok[1], _run(engine, b, d, now, 0, 1)[1])
+
+
+def test_gpu_host_entry_pinned_inputs(engine, byz):
+    """Inputs the caller built in page-locked memory (hlc_host_alloc) are DMA'd without the staging
+    copy: all arrays pinned, or only some (the library checks each one), equal the pageable call and
+    the oracle bit for bit."""
+    b, d, now = byz
+    ref = _run(engine, b, d, now, "100")
+    pb = b.pinned()
+    got = _run(engine, pb, d, now, "100")
+    for x, y in zip(ref, got):
+        assert np.array_equal(x, y)
+    mixed = b.__class__(b.vote_id, pb.proposal_id, b.timestamp, pb.vote, pb.arena, b.field_off, pb.field_len)
+    got2 = _run(engine, mixed, d, now, "64,128")
+    for x, y in zip(ref, got2):
+        assert np.array_equal(x, y)
+    cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
+    assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
+    assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec)

@@ -41,6 +41,7 @@ def main() -> int:
     ap.add_argument("--threads", default="4", help="HLC_HOST_THREADS settings")
     ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
     ap.add_argument("--proposals", type=int, default=10_000)
+    ap.add_argument("--pinned", action="store_true", help="the host batch in page-locked memory (hlc_host_alloc)")
     ap.add_argument("--print-trace", default=None, help="print an HLC_HOST_TRACE log as a table and exit")
     a = ap.parse_args()
     if a.print_trace:
@@ -56,6 +57,8 @@ def main() -> int:
     eng = Engine(0)
     db = DeviceBatch.synthetic(eng, a.proposals, 64, 64, True, synth.config_seed(2))
     b, d, _ = db.to_host()
+    if a.pinned:
+        b = b.pinned()
     torch.cuda.synchronize()
     bytes_in = int(b.arena.nbytes + b.vote_id.nbytes + b.proposal_id.nbytes + b.timestamp.nbytes + b.vote.nbytes
                    + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
@@ -75,7 +78,7 @@ def main() -> int:
         for _ in range(a.steps):
             eng.validate_proposals(b, d, db.now, want_votes=True)
         el = (time.perf_counter() - t) / a.steps
-        row = {"split": sp, "rest_pieces": int(pc), "threads": int(th), "ms_per_call": el * 1e3,
+        row = {"split": sp, "rest_pieces": int(pc), "threads": int(th), "pinned": a.pinned, "ms_per_call": el * 1e3,
                "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in, "outputs_equal_first_setting": True}
         print(json.dumps(row), flush=True)
     eng.close()
