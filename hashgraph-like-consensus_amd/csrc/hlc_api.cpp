@@ -384,8 +384,11 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
   }
   if (c->timing) HIPCHK(hipEventRecord(p0, aux));
+  // votes the checks before the signature reject (proposal_id mismatch, empty owner / vote_hash,
+  // no covering proposal) are not recovered: vote_prop exists before the fork
+  const hlc::RecSkip skip{vote_prop, dprops, dv->proposal_id, dv->field_len};
   hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
-                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux);
+                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux, &skip);
   if (c->timing) {
     HIPCHK(hipEventRecord(p1, aux));
     c->rec_prep_ev.emplace_back(p0, p1);

@@ -69,8 +69,17 @@ void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop
 // the main stage (u2 R) only the prep records, so a caller may enqueue both on a second stream
 // concurrently with the prehash kernels; the finish (k_rec_comb: u1 G + the addition; k_rec_final;
 // k_rec_addr) once both are done
+// validate-many's checks before the signature (skip != nullptr in launch_recover_prep): votes that
+// fail them are not recovered (their status does not depend on it)
+struct RecSkip {
+  const uint32_t* vote_prop;   // proposal index per vote (NO_PROP: not covered)
+  const hlc_proposal* props;
+  const uint32_t* proposal_id; // per vote
+  const uint32_t* field_len;   // hlc_votes.field_len
+};
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
-                         const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s);
+                         const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s,
+                         const RecSkip* skip = nullptr);
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact = 0);
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,

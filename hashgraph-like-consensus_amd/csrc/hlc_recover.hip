@@ -28,10 +28,12 @@ constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
 // Lane t owns votes t + k * L (k < REC_BATCH): a wave reads 64 consecutive votes per k.
 // Forward: acc_k = mont(acc_{k-1}, r_k) = (prod r) R^-k over the lane's valid votes, each acc_{k-1}
 // kept in `pfx`; one inversion cur = acc^-1; backward: r_k^-1 = mont(acc_{k-1}, cur),
-// cur = mont(cur, r_k).  The stage reads only the signatures (every 65-byte one: which votes the
-// pre-checks reject is not known yet), so it runs on a second stream while the prehash kernels
-// run (hlc_api.cpp vote_stage); a vote's scheme error goes to bits 8-15 of its record flags and
-// the main stage turns it into the vote's state.
+// cur = mont(cur, r_k).  The stage reads the signatures (and, in validate-many, the checks that
+// precede the signature in validate_vote) while the prehash kernels run on the launch stream
+// (hlc_api.cpp vote_stage).  It decides every vote that needs no recovery -- no 65-byte signature, a
+// v / r / s the scheme rejects, or (skip != nullptr) a vote the pre-checks reject whatever its
+// signature -- writing its k_rec_main state byte, and appends the others to the work list that
+// k_rec_main's waves take their votes from (in runs of up to 64 consecutive votes).
 constexpr int PREP_TPB = 64;
 constexpr uint32_t PREP_SKIP = 0xFFu;  // record flags bits 8-15: no 65-byte signature, not parsed
 // k_rec_main -> k_rec_comb, one byte per vote: u2 R finite / at infinity / nothing to recover, or
@@ -54,29 +56,46 @@ HLC_DEV bool prep_sig(const uint8_t* bytes, const uint64_t* sig_off, size_t off_
   return true;
 }
 
+// The checks validate_proposal / validate_vote make before the signature (utils.rs:113-115 proposal_id
+// match, 133-140 empty owner / vote_hash; the empty signature is a length skip already), and votes no
+// proposal covers: such a vote's status never depends on its recovery (k_prehash_fused decides it
+// from the same fields), so k_rec_main does not run its u2 R chain.
+HLC_DEV bool pre_rejected(const RecSkip& k, uint64_t i) {
+  if (!k.vote_prop) return false;
+  const uint32_t p = k.vote_prop[i];
+  if (p == NO_PROP) return true;
+  if (k.proposal_id[i] != k.props[p].proposal_id) return true;
+  const uint32_t* fl = k.field_len + i * HLC_NFIELDS;
+  return fl[HLC_F_OWNER] == 0 || fl[HLC_F_VOTE_HASH] == 0;
+}
+
 __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, const uint8_t* bytes,
                                                        const uint64_t* sig_off, size_t off_stride,
                                                        const uint32_t* sig_len, size_t len_stride, uint32_t* rec,
-                                                       uint32_t* pfx, unsigned long long* main_ctr) {
+                                                       uint32_t* pfx, uint8_t* mst, uint32_t* list,
+                                                       unsigned long long* list_len, RecSkip sk) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t == 0) *main_ctr = 0;  // k_rec_main's work counter (it runs after this kernel)
   if (t >= L) return;
   fe acc;
   fe_set(acc, 1);
+  uint32_t active = 0;  // bit k: vote t + k L goes to k_rec_main
 #pragma unroll 1
   for (int k = 0; k < REC_BATCH; ++k) {
     const uint64_t i = t + (uint64_t)k * L;
     if (i >= n) break;
     fe r, s;
     int parity, code;
-    if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) {
+    if (pre_rejected(sk, i) || !prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) {
       rec[(size_t)REC_FLAGS * n + i] = PREP_SKIP << 8;
+      mst[i] = MST_SKIP;
       continue;
     }
     if (code != SCHEME_NONE) {
       rec[(size_t)REC_FLAGS * n + i] = (uint32_t)code << 8;
+      mst[i] = (uint8_t)(1 + code);
       continue;
     }
+    active |= 1u << k;
     store_fe_ws(acc, pfx + (size_t)k * 8 * L + t, L);
     sc_mont_mul(acc, acc, r);
   }
@@ -85,15 +104,27 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
 #pragma unroll 1
   for (int k = REC_BATCH - 1; k >= 0; --k) {
     const uint64_t i = t + (uint64_t)k * L;
-    if (i >= n) continue;
+    if (i >= n || !((active >> k) & 1u)) continue;
     fe r, s, prev, rinv;
     int parity, code;
-    if (!prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code) || code != SCHEME_NONE)
-      continue;
+    prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code);
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
     sc_mont_mul(rinv, prev, cur);  // r_k^-1
     sc_mont_mul(cur, cur, r);      // acc_{k-1}^-1
     rec_prep_scalars(s, rinv, parity, rec + i, n);
+  }
+  // the work list: per k, the wave's active votes (64 consecutive indices) in one run, one atomic
+  const unsigned lane = threadIdx.x & 63u;
+#pragma unroll 1
+  for (int k = 0; k < REC_BATCH; ++k) {
+    const bool a = (active >> k) & 1u;
+    const unsigned long long bal = __ballot(a);
+    if (!bal) continue;
+    const unsigned leader = (unsigned)__ffsll((long long)bal) - 1u;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(list_len, (unsigned long long)__popcll(bal));
+    base = __shfl(base, (int)leader);
+    if (a) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)(t + (uint64_t)k * L);
   }
 }
 
@@ -110,7 +141,9 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
                                                                      const uint64_t* sig_off, size_t off_stride,
                                                                      uint32_t* scratch, uint64_t lanes,
                                                                      const uint32_t* rec, uint32_t* q, uint8_t* mst,
-                                                                     int force_exact, unsigned long long* ctr) {
+                                                                     int force_exact, unsigned long long* ctr,
+                                                                     const uint32_t* list,
+                                                                     const unsigned long long* list_len) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
   rtab29 tab;
@@ -122,21 +155,17 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
   uint32_t done = 0;
 #endif
   const unsigned lane = threadIdx.x & 63u;
+  const unsigned long long nl = *list_len;  // votes k_rec_prep listed
   for (;;) {
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(ctr, 64ull);
     base = __shfl(base, 0);
-    if (base >= n) break;
-    const uint64_t i = base + lane;
-    if (i >= n) continue;  // the next grab is past n: the wave leaves together
+    if (base >= nl) break;
+    if (base + lane >= nl) continue;  // the next grab is past the list's end: the wave leaves together
+    const uint64_t i = list[base + lane];
 #ifdef HLC_CLOCK_PROBE
     ++done;
 #endif
-    const uint32_t prep_code = (rec[(size_t)REC_FLAGS * n + i] >> 8) & 0xFFu;
-    if (prep_code != SCHEME_NONE) {  // no 65-byte signature, or v / r / s rejected by the prep stage
-      mst[i] = prep_code == PREP_SKIP ? MST_SKIP : (uint8_t)(1 + prep_code);
-      continue;
-    }
     fe r, qx, qy, qz;
     bool inf = false;
     fe_load_be(r, sig_at(bytes, sig_off, off_stride, i));
@@ -364,7 +393,7 @@ uint64_t recover_scratch_words() { return SCRATCH_WORDS; }
 
 uint64_t recover_work_words(uint64_t n) {
   const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH, Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
-  return n * (uint64_t)(REC_WORDS + Q_WORDS) + std::max(L * REC_BATCH, Lf * FIN_BATCH) * 8 + (n + 3) / 4 + 64;
+  return n * (uint64_t)(REC_WORDS + Q_WORDS + 1) + std::max(L * REC_BATCH, Lf * FIN_BATCH) * 8 + (n + 3) / 4 + 64;
 }
 
 uint64_t recover_grid_lanes() {
@@ -378,32 +407,35 @@ uint64_t recover_grid_lanes() {
 
 namespace {
 struct RecBufs {
-  uint32_t *rec, *q, *pfx;
+  uint32_t *rec, *q, *pfx, *list;
   uint8_t* mst;
-  unsigned long long* ctr;
+  unsigned long long* ctr;  // [0] k_rec_main's grab counter, [1] the work list's length
   uint64_t L;
 };
 RecBufs rec_bufs(uint64_t n, uint32_t* work) {
   RecBufs b;
   b.rec = work;
   b.q = b.rec + n * (uint64_t)REC_WORDS;
-  b.pfx = b.q + n * (uint64_t)Q_WORDS;
+  b.list = b.q + n * (uint64_t)Q_WORDS;
+  b.pfx = b.list + n;
   b.L = (n + REC_BATCH - 1) / REC_BATCH;
   const uint64_t Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
   b.mst = reinterpret_cast<uint8_t*>(b.pfx + std::max(b.L * REC_BATCH, Lf * FIN_BATCH) * 8);  // n bytes
-  // k_rec_main's work counter: 8-byte aligned inside the 64-word tail of recover_work_words(n)
+  // the two counters: 8-byte aligned inside the 64-word tail of recover_work_words(n)
   b.ctr = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(b.mst + n) + 7) & ~uintptr_t(7));
   return b;
 }
 }  // namespace
 
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
-                         const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s) {
+                         const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s, const RecSkip* skip) {
   if (!n) return;
   const RecBufs b = rec_bufs(n, work);
   const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
+  (void)hipMemsetAsync(b.ctr, 0, 2 * sizeof(unsigned long long), s);  // grab counter, list length
+  const RecSkip none{nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, bytes, sig_off, off_stride, sig_len,
-                     len_stride, b.rec, b.pfx, b.ctr);
+                     len_stride, b.rec, b.pfx, b.mst, b.list, b.ctr + 1, skip ? *skip : none);
 }
 
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
@@ -414,7 +446,7 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
   uint64_t need = (n + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
   hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, bytes, sig_off, off_stride, scratch,
-                     (uint64_t)blocks * REC_TPB, b.rec, b.q, b.mst, force_exact, b.ctr);
+                     (uint64_t)blocks * REC_TPB, b.rec, b.q, b.mst, force_exact, b.ctr, b.list, b.ctr + 1);
 }
 
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
