@@ -177,6 +177,67 @@ def rocprof_kernel_ms():
     return out
 
 
+CHAIN_KERNELS = ("k_chain_small", "k_clear_if", "k_tables", "k_chain_check", "k_vote_status", "k_finalize")
+HBM_ACHIEVABLE_GBPS = 6290.0  # MI355X_MICROARCH.md: 8 TB/s spec, 6.29 TB/s measured (float4 copy)
+
+
+def chain_counters(trace_dir: str, fetch_dir: str, write_dir: str):
+    """Chain check + duplicate detection + tally kernels (validate_vote_chain utils.rs:175-215,
+    initialize_with_votes session.rs:253-298, the tally utils.rs:227-286; k_vote_status's per-proposal
+    first failing vote with them) per validate-many call, from the committed profile: each kernel's
+    memory-side bytes (FETCH_SIZE doubled per the gfx950 note of MI355X_MICROARCH.md, the raw figure
+    beside it; WRITE_SIZE) over its own duration in a kernel trace where it runs alone (HLC_SERIAL_STAGES
+    =1 for config 2, where k_chain_small otherwise shares the SIMDs with k_rec_main), and the achieved
+    GB/s against the guide's measured 6.29 TB/s.  Per call = sum over the kernel's launches / the calls
+    (k_finalize launches)."""
+    import csv
+    import re
+
+    def rows(sub, fname):
+        path = os.path.join(PMC_PROFILE, sub, fname)
+        if not os.path.exists(path):
+            return []
+        with open(path, newline="") as f:
+            return list(csv.DictReader(f))
+
+    def kname(r):
+        m = re.search(r"::(k_\w+)\(", r["Kernel_Name"])
+        return m.group(1) if m else None
+
+    tr = rows(trace_dir, "run_kernel_trace.csv")
+    calls = sum(1 for r in tr if kname(r) == "k_finalize")
+    if not calls:
+        return None
+    dur = {k: 0.0 for k in CHAIN_KERNELS}
+    for r in tr:
+        k = kname(r)
+        if k in dur:
+            dur[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    out = {}
+    for sub, ctr in ((fetch_dir, "FETCH_SIZE"), (write_dir, "WRITE_SIZE")):
+        rr = rows(sub, "run_counter_collection.csv")
+        pc = sum(1 for r in rr if kname(r) == "k_finalize" and r["Counter_Name"] == ctr)
+        for k in CHAIN_KERNELS:
+            v = sum(float(r["Counter_Value"]) for r in rr if kname(r) == k and r["Counter_Name"] == ctr) * 1024.0
+            out.setdefault(k, {})[ctr] = v / max(pc, 1)
+    per = {}
+    tot_b = tot_raw = tot_ms = 0.0
+    for k in CHAIN_KERNELS:
+        f = out.get(k, {}).get("FETCH_SIZE", 0.0)
+        w = out.get(k, {}).get("WRITE_SIZE", 0.0)
+        ms = dur[k] / calls
+        b = 2.0 * f + w
+        per[k] = {"fetch_raw_bytes": f, "fetch_bytes": 2.0 * f, "write_bytes": w, "ms": ms,
+                  "GBps": b / max(ms * 1e-3, 1e-12) / 1e9 if ms > 0 else None}
+        tot_b += b
+        tot_raw += f + w
+        tot_ms += ms
+    gbps = tot_b / max(tot_ms * 1e-3, 1e-12) / 1e9
+    return {"bytes_per_call": tot_b, "bytes_per_call_raw_fetch": tot_raw, "isolated_ms_per_call": tot_ms,
+            "GBps": gbps, "frac_of_hbm_achievable": gbps / HBM_ACHIEVABLE_GBPS, "per_kernel": per,
+            "source": f"{os.path.relpath(PMC_PROFILE, ROOT)}/{{{trace_dir},{fetch_dir},{write_dir}}}"}
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -437,6 +498,7 @@ def config3_leg(eng, args, torch, synth, DeviceBatch, dev, ct):
     ch_s = ch_ms / max(ch_n, 1) / 1e3
     ch_bytes = ct["bytes_per_vote"] * V + ct["bytes_per_proposal"]
     return {
+        "chain_tally_counters": chain_counters("c3_trace", "c3_fetch", "c3_write"),
         "metric": "verified votes/s, config 3 (1 P2P proposal, 1,000,000 chained votes, n = 1,500,000)",
         "value": V / el,
         "unit": "votes/s",
@@ -735,11 +797,13 @@ def main() -> int:
         },
         "chain_tally": {
             "what": "chain check + duplicate detection + tally kernels (utils.rs:175-286, session.rs:253-298), "
-                    "HIP-event bracket per call",
+                    "HIP-event bracket per call (k_chain_small shares the SIMDs with k_rec_main here, so the "
+                    "bracket is stretched; `counters` holds the isolated, counter-based figures)",
             "ms_per_call": chain_avg_s * 1e3,
             "bytes_per_call": chain_bytes,
             "GBps": chain_bytes / max(chain_avg_s, 1e-12) / 1e9,
             "bytes_model": ct["source"],
+            "counters": chain_counters("trace_serial", "pmc_fetch", "pmc_write") if config == 2 else None,
         },
         "gen_seconds": t_gen,
     }
