@@ -174,10 +174,6 @@ HLC_HD void fe29_neg(fe29& r, const fe29& a);
 // a lazy value < 2^30 -- the sign of a gathered table entry's y, which only enters products and
 // lazy subtractions (hlc_point29.hpp).  64p - a == 64p + ~a + 1 (mod 2^32).
 HLC_HD void fe29_cneg_lazy(fe29& r, const fe29& a, bool c) {
-#ifdef HLC_BRANCH_NEG  // A/B: the branchy, carried negation it replaced
-  if (c) fe29_neg(r, a); else r = a;
-  return;
-#endif
   const uint32_t m = 0u - (uint32_t)c;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {

@@ -24,7 +24,8 @@ static void st(uint32_t* p, const fe29& r) {
 extern "C" {
 // op: 0 mul, 1 sqr, 2 add, 3 sub, 4 neg, 5 mul_small(m = b[0]), 6 normalize, 7 is_zero (out[0]),
 //     8 from32 (a = 8 words), 9 to32 (out = 8 words), 10 sub_lazy, 11 norm (carry step),
-//     12 sub2, 13 sub_b2c, 14 cneg_lazy, 15 muladd (b = [b; c; e] rows)
+//     12 sub2, 13 sub_b2c, 14 cneg_lazy, 15 muladd (b = [b; c; e] rows), 16 mul_add (a b + f, b =
+//     [b; f] rows, f raw addend words), 17 sqr_add (a^2 + f, b = f rows), 18 neg_addend (f = 128p - a - b)
 void fe29_op(int op, uint64_t n, const uint32_t* a, const uint32_t* b, uint32_t* out) {
   for (uint64_t k = 0; k < n; ++k) {
     const uint32_t* x = a + 9 * k;
@@ -48,6 +49,9 @@ void fe29_op(int op, uint64_t n, const uint32_t* a, const uint32_t* b, uint32_t*
       case 13: hlc::fe29_sub_b2c(r, u, v, ld(y + 9 * n)); st(o, r); break;      // a - b - 2c
       case 14: hlc::fe29_cneg_lazy(r, u, y[0] != 0); st(o, r); break;            // b[0] ? -a : a
       case 15: hlc::fe29_muladd(r, u, v, ld(y + 9 * n), ld(y + 18 * n)); st(o, r); break;  // a b + c e
+      case 16: hlc::fe29_mul_add(r, u, v, y + 9 * n); st(o, r); break;                     // a b + f
+      case 17: hlc::fe29_sqr_add(r, u, y); st(o, r); break;                                // a^2 + f
+      case 18: hlc::fe29_neg_addend(o, u, v); break;                                       // 128p - a - b
     }
   }
 }

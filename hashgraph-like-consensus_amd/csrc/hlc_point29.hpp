@@ -55,33 +55,22 @@ HLC_HD void gej29_double(gej29& r, const gej29& a) {
   fe29_mul_small(E, A, 3);      // 3 X^2, normalised: it is squared next
   fe29_add(Z2, a.z, a.z);
   fe29_mul(r.z, a.y, Z2);       // Z3 = 2 Y Z
-#ifdef HLC_FUSED_SUB_OFF        // A/B: F = E^2 reduced, then a carried subtraction
-  fe29 F;
-  fe29_sqr(F, E);
-  fe29_sub2(r.x, F, D, D);      // X3 = F - 2D
-#else
   {
     uint32_t f[9];
     fe29_neg_addend(f, D, D);
     fe29_sqr_add(r.x, E, f);    // X3 = E^2 + (128p - 2D): one reduction
   }
-#endif
   fe29_sub_lazy(t, D, r.x);     // D - X3, lazy: multiplies the normalised E
-#ifdef HLC_DBL_SQR_C4           // A/B: C4 = (2B)^2 squared and subtracted after a separate product
-  fe29 C4, M;
-  fe29_sqr(C4, B2);             // 4 Y^4
-  fe29_mul(M, E, t);
-  fe29_sub2(r.y, M, C4, C4);    // Y3 = E (D - X3) - 8 Y^4
-#else
   // Y3 = E (D - X3) - 2 (2B)^2 = E t + 4B (-2B): one sum of two products, one reduction
   // (fe29_muladd).  -2B is carried to normalised form; 4B stays lazy (< 2^31.01).  Column bound:
-  // 9 (2^29.01 2^30.59 + 2^31.01 2^29.01) < 2^63.98.  (-4B against 2B would need 4B <= 128p's
-  // limb 8, 2^31 - 5, which a normalised B at its limb-8 maximum exceeds.)
+  // 9 (2^29.01 2^30.59 + 2^31.01 2^29.01) ~= 2^63.995 < 2^64; the fold and carry terms (~2^47) fit the
+  // ~2^55.8 left (tests/test_fe29_host.py::test_muladd_doubling_bounds drives every limb of 4B, E,
+  // t and -2B at its maximum).  (-4B against 2B would need 4B <= 128p's limb 8, 2^31 - 5, which a
+  // normalised B at its limb-8 maximum exceeds.)
   fe29 nb, b4;
   fe29_neg(nb, B2);
   fe29_add(b4, B2, B2);
   fe29_muladd(r.y, E, t, b4, nb);
-#endif
   r.inf = a.inf;
 }
 
@@ -101,16 +90,11 @@ HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullp
   }
   fe29 z1z1, u2, s2, h, rr, hh, i4, j, v, h2, z3, x3, t, y3, y1j;
   fe29_sqr(z1z1, a.z);
-#ifdef HLC_FUSED_SUB_OFF
-  fe29_mul(u2, b.x, z1z1);
-  fe29_sub(h, u2, a.x);
-#else
   {
     uint32_t f[9];
     fe29_neg_addend(f, a.x, fe29{});
     fe29_mul_add(h, b.x, z1z1, f);  // H = U2 - X1 = x2 Z1^2 + (128p - X1): one reduction
   }
-#endif
   fe29_mul(s2, b.y, a.z);
   fe29_mul(s2, s2, z1z1);
   fe29_sub_lazy(rr, s2, a.y);      // S2 - Y1, lazy
@@ -133,10 +117,6 @@ HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullp
   fe29_shl(i4, hh, 2);             // I = 4 HH, lazy (< 2^31.01)
   fe29_mul(j, h, i4);              // J = H I
   fe29_mul(v, a.x, i4);            // V = X1 I
-#ifdef HLC_FUSED_SUB_OFF
-  fe29_sqr(x3, rr);
-  fe29_sub_b2c(x3, x3, j, v);      // X3 = R^2 - J - 2V
-#else
   {
     uint32_t f[9];
 #pragma unroll
@@ -146,18 +126,10 @@ HLC_HD void gej29_madd(gej29& r, const gej29& a, const ge29& b, fe29* zr = nullp
     }
     fe29_sqr_add(x3, rr, f);       // X3 = R^2 + (128p - J - 2V): one reduction
   }
-#endif
   fe29_sub_lazy(t, v, x3);         // V - X3, lazy: multiplies the normalised R
-#ifdef HLC_MADD_TWO_REDUCTIONS     // A/B: the two products reduced separately, then subtracted
-  fe29_mul(y3, rr, t);
-  fe29_add(t, a.y, a.y);
-  fe29_mul(y1j, t, j);             // 2 Y1 J
-  fe29_sub(y3, y3, y1j);           // Y3 = R (V - X3) - 2 Y1 J
-#else
   fe29_neg(y1j, j);                // -J, normalised
   fe29_add(h2, a.y, a.y);          // 2 Y1 (h2 is dead here)
   fe29_muladd(y3, rr, t, h2, y1j); // Y3 = R (V - X3) + 2 Y1 (-J): one reduction for both products
-#endif
   r.x = x3;
   r.y = y3;
   r.z = z3;

@@ -501,3 +501,49 @@ def test_point_formulas_with_lazy_y(checked):
     Ai[:, 27] = 1
     mi = runp(checked, 2, Ai, B)
     assert (mi[:, 9:18] == y2).all() and (mi[:, 27] == 0).all()
+
+
+def test_muladd_doubling_bounds(checked):
+    """fe29_muladd at the operands of the doubling's Y3 = E (D - X3) + 4B (-2B) (hlc_point29.hpp
+    gej29_double), its tightest use: E normalised, t = D - X3 a lazy difference (< 2^30.59), 4B a
+    doubled doubling of a normalised B (limbs up to 4 x the normalised maxima: 2^31 + 2^21 at limb
+    2), -2B normalised -- with every limb of every operand at its maximum in the first rows."""
+    rnd = random.Random(62)
+    n = 3000
+    a, e = nrm_limbs(rnd, n), nrm_limbs(rnd, n)
+    b = limbs(rnd, n, int(2**30.59))
+    B = nrm_limbs(rnd, n)
+    c = (4 * B.astype(np.uint64)).astype(np.uint32)  # 4B, lazy
+    a[:3] = NB
+    e[:3] = NB
+    b[:3] = int(2**30.59) - 1
+    c[:3] = [4 * x for x in NB]
+    o = run(checked, 15, a, np.concatenate([b, c, e]))
+    check_normalised(o, 1, 1, rest=0)
+    for k in range(n):
+        assert val(o[k]) % P == (val(a[k]) * val(b[k]) + val(c[k]) * val(e[k])) % P, k
+
+
+def test_mul_add_sqr_add_at_bounds(checked):
+    """fe29_mul_add / fe29_sqr_add (a product and the subtraction after it with one reduction: the
+    doubling's X3 = E^2 + (128p - 2D), the mixed addition's H = x2 Z1^2 + (128p - X1) and X3, the co-Z
+    X3 / Y3): mul / sqr operands up to their bound, the addend 128p - b - c of two normalised values
+    (fe29_neg_addend) at its largest (b = c = 0) and smallest (b, c at the normalised maxima)."""
+    rnd = random.Random(63)
+    n = 3000
+    a, b = limbs(rnd, n, MUL_IN), limbs(rnd, n, MUL_IN)
+    a[:2] = MUL_IN - 1
+    b[:2] = MUL_IN - 1
+    sb, sc = nrm_limbs(rnd, n), nrm_limbs(rnd, n)
+    sb[0] = sc[0] = 0
+    sb[1] = sc[1] = NB
+    f = run(checked, 18, sb, sc)
+    o = run(checked, 16, a, np.concatenate([b, f]))
+    q = run(checked, 17, a, f)
+    check_normalised(o, 1, 1, rest=0)
+    check_normalised(q, 1, 1, rest=0)
+    for k in range(n):
+        fv = val(f[k])
+        assert fv % P == (-val(sb[k]) - val(sc[k])) % P, k
+        assert val(o[k]) % P == (val(a[k]) * val(b[k]) + fv) % P, k
+        assert val(q[k]) % P == (val(a[k]) ** 2 + fv) % P, k
