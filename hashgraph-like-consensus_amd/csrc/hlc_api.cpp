@@ -169,8 +169,8 @@ struct hlc_ctx {
   std::vector<std::unique_ptr<DBuf>> rec_works;  // per-vote records of each recovery range but the first
   PBuf pin_in, pin_out;
   DBuf dev_in, dev_out;
-  std::vector<hipEvent_t> ev_sig, ev_main;  // per recovery range: signatures landed, main stage done
-  hipEvent_t ev_rest = nullptr, ev_done = nullptr;
+  std::vector<hipEvent_t> ev_up, ev_main;  // per recovery range: inputs landed, main stage done
+  hipEvent_t ev_done = nullptr;
   std::unique_ptr<HostPool> pool;  // staging workers (HLC_HOST_THREADS)
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
@@ -197,10 +197,9 @@ struct hlc_ctx {
     for (auto& pr : rec_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : rec_prep_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    for (hipEvent_t e : ev_sig) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_up) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_main) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_rest, ev_done})
-      if (e) (void)hipEventDestroy(e);
+    if (ev_done) (void)hipEventDestroy(ev_done);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -723,14 +722,6 @@ std::vector<uint64_t> split_ranges(uint64_t n) {
   return b;  // range k = [b[k], b[k+1])
 }
 
-// Pieces the inputs other than the signatures are staged and uploaded in (HLC_REST_PIECES, default 3):
-// piece k+1 is copied into page-locked memory while piece k's DMA runs.
-int rest_pieces() {
-  const char* e = std::getenv("HLC_REST_PIECES");
-  const int k = e ? std::atoi(e) : 3;
-  return std::max(1, std::min(k, 64));
-}
-
 // Whether [p, p + len) lies in page-locked host memory the device can DMA from directly
 // (hlc_host_alloc, hipHostMalloc or hipHostRegister): then the host-buffer entries upload that array
 // from the caller's memory and skip its staging copy.
@@ -762,8 +753,7 @@ int host_resources(hlc_ctx* c) {
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   if (!c->copy) HIPCHK(hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, greatest));
   if (!c->aux2) HIPCHK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, least));
-  for (hipEvent_t* e : {&c->ev_rest, &c->ev_done})
-    if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  if (!c->ev_done) HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
   if (!c->pool || c->pool->parts() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
   CHK(ensure_recover_scratch(c));
   CHK(c->rec_scratch2.ensure(c->rec_lanes * hlc::recover_scratch_words() * sizeof(uint32_t)));
@@ -834,96 +824,99 @@ struct Staging {
   }
 };
 
-// The recovery's front half of a host-buffer call: the signatures of the items of each range of
-// split_ranges(n) (sig_off / sig_len with stride `stride`) gathered by the host pool into the dense
-// array at o_sig (65 B per item; slots of other lengths left as they are) and their lengths at
-// o_len, each range uploaded and its k_rec_prep + k_rec_main enqueued (on the aux streams in turn)
-// as soon as its DMA is enqueued.  Sizes each range's records.  HLC_EINVAL, before its bytes are
-// read, for a 65-byte signature outside the arena.
-int launch_fronts(hlc_ctx* c, Staging& st, HostTrace& tr, uint64_t n, const uint8_t* bytes, uint64_t bytes_len,
-                  const uint64_t* sig_off, const uint32_t* sig_len, size_t stride, size_t o_sig, size_t o_len,
-                  std::vector<RecFront>& fronts) {
-  HostPool& pool = *c->pool;
-  const int parts = pool.parts();
-  const std::vector<uint64_t> rb = split_ranges(n);
+// The recovery ranges of a host-buffer call (split_ranges) with their per-vote records and events.
+int prepare_ranges(hlc_ctx* c, uint64_t n, std::vector<uint64_t>& rb) {
+  rb = split_ranges(n);
   const size_t R = rb.size() - 1;
   while (c->rec_works.size() + 1 < R) c->rec_works.emplace_back(new DBuf());
-  while (c->ev_sig.size() < R) {
+  while (c->ev_up.size() < R) {
     hipEvent_t a = nullptr, b = nullptr;
     HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
-    c->ev_sig.push_back(a);
+    c->ev_up.push_back(a);
     HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
     c->ev_main.push_back(b);
   }
-  uint32_t* scratch[2] = {c->rec_scratch.as<uint32_t>(), c->rec_scratch2.as<uint32_t>()};
-  hipStream_t aux[2] = {c->aux, c->aux2};
-  fronts.clear();
   for (size_t k = 0; k < R; ++k) {
-    const uint64_t a0 = rb[k], m = rb[k + 1] - rb[k];
-    if (!m) continue;
     DBuf& wb = k == 0 ? c->rec_work : *c->rec_works[k - 1];
-    CHK(wb.ensure(hlc::recover_work_words(m) * sizeof(uint32_t)));
-    std::vector<int> bad(parts, 0);
-    pool.run([&](int t, int T) {
-      const uint64_t b0 = a0 + m * t / T, b1 = a0 + m * (t + 1) / T;
-      uint8_t* sg = st.P + o_sig;
-      uint32_t* sl = reinterpret_cast<uint32_t*>(st.P + o_len);
-      for (uint64_t i = b0; i < b1; ++i) {
-        const uint64_t off = sig_off[i * stride];
-        const uint32_t len = sig_len[i * stride];
-        sl[i] = len;
-        if (len != 65) continue;  // the prep stage skips it (a length error decided elsewhere)
-        if (!bytes || off + 65 > bytes_len || off + 65 < off) {
-          bad[t] = 1;
-          return;
-        }
-        std::memcpy(sg + 65 * i, bytes + off, 65);
-      }
-    });
-    for (int x : bad) {
-      if (x) {
-        st.drain();
-        return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-      }
-    }
-    tr.mark("sigs_staged_" + std::to_string(k));
-    CHK(st.up(o_sig + 65 * a0, 65 * m));
-    CHK(st.up(o_len + 4 * a0, 4 * m));
-    HIPCHK(hipEventRecord(c->ev_sig[k], c->copy));
-    tr.ev("sigs_landed_" + std::to_string(k), c->copy);
-    hipStream_t a = aux[k % 2];
-    HIPCHK(hipStreamWaitEvent(a, c->ev_sig[k], 0));
-    const uint8_t* sb = st.D + o_sig + 65 * a0;
-    const uint32_t* sl = reinterpret_cast<const uint32_t*>(st.D + o_len) + a0;
-    hlc::launch_recover_prep(m, sb, nullptr, 0, sl, 1, wb.as<uint32_t>(), a);
-    hlc::launch_recover_main(m, sb, nullptr, 0, scratch[k % 2], c->rec_lanes, wb.as<uint32_t>(), a, c->rec_force_exact);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev_main[k], a));
-    tr.ev("main_end_" + std::to_string(k), a);
-    fronts.push_back(RecFront{a0, a0 + m, wb.as<uint32_t>(), c->ev_main[k]});
+    CHK(wb.ensure(hlc::recover_work_words(rb[k + 1] - rb[k]) * sizeof(uint32_t)));
   }
   return 0;
 }
 
+// Range k's front half of the recovery -- k_rec_prep + k_rec_main over its m items, signatures read
+// through (sig_off, sig_len) from the device arena -- on the aux streams in turn (k even: aux, odd:
+// aux2, each with its own per-lane scratch), once its upload (ev_up[k]) has landed.
+int launch_front(hlc_ctx* c, HostTrace& tr, size_t k, uint64_t a0, uint64_t m, const uint8_t* dbytes,
+                 const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len, size_t len_stride,
+                 std::vector<RecFront>& fronts) {
+  if (!m) return 0;
+  DBuf& wb = k == 0 ? c->rec_work : *c->rec_works[k - 1];
+  hipStream_t a = k % 2 ? c->aux2 : c->aux;
+  uint32_t* scratch = (k % 2 ? c->rec_scratch2 : c->rec_scratch).as<uint32_t>();
+  HIPCHK(hipStreamWaitEvent(a, c->ev_up[k], 0));
+  hlc::launch_recover_prep(m, dbytes, sig_off, off_stride, sig_len, len_stride, wb.as<uint32_t>(), a);
+  hlc::launch_recover_main(m, dbytes, sig_off, off_stride, scratch, c->rec_lanes, wb.as<uint32_t>(), a,
+                           c->rec_force_exact);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_main[k], a));
+  tr.ev("main_end_" + std::to_string(k), a);
+  fronts.push_back(RecFront{a0, a0 + m, wb.as<uint32_t>(), c->ev_main[k]});
+  return 0;
+}
+
+// One input array of a host-buffer call: `elem` bytes per item at `src`, staged at `dst`; uploaded
+// from the caller's memory when that is page-locked.
+struct Arr {
+  const uint8_t* src;
+  size_t dst, elem;
+  bool pinned;
+};
+
+// Items [a0, a1) of the arrays: staging copies of the pageable ones, then the uploads (the pinned
+// ones straight from the caller).
+int stage_rows(Staging& st, HostPool& pool, Arr* arr, int na, uint64_t a0, uint64_t a1) {
+  pool.run([&](int t, int T) {
+    const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
+    for (int q = 0; q < na; ++q)
+      if (!arr[q].pinned && b1 > b0)
+        std::memcpy(st.P + arr[q].dst + arr[q].elem * b0, arr[q].src + arr[q].elem * b0, arr[q].elem * (b1 - b0));
+  });
+  for (int q = 0; q < na; ++q) {
+    const size_t off = arr[q].elem * a0, len = arr[q].elem * (a1 - a0);
+    if (arr[q].pinned) CHK(st.up_from(arr[q].dst + off, arr[q].src + off, len));
+    else CHK(st.up(arr[q].dst + off, len));
+  }
+  return 0;
+}
+
+// The arena bytes [lo, hi) (staged unless page-locked) -> the device arena at o_arena.
+int stage_span(Staging& st, HostPool& pool, const uint8_t* bytes, bool pinned, size_t o_arena, uint64_t lo,
+               uint64_t hi) {
+  if (hi <= lo) return 0;
+  if (pinned) return st.up_from(o_arena + lo, bytes + lo, hi - lo);
+  pool.run([&](int t, int T) {
+    const uint64_t d0 = lo + (hi - lo) * t / T, d1 = lo + (hi - lo) * (t + 1) / T;
+    if (d1 > d0) std::memcpy(st.P + o_arena + d0, bytes + d0, d1 - d0);
+  });
+  return st.up(o_arena + lo, hi - lo);
+}
+
 // hlc_validate_proposals over host buffers (what INTEGRATION.md's process_incoming_proposals calls).
-// The caller's votes go to the device through page-locked staging on the context's upload stream,
-// ordered by what the kernels need first, so that the VALU-bound recovery starts long before the
-// whole batch has landed:
-//   1. the signatures of votes [0, na), gathered into a dense array (65 B per vote) with their
-//      lengths -> k_rec_prep + k_rec_main over them on the aux stream (recovery slot 1);
-//   2. the signatures of votes [na, n) -> k_rec_prep + k_rec_main over them on the second aux stream
-//      (slot 2: its own per-lane scratch and records), whose waves take the SIMD slots the first
-//      grid's waves free (one k_rec_main tail per call, as in the device-resident call);
-//   3. every other input (SoA arrays, proposals, the byte arena) in rest_pieces() pieces, each copied
-//      into page-locked memory by the host pool while the previous piece's DMA runs -> the prehash,
-//      chain / duplicate / YES kernels on the launch stream, then each range's finish (u1 G, Z^-1,
-//      address) once its main stage is done, the statuses, tables, finalize, and one D2H of every
-//      output into page-locked memory.
-// Every field's (offset, length) is checked on the host pool while it is staged (signatures before
-// their bytes are read); a violation returns HLC_EINVAL before anything reaches the caller's outputs
-// (the device work already enqueued is drained and discarded).  Only stream / event dependencies
-// order the stages: no kernel waits on a flag, so any mapping of the streams onto hardware queues
-// is correct (one that serialises them is only slower).
+// The batch goes to the device in the recovery ranges of split_ranges(n) (small ones first) on the
+// context's upload stream: for range k the host pool copies the votes' SoA rows into page-locked
+// staging (checking every field's (offset, length) on the way and finding the arena span the
+// range's fields use), then that span; each is uploaded as soon as it is staged, and range k's
+// k_rec_prep + k_rec_main are enqueued behind its upload, on the two aux streams in turn (each with
+// its own per-lane scratch), so range k's k_rec_main waves take the SIMD slots range k-1's waves free
+// (one grid tail per call, as in the device-resident call) while the host stages range k+1.  Once
+// the last range has landed, the launch stream runs the prehash and chain kernels over the whole
+// batch, each range's finish (u1 G, Z^-1, address) after its main stage, the statuses, tables and
+// finalize, and one D2H of every output into page-locked memory.  An array the caller holds in
+// page-locked memory (hlc_host_alloc) is uploaded straight from there.  A field outside the arena
+// returns HLC_EINVAL before anything reaches the caller's outputs (device work already enqueued is
+// drained and discarded).  Only stream / event dependencies order the stages: no kernel waits on a
+// flag, so any mapping of the streams onto hardware queues is correct (one that serialises them is
+// only slower).
 int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
                   hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec) {
   const uint64_t n = v->n;
@@ -933,20 +926,18 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   HostTrace tr;
   if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
   tr.start(c->copy);
-  // inputs, page-locked and on the device alike: dense signatures | signature lengths | vote_id |
-  // proposal_id | timestamp | vote | field_off | field_len | proposals | arena
-  size_t o[11];
+  // inputs, page-locked and on the device alike: vote_id | proposal_id | timestamp | vote |
+  // field_off | field_len | proposals | arena
+  size_t o[9];
   o[0] = 0;
-  o[1] = o[0] + al256(n * 65);
+  o[1] = o[0] + al256(n * 4);
   o[2] = o[1] + al256(n * 4);
-  o[3] = o[2] + al256(n * 4);
-  o[4] = o[3] + al256(n * 4);
-  o[5] = o[4] + al256(n * 8);
-  o[6] = o[5] + al256(n);
-  o[7] = o[6] + al256(n * 8 * HLC_NFIELDS);
-  o[8] = o[7] + al256(n * 4 * HLC_NFIELDS);
-  o[9] = o[8] + al256(np * sizeof(hlc_proposal));
-  o[10] = o[9] + blen;
+  o[3] = o[2] + al256(n * 8);
+  o[4] = o[3] + al256(n);
+  o[5] = o[4] + al256(n * 8 * HLC_NFIELDS);
+  o[6] = o[5] + al256(n * 4 * HLC_NFIELDS);
+  o[7] = o[6] + al256(np * sizeof(hlc_proposal));
+  o[8] = o[7] + blen;
   // outputs: results | status | reason | recovered
   size_t r[5];
   r[0] = 0;
@@ -954,82 +945,83 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   r[2] = r[1] + al256(n + 1);
   r[3] = r[2] + al256(n + 1);
   r[4] = r[3] + (out_rec ? al256(n * 20 + 20) : 0);
-  CHK(c->pin_in.ensure(o[10] + 16));
-  CHK(c->dev_in.ensure(o[10] + 16));
+  CHK(c->pin_in.ensure(o[8] + 16));
+  CHK(c->dev_in.ensure(o[8] + 16));
   CHK(c->pin_out.ensure(r[4] + 16));
   CHK(c->dev_out.ensure(r[4] + 16));
   CHK(reserve_validate(c, n, np));
+  std::vector<uint64_t> rb;
+  CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
-  uint8_t* P = st.P;
-  uint8_t* D = st.D;
-  auto up = [&](size_t off, size_t len) { return st.up(off, len); };
+  Arr arr[6] = {{reinterpret_cast<const uint8_t*>(v->vote_id), o[0], 4, false},
+                {reinterpret_cast<const uint8_t*>(v->proposal_id), o[1], 4, false},
+                {reinterpret_cast<const uint8_t*>(v->timestamp), o[2], 8, false},
+                {v->vote, o[3], 1, false},
+                {reinterpret_cast<const uint8_t*>(v->field_off), o[4], 8 * HLC_NFIELDS, false},
+                {reinterpret_cast<const uint8_t*>(v->field_len), o[5], 4 * HLC_NFIELDS, false}};
+  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
+  Arr parr{reinterpret_cast<const uint8_t*>(props), o[6], sizeof(hlc_proposal), false};
+  parr.pinned = is_pinned(props, np * sizeof(hlc_proposal));
+  const bool arena_pinned = is_pinned(v->bytes, blen);
+  const uint8_t* D = st.D;
   const int parts = pool.parts();
   std::vector<RecFront> fronts;
-  CHK(launch_fronts(c, st, tr, n, v->bytes, v->bytes_len, v->field_off + HLC_F_SIGNATURE,
-                    v->field_len + HLC_F_SIGNATURE, HLC_NFIELDS, o[0], o[1], fronts));
-  // everything else, piece by piece, field checks on the way.  An array the caller holds in
-  // page-locked memory goes to the device straight from there; the others through the staging copy.
-  struct Arr {
-    const uint8_t* src;
-    size_t dst, elem;  // staging offset, bytes per vote (0: the proposals)
-    bool pinned;
-  };
-  Arr arr[7] = {{reinterpret_cast<const uint8_t*>(v->vote_id), o[2], 4, false},
-                {reinterpret_cast<const uint8_t*>(v->proposal_id), o[3], 4, false},
-                {reinterpret_cast<const uint8_t*>(v->timestamp), o[4], 8, false},
-                {v->vote, o[5], 1, false},
-                {reinterpret_cast<const uint8_t*>(v->field_off), o[6], 8 * HLC_NFIELDS, false},
-                {reinterpret_cast<const uint8_t*>(v->field_len), o[7], 4 * HLC_NFIELDS, false},
-                {reinterpret_cast<const uint8_t*>(props), o[8], 0, false}};
-  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem ? x.elem * n : np * sizeof(hlc_proposal));
-  const bool arena_pinned = is_pinned(v->bytes, blen);
-  const int K = rest_pieces();
-  std::vector<int> bad(parts, 0);
-  for (int k = 0; k < K; ++k) {
-    const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K, c0 = blen * k / K, c1 = blen * (k + 1) / K;
+  CHK(stage_rows(st, pool, &parr, 1, 0, np));
+  for (size_t k = 0; k + 1 < rb.size(); ++k) {
+    const uint64_t a0 = rb[k], a1 = rb[k + 1];
+    // field checks and the range's arena span (the SoA rows' staging copies ride along)
+    std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
+    std::vector<int> bad(parts, 0);
     pool.run([&](int t, int T) {
-      const uint64_t b0 = v0 + (v1 - v0) * t / T, b1 = v0 + (v1 - v0) * (t + 1) / T, m = b1 - b0;
-      if (m) {
-        for (const Arr& x : arr)
-          if (x.elem && !x.pinned) std::memcpy(P + x.dst + x.elem * b0, x.src + x.elem * b0, x.elem * m);
-        for (uint64_t i = b0 * HLC_NFIELDS; i < b1 * HLC_NFIELDS; ++i) {
-          const uint64_t off = v->field_off[i], len = v->field_len[i];
-          if (len && (!v->bytes || off + len > v->bytes_len || off + len < off)) {
-            bad[t] = 1;
-            break;
-          }
+      const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
+      uint64_t l = UINT64_MAX, h = 0;
+      for (uint64_t i = b0 * HLC_NFIELDS; i < b1 * HLC_NFIELDS; ++i) {
+        const uint64_t off = v->field_off[i], len = v->field_len[i];
+        if (!len) continue;
+        if (!v->bytes || off + len > v->bytes_len || off + len < off) {
+          bad[t] = 1;
+          return;
         }
+        l = std::min(l, off);
+        h = std::max(h, off + len);
       }
-      const uint64_t d0 = c0 + (c1 - c0) * t / T, d1 = c0 + (c1 - c0) * (t + 1) / T;
-      if (d1 > d0 && !arena_pinned) std::memcpy(P + o[9] + d0, v->bytes + d0, d1 - d0);
-      if (k == 0 && t == 0 && np && !arr[6].pinned) std::memcpy(P + o[8], props, np * sizeof(hlc_proposal));
+      lo[t] = l;
+      hi[t] = h;
     });
-    for (const Arr& x : arr) {
-      const size_t off = x.elem ? x.elem * v0 : 0, len = x.elem ? x.elem * (v1 - v0) : (k == 0 ? np * sizeof(hlc_proposal) : 0);
-      if (x.pinned) CHK(st.up_from(x.dst + off, x.src + off, len));
-      else CHK(up(x.dst + off, len));
+    uint64_t slo = UINT64_MAX, shi = 0;
+    for (int t = 0; t < parts; ++t) {
+      if (bad[t]) {
+        st.drain();
+        return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+      }
+      slo = std::min(slo, lo[t]);
+      shi = std::max(shi, hi[t]);
     }
-    if (arena_pinned) CHK(st.up_from(o[9] + c0, v->bytes + c0, c1 - c0));
-    else CHK(up(o[9] + c0, c1 - c0));
+    CHK(stage_rows(st, pool, arr, 6, a0, a1));
+    if (slo < shi) CHK(stage_span(st, pool, v->bytes, arena_pinned, o[7], slo, shi));
+    HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
+    tr.mark("staged_" + std::to_string(k));
+    tr.ev("landed_" + std::to_string(k), c->copy);
+    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[7],
+                     reinterpret_cast<const uint64_t*>(D + o[4]) + a0 * HLC_NFIELDS + HLC_F_SIGNATURE, HLC_NFIELDS,
+                     reinterpret_cast<const uint32_t*>(D + o[5]) + a0 * HLC_NFIELDS + HLC_F_SIGNATURE, HLC_NFIELDS,
+                     fronts));
   }
-  tr.mark("rest_staged");
-  HIPCHK(hipEventRecord(c->ev_rest, c->copy));
-  tr.ev("rest_landed", c->copy);
-  // the validation on the launch stream, the two recovery ranges joined in by their events
+  // the validation on the launch stream, once every range has landed (the upload stream is in order)
   hipStream_t s = c->stream;
-  HIPCHK(hipStreamWaitEvent(s, c->ev_rest, 0));
+  HIPCHK(hipStreamWaitEvent(s, c->ev_up[rb.size() - 2], 0));  // split_ranges gives >= 1 range
   hlc_votes dv;
   dv.n = n;
-  dv.vote_id = reinterpret_cast<const uint32_t*>(D + o[2]);
-  dv.proposal_id = reinterpret_cast<const uint32_t*>(D + o[3]);
-  dv.timestamp = reinterpret_cast<const uint64_t*>(D + o[4]);
-  dv.vote = D + o[5];
-  dv.field_off = reinterpret_cast<const uint64_t*>(D + o[6]);
-  dv.field_len = reinterpret_cast<const uint32_t*>(D + o[7]);
-  dv.bytes = D + o[9];
+  dv.vote_id = reinterpret_cast<const uint32_t*>(D + o[0]);
+  dv.proposal_id = reinterpret_cast<const uint32_t*>(D + o[1]);
+  dv.timestamp = reinterpret_cast<const uint64_t*>(D + o[2]);
+  dv.vote = D + o[3];
+  dv.field_off = reinterpret_cast<const uint64_t*>(D + o[4]);
+  dv.field_len = reinterpret_cast<const uint32_t*>(D + o[5]);
+  dv.bytes = D + o[7];
   dv.bytes_len = blen;
   uint8_t* ob = c->dev_out.as<uint8_t>();
-  CHK(validate_device(c, &dv, reinterpret_cast<const hlc_proposal*>(D + o[8]), np, now,
+  CHK(validate_device(c, &dv, reinterpret_cast<const hlc_proposal*>(D + o[6]), np, now,
                       reinterpret_cast<hlc_result*>(ob + r[0]), ob + r[1], ob + r[2], out_rec ? ob + r[3] : nullptr, s,
                       fronts.data(), (int)fronts.size()));
   tr.ev("kernels_end", s);
@@ -1037,12 +1029,6 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   HIPCHK(hipEventRecord(c->ev_done, s));
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
-  for (int x : bad) {
-    if (x) {
-      st.drain();
-      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-    }
-  }
   HIPCHK(hipEventSynchronize(c->ev_done));
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);
@@ -1059,12 +1045,13 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   return 0;
 }
 
-// hlc_eth_verify_batch over host buffers: the same schedule as validate_host -- the signatures
-// first (dense, two recovery ranges on two streams), then identities, payloads and the arena in
-// pieces, field checks on the way -- with the verify byte stage (length checks + EIP-191 keccak of
-// each payload, k_verify_prehash) on the launch stream, each range's finish after its main stage,
-// one D2H of the statuses (and addresses).  An (offset, length) outside the arena returns
-// HLC_EINVAL before anything reaches the caller's outputs.
+// hlc_eth_verify_batch over host buffers: the same schedule as validate_host -- the items in
+// recovery ranges (per-item offset / length rows and the range's arena span, staged unless
+// page-locked), each range's k_rec_prep + k_rec_main behind its upload on the aux streams in turn --
+// with the verify byte stage (length checks + EIP-191 keccak of each payload, k_verify_prehash) on the
+// launch stream once every range has landed, each range's finish after its main stage, one D2H of
+// the statuses (and addresses).  An (offset, length) outside the arena returns HLC_EINVAL before
+// anything reaches the caller's outputs.
 int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len, const uint64_t* id_off,
                 const uint32_t* id_len, const uint64_t* pay_off, const uint32_t* pay_len, const uint64_t* sig_off,
                 const uint32_t* sig_len, uint8_t* out_status, uint8_t* out_addr) {
@@ -1074,14 +1061,13 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   HostTrace tr;
   if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
   tr.start(c->copy);
-  // inputs: dense signatures | signature lengths | identity lengths | payload lengths | identity
-  // offsets | payload offsets | arena
+  // inputs: identity / payload / signature lengths | their offsets | arena
   size_t o[8];
   o[0] = 0;
-  o[1] = o[0] + al256(n * 65);
+  o[1] = o[0] + al256(n * 4);
   o[2] = o[1] + al256(n * 4);
   o[3] = o[2] + al256(n * 4);
-  o[4] = o[3] + al256(n * 4);
+  o[4] = o[3] + al256(n * 8);
   o[5] = o[4] + al256(n * 8);
   o[6] = o[5] + al256(n * 8);
   o[7] = o[6] + blen;
@@ -1092,64 +1078,70 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   CHK(c->dev_out.ensure(r2 + 16));
   CHK(c->pre.ensure(n + 1));
   CHK(c->kec_dig.ensure(n * 32 + 32));
+  std::vector<uint64_t> rb;
+  CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
-  std::vector<RecFront> fronts;
-  CHK(launch_fronts(c, st, tr, n, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], fronts));
-  const int K = rest_pieces(), parts = pool.parts();
-  std::vector<int> bad(parts, 0);
-  // (an array the caller holds in page-locked memory is uploaded from there, with no staging copy)
-  struct Arr {
-    const uint8_t* src;
-    size_t dst, elem;
-    bool pinned;
-  };
-  Arr arr[4] = {{reinterpret_cast<const uint8_t*>(id_len), o[2], 4, false},
-                {reinterpret_cast<const uint8_t*>(pay_len), o[3], 4, false},
-                {reinterpret_cast<const uint8_t*>(id_off), o[4], 8, false},
-                {reinterpret_cast<const uint8_t*>(pay_off), o[5], 8, false}};
+  Arr arr[6] = {{reinterpret_cast<const uint8_t*>(id_len), o[0], 4, false},
+                {reinterpret_cast<const uint8_t*>(pay_len), o[1], 4, false},
+                {reinterpret_cast<const uint8_t*>(sig_len), o[2], 4, false},
+                {reinterpret_cast<const uint8_t*>(id_off), o[3], 8, false},
+                {reinterpret_cast<const uint8_t*>(pay_off), o[4], 8, false},
+                {reinterpret_cast<const uint8_t*>(sig_off), o[5], 8, false}};
   for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
   const bool arena_pinned = is_pinned(bytes, blen);
-  for (int k = 0; k < K; ++k) {
-    const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K, c0 = blen * k / K, c1 = blen * (k + 1) / K;
+  const uint8_t* D = st.D;
+  const int parts = pool.parts();
+  std::vector<RecFront> fronts;
+  for (size_t k = 0; k + 1 < rb.size(); ++k) {
+    const uint64_t a0 = rb[k], a1 = rb[k + 1];
+    std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
+    std::vector<int> bad(parts, 0);
     pool.run([&](int t, int T) {
-      const uint64_t b0 = v0 + (v1 - v0) * t / T, b1 = v0 + (v1 - v0) * (t + 1) / T, m = b1 - b0;
-      if (m) {
-        for (const Arr& x : arr)
-          if (!x.pinned) std::memcpy(st.P + x.dst + x.elem * b0, x.src + x.elem * b0, x.elem * m);
-        for (uint64_t i = b0; i < b1; ++i) {
-          const uint64_t f[3][2] = {{id_off[i], id_len[i]}, {pay_off[i], pay_len[i]}, {sig_off[i], sig_len[i]}};
-          for (const auto& x : f) {
-            if (x[0] + x[1] > bytes_len || x[0] + x[1] < x[0] || (x[1] && !bytes)) {
-              bad[t] = 1;
-              return;
-            }
+      const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
+      uint64_t l = UINT64_MAX, h = 0;
+      for (uint64_t i = b0; i < b1; ++i) {
+        const uint64_t f[3][2] = {{id_off[i], id_len[i]}, {pay_off[i], pay_len[i]}, {sig_off[i], sig_len[i]}};
+        for (const auto& x : f) {
+          if (x[0] + x[1] > bytes_len || x[0] + x[1] < x[0] || (x[1] && !bytes)) {
+            bad[t] = 1;
+            return;
+          }
+          if (x[1]) {
+            l = std::min(l, x[0]);
+            h = std::max(h, x[0] + x[1]);
           }
         }
       }
-      const uint64_t d0 = c0 + (c1 - c0) * t / T, d1 = c0 + (c1 - c0) * (t + 1) / T;
-      if (d1 > d0 && !arena_pinned) std::memcpy(st.P + o[6] + d0, bytes + d0, d1 - d0);
+      lo[t] = l;
+      hi[t] = h;
     });
-    for (const Arr& x : arr) {
-      if (x.pinned) CHK(st.up_from(x.dst + x.elem * v0, x.src + x.elem * v0, x.elem * (v1 - v0)));
-      else CHK(st.up(x.dst + x.elem * v0, x.elem * (v1 - v0)));
+    uint64_t slo = UINT64_MAX, shi = 0;
+    for (int t = 0; t < parts; ++t) {
+      if (bad[t]) {
+        st.drain();
+        return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
+      }
+      slo = std::min(slo, lo[t]);
+      shi = std::max(shi, hi[t]);
     }
-    if (arena_pinned) CHK(st.up_from(o[6] + c0, bytes + c0, c1 - c0));
-    else CHK(st.up(o[6] + c0, c1 - c0));
+    CHK(stage_rows(st, pool, arr, 6, a0, a1));
+    if (slo < shi) CHK(stage_span(st, pool, bytes, arena_pinned, o[6], slo, shi));
+    HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
+    tr.mark("staged_" + std::to_string(k));
+    tr.ev("landed_" + std::to_string(k), c->copy);
+    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[6], reinterpret_cast<const uint64_t*>(D + o[5]) + a0, 1,
+                     reinterpret_cast<const uint32_t*>(D + o[2]) + a0, 1, fronts));
   }
-  tr.mark("rest_staged");
-  HIPCHK(hipEventRecord(c->ev_rest, c->copy));
-  tr.ev("rest_landed", c->copy);
   hipStream_t s = c->stream;
-  HIPCHK(hipStreamWaitEvent(s, c->ev_rest, 0));
-  const uint8_t* D = st.D;
+  HIPCHK(hipStreamWaitEvent(s, c->ev_up[rb.size() - 2], 0));
   const uint8_t* dbytes = D + o[6];
-  const uint64_t* did_off = reinterpret_cast<const uint64_t*>(D + o[4]);
+  const uint64_t* did_off = reinterpret_cast<const uint64_t*>(D + o[3]);
   uint8_t* ob = c->dev_out.as<uint8_t>();
   uint8_t* dstat = ob;
   uint8_t* daddr = out_addr ? ob + r1 : nullptr;
-  hlc::launch_verify_prehash(n, dbytes, reinterpret_cast<const uint64_t*>(D + o[5]),
-                             reinterpret_cast<const uint32_t*>(D + o[3]), reinterpret_cast<const uint32_t*>(D + o[1]),
-                             reinterpret_cast<const uint32_t*>(D + o[2]), c->kec_dig.as<uint32_t>(),
+  hlc::launch_verify_prehash(n, dbytes, reinterpret_cast<const uint64_t*>(D + o[4]),
+                             reinterpret_cast<const uint32_t*>(D + o[1]), reinterpret_cast<const uint32_t*>(D + o[2]),
+                             reinterpret_cast<const uint32_t*>(D + o[0]), c->kec_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), dstat, s);
   if (daddr) HIPCHK(hipMemsetAsync(daddr, 0, n * 20, s));
   for (const RecFront& f : fronts) {
@@ -1164,12 +1156,6 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   HIPCHK(hipEventRecord(c->ev_done, s));
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
-  for (int x : bad) {
-    if (x) {
-      st.drain();
-      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
-    }
-  }
   HIPCHK(hipEventSynchronize(c->ev_done));
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);

@@ -1,12 +1,13 @@
-"""The host-buffer entry hlc_validate_proposals (hlc_api.cpp validate_host: signatures staged and
-uploaded first as a dense array, the recovery's front half over two vote ranges on two streams, the
-other inputs in pieces behind them) equals the single-range schedule and the C oracle bit for bit:
+"""The host-buffer entry hlc_validate_proposals (hlc_api.cpp validate_host: the batch staged and
+uploaded in recovery ranges, each range's k_rec_prep + k_rec_main behind its upload on two streams in
+turn, the rest of the validation once every range has landed) equals the single-range schedule and
+the C oracle bit for bit:
 per-proposal results, per-vote statuses, scheme reasons and recovered addresses, on a Byzantine
 batch; also with empty proposals, votes no proposal covers (status 0xFF), proposals listed out of
 vote order, and an out-of-arena field -- a signature in the second range or another field in a late
 piece -- which returns HLC_EINVAL with the caller's outputs untouched (the device work already
-enqueued is drained and discarded).  Schedule knobs: HLC_SPLIT_VOTES (sizes of the recovery ranges
-before the last, "0" = one range), HLC_REST_PIECES."""
+enqueued is drained and discarded).  Schedule knob: HLC_SPLIT_VOTES (sizes of the recovery ranges
+before the last, "0" = one range)."""
 import ctypes
 import os
 
@@ -23,14 +24,12 @@ pytestmark = pytest.mark.gpu
 HLC_EINVAL = -1  # include/hlc.h
 
 
-def _run(engine, batch, desc, now, split, pieces=3):
+def _run(engine, batch, desc, now, split):
     os.environ["HLC_SPLIT_VOTES"] = str(split)
-    os.environ["HLC_REST_PIECES"] = str(pieces)
     try:
         return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
     finally:
         os.environ.pop("HLC_SPLIT_VOTES", None)
-        os.environ.pop("HLC_REST_PIECES", None)
 
 
 @pytest.fixture(scope="module")
@@ -40,12 +39,11 @@ def byz():
     return b, d, w.now
 
 
-@pytest.mark.parametrize("split,pieces", [("100", 3), ("240", 1), ("333", 7), ("100", 64), ("1", 2), ("0", 5),
-                                          ("64,128", 3), ("100,150,90", 2)])
-def test_gpu_host_entry_equals_single_range_and_oracle(engine, byz, split, pieces):
+@pytest.mark.parametrize("split", ["100", "240", "333", "1", "1,1,1,1", "64,128", "100,150,90", "32,32,32,32,32,32,32"])
+def test_gpu_host_entry_equals_single_range_and_oracle(engine, byz, split):
     b, d, now = byz
-    one = _run(engine, b, d, now, 0, 1)
-    got = _run(engine, b, d, now, split, pieces)
+    one = _run(engine, b, d, now, 0)
+    got = _run(engine, b, d, now, split)
     for x, y in zip(one, got):
         assert np.array_equal(x, y)
     cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
@@ -60,7 +58,7 @@ def test_gpu_host_entry_gaps_and_empty_proposals(engine, byz):
     d2["vote_count"][3] = 0            # an empty proposal (StillActive)
     d2["vote_count"][10] -= 5          # its last 5 votes are covered by no proposal
     d2["vote_count"][25] = 0
-    one = _run(engine, b, d2, now, 0, 1)
+    one = _run(engine, b, d2, now, 0)
     got = _run(engine, b, d2, now, 100)
     for x, y in zip(one, got):
         assert np.array_equal(x, y)
@@ -73,7 +71,7 @@ def test_gpu_host_entry_gaps_and_empty_proposals(engine, byz):
 def test_gpu_host_entry_out_of_order_proposals(engine, byz):
     b, d, now = byz
     d2 = d[::-1].copy()  # proposals listed in reverse vote order
-    one = _run(engine, b, d2, now, 0, 1)
+    one = _run(engine, b, d2, now, 0)
     got = _run(engine, b, d2, now, 100)
     for x, y in zip(one, got):
         assert np.array_equal(x, y)
@@ -113,7 +111,7 @@ def test_gpu_host_entry_rejects_bad_field_outputs_untouched(engine, byz, field, 
     for o in outs:
         assert (o == 0xAB).all(), "outputs were written on error"
     ok = _run(engine, b, d, now, 100)  # the context is still usable
-    assert np.array_equal(ok[1], _run(engine, b, d, now, 0, 1)[1])
+    assert np.array_equal(ok[1], _run(engine, b, d, now, 0)[1])
 
 
 def test_gpu_host_entry_pinned_inputs(engine, byz):

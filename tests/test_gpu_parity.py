@@ -142,21 +142,19 @@ def test_gpu_verify_batch_sizes(engine):
         assert [a.tobytes() for a in addr] == exp_addr[:n], n
 
 
-@pytest.mark.parametrize("split,pieces", [("0", 1), ("100", 3), ("700", 5), ("1", 64), ("200,300", 2)])
-def test_gpu_verify_batch_split_schedules(engine, split, pieces):
-    """hlc_eth_verify_batch stages the signatures first and recovers them in two ranges on two
-    streams in turn (HLC_SPLIT_VOTES: the sizes of the ranges before the last), the identities / payloads / arena in
-    HLC_REST_PIECES pieces: every schedule equals the oracle item for item (payloads of 0..299 bytes:
-    1-3 digit EIP-191 lengths, 1-3 keccak blocks)."""
+@pytest.mark.parametrize("split", ["0", "100", "700", "1", "200,300", "1,1,64"])
+def test_gpu_verify_batch_split_schedules(engine, split):
+    """hlc_eth_verify_batch stages the items in recovery ranges (HLC_SPLIT_VOTES: the sizes of the
+    ranges before the last), each range's k_rec_prep + k_rec_main behind its upload on two streams in
+    turn: every schedule equals the oracle item for item (payloads of 0..299 bytes: 1-3 digit
+    EIP-191 lengths, 1-3 keccak blocks)."""
     ids, pays, sigs = _mutated_items(1500, 11)
     exp_st, exp_addr = _oracle_verify(ids, pays, sigs)
-    os.environ["HLC_SPLIT_VOTES"] = str(split)
-    os.environ["HLC_REST_PIECES"] = str(pieces)
+    os.environ["HLC_SPLIT_VOTES"] = split
     try:
         st, addr = engine.eth_verify_batch(ids, pays, sigs)
     finally:
         os.environ.pop("HLC_SPLIT_VOTES", None)
-        os.environ.pop("HLC_REST_PIECES", None)
     assert [int(x) for x in st] == exp_st
     assert [a.tobytes() for a in addr] == exp_addr
 

@@ -1,12 +1,12 @@
 """The host-buffer entry hlc_validate_proposals (what the Rust process_incoming_proposals of
 INTEGRATION.md calls) on the config-2 workload (GPU box).
 
-For each setting of the split-recovery schedule (hlc_api.cpp validate_host: HLC_SPLIT_VOTES,
-HLC_REST_PIECES, HLC_HOST_THREADS, read on every call): outputs equal the first setting's bit for
+For each setting of the range schedule (hlc_api.cpp validate_host: HLC_SPLIT_VOTES, HLC_HOST_THREADS,
+read on every call): outputs equal the first setting's bit for
 bit, then --steps calls are timed (host buffers in, per-vote statuses + per-proposal results out,
 blocking).
 
-    python tools/host_pipe.py --steps 10 --split 0/131072/131072,196608 --pieces 1,3 --threads 4,8 --rounds 2
+    python tools/host_pipe.py --steps 10 --split 0/131072/131072,196608 --threads 4,8 --rounds 2
     (HLC_HOST_TRACE=1 in the environment adds each call's timeline on stderr)
     python tools/host_pipe.py --print-trace gpurun_out/trace.txt   (that timeline as a table; no GPU)
 """
@@ -37,7 +37,6 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--split", default="131072,196608", help="'/'-separated HLC_SPLIT_VOTES settings (range sizes "
                     "before the last, e.g. 131072,196608/0; 0 = one recovery range)")
-    ap.add_argument("--pieces", default="3", help="HLC_REST_PIECES settings")
     ap.add_argument("--threads", default="4", help="HLC_HOST_THREADS settings")
     ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
     ap.add_argument("--proposals", type=int, default=10_000)
@@ -63,11 +62,9 @@ def main() -> int:
     bytes_in = int(b.arena.nbytes + b.vote_id.nbytes + b.proposal_id.nbytes + b.timestamp.nbytes + b.vote.nbytes
                    + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
     ref = None
-    settings = [(sp, pc, th) for sp in a.split.split("/") for pc in a.pieces.split(",")
-                for th in a.threads.split(",")] * max(1, a.rounds)
-    for sp, pc, th in settings:
+    settings = [(sp, th) for sp in a.split.split("/") for th in a.threads.split(",")] * max(1, a.rounds)
+    for sp, th in settings:
         os.environ["HLC_SPLIT_VOTES"] = sp
-        os.environ["HLC_REST_PIECES"] = pc
         os.environ["HLC_HOST_THREADS"] = th
         r = eng.validate_proposals(b, d, db.now, want_votes=True)
         if ref is None:
@@ -78,7 +75,7 @@ def main() -> int:
         for _ in range(a.steps):
             eng.validate_proposals(b, d, db.now, want_votes=True)
         el = (time.perf_counter() - t) / a.steps
-        row = {"split": sp, "rest_pieces": int(pc), "threads": int(th), "pinned": a.pinned, "ms_per_call": el * 1e3,
+        row = {"split": sp, "threads": int(th), "pinned": a.pinned, "ms_per_call": el * 1e3,
                "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in, "outputs_equal_first_setting": True}
         print(json.dumps(row), flush=True)
     eng.close()
