@@ -872,14 +872,17 @@ struct Arr {
   bool pinned;
 };
 
-// Items [a0, a1) of the arrays: staging copies of the pageable ones, then the uploads (the pinned
-// ones straight from the caller).
-int stage_rows(Staging& st, HostPool& pool, Arr* arr, int na, uint64_t a0, uint64_t a1) {
+// Items [a0, a1) of the arrays: staging copies of the pageable ones (and per part, `also`(part,
+// b0, b1) right after its copies, while the rows are in cache: the callers' field checks), then the
+// uploads (the pinned ones straight from the caller).
+int stage_rows(Staging& st, HostPool& pool, Arr* arr, int na, uint64_t a0, uint64_t a1,
+               const std::function<void(int, uint64_t, uint64_t)>& also = nullptr) {
   pool.run([&](int t, int T) {
     const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
     for (int q = 0; q < na; ++q)
       if (!arr[q].pinned && b1 > b0)
         std::memcpy(st.P + arr[q].dst + arr[q].elem * b0, arr[q].src + arr[q].elem * b0, arr[q].elem * (b1 - b0));
+    if (also) also(t, b0, b1);
   });
   for (int q = 0; q < na; ++q) {
     const size_t off = arr[q].elem * a0, len = arr[q].elem * (a1 - a0);
@@ -969,11 +972,12 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   CHK(stage_rows(st, pool, &parr, 1, 0, np));
   for (size_t k = 0; k + 1 < rb.size(); ++k) {
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
-    // field checks and the range's arena span (the SoA rows' staging copies ride along)
+    // the SoA rows' staging copies, with the field checks and the range's arena span riding along
+    // (the uploads of the rows are enqueued before the checks' verdict: a bad field is reported
+    // before anything reaches the caller's outputs, and the enqueued work is drained)
     std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
     std::vector<int> bad(parts, 0);
-    pool.run([&](int t, int T) {
-      const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
+    CHK(stage_rows(st, pool, arr, 6, a0, a1, [&](int t, uint64_t b0, uint64_t b1) {
       uint64_t l = UINT64_MAX, h = 0;
       for (uint64_t i = b0 * HLC_NFIELDS; i < b1 * HLC_NFIELDS; ++i) {
         const uint64_t off = v->field_off[i], len = v->field_len[i];
@@ -987,7 +991,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
       }
       lo[t] = l;
       hi[t] = h;
-    });
+    }));
     uint64_t slo = UINT64_MAX, shi = 0;
     for (int t = 0; t < parts; ++t) {
       if (bad[t]) {
@@ -997,7 +1001,6 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
       slo = std::min(slo, lo[t]);
       shi = std::max(shi, hi[t]);
     }
-    CHK(stage_rows(st, pool, arr, 6, a0, a1));
     if (slo < shi) CHK(stage_span(st, pool, v->bytes, arena_pinned, o[7], slo, shi));
     HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
     tr.mark("staged_" + std::to_string(k));
@@ -1096,8 +1099,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
     std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
     std::vector<int> bad(parts, 0);
-    pool.run([&](int t, int T) {
-      const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
+    CHK(stage_rows(st, pool, arr, 6, a0, a1, [&](int t, uint64_t b0, uint64_t b1) {
       uint64_t l = UINT64_MAX, h = 0;
       for (uint64_t i = b0; i < b1; ++i) {
         const uint64_t f[3][2] = {{id_off[i], id_len[i]}, {pay_off[i], pay_len[i]}, {sig_off[i], sig_len[i]}};
@@ -1114,7 +1116,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
       }
       lo[t] = l;
       hi[t] = h;
-    });
+    }));
     uint64_t slo = UINT64_MAX, shi = 0;
     for (int t = 0; t < parts; ++t) {
       if (bad[t]) {
@@ -1124,7 +1126,6 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
       slo = std::min(slo, lo[t]);
       shi = std::max(shi, hi[t]);
     }
-    CHK(stage_rows(st, pool, arr, 6, a0, a1));
     if (slo < shi) CHK(stage_span(st, pool, bytes, arena_pinned, o[6], slo, shi));
     HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
     tr.mark("staged_" + std::to_string(k));
