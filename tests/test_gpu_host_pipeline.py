@@ -131,3 +131,66 @@ def test_gpu_host_entry_pinned_inputs(engine, byz):
     cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
     assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
     assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec)
+
+
+def test_gpu_host_entry_arena_layouts(engine, byz):
+    """Arena layouts the range spans must handle: fields of late votes placed first in the arena
+    (the first range's span covers almost all of it), votes sharing the same bytes (overlapping
+    spans across ranges), and unused garbage around the fields -- all equal the packed layout."""
+    b, d, now = byz
+    ref = _run(engine, b, d, now, "0")
+    n = b.n
+    # reversed: vote i's fields move to the mirrored position of the arena
+    order = np.arange(n)[::-1]
+    chunks, off, pos = [], np.zeros_like(b.field_off), 0
+    junk = np.frombuffer(bytes(range(256)) * 4, np.uint8)
+    for i in order:
+        for f in range(5):
+            ln = int(b.field_len[i, f])
+            src = b.arena[int(b.field_off[i, f]):int(b.field_off[i, f]) + ln]
+            chunks.append(src)
+            off[i, f] = pos
+            pos += ln
+        chunks.append(junk[: (i * 7) % 97])  # garbage between votes
+        pos += (i * 7) % 97
+    arena = np.concatenate(chunks).astype(np.uint8) if chunks else np.zeros(0, np.uint8)
+    rev = b.__class__(b.vote_id, b.proposal_id, b.timestamp, b.vote, arena, off, b.field_len)
+    for split in ("100", "64,128"):
+        got = _run(engine, rev, d, now, split)
+        for x, y in zip(ref, got):
+            assert np.array_equal(x, y), split
+    # shared bytes: every vote's owner field points at the first vote's owner bytes (an arena region
+    # read by every range); only the owners change, so compare with the oracle
+    off2 = b.field_off.copy()
+    off2[:, 0] = b.field_off[0, 0]
+    ln2 = b.field_len.copy()
+    ln2[:, 0] = b.field_len[0, 0]
+    shared = b.__class__(b.vote_id, b.proposal_id, b.timestamp, b.vote, b.arena, off2, ln2)
+    got = _run(engine, shared, d, now, "100")
+    one = _run(engine, shared, d, now, "0")
+    for x, y in zip(one, got):
+        assert np.array_equal(x, y)
+    cres, cvst, _, _ = coracle.validate_proposals(shared, d, now, threads=8)
+    assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
+
+
+def test_gpu_host_entry_no_votes(engine):
+    """Proposals with no votes at all (an empty batch, no arena): every proposal StillActive, as
+    initialize_with_votes on an empty list (session.rs:266-268) -- through the host entry."""
+    from hashgraph_like_consensus import _ffi as ffi
+    from hashgraph_like_consensus.batch import VoteBatch
+    d = np.zeros(3, ffi.PROPOSAL_DTYPE)
+    d["proposal_id"] = [1, 2, 3]
+    d["timestamp"] = 1_760_000_000
+    d["expiration_timestamp"] = 1_760_003_600
+    d["expected_voters_count"] = 3
+    d["max_rounds"] = 2
+    d["consensus_threshold"] = 2 / 3
+    d["use_gossipsub_rounds"] = 1
+    e = np.zeros(0, np.uint32)
+    b = VoteBatch(e, e.copy(), np.zeros(0, np.uint64), np.zeros(0, np.uint8), np.zeros(0, np.uint8),
+                  np.zeros((0, 5), np.uint64), np.zeros((0, 5), np.uint32))
+    res, _, _, _ = engine.validate_proposals(b, d, 1_760_001_800, want_votes=True)
+    cres, _, _, _ = coracle.validate_proposals(b, d, 1_760_001_800, threads=1)
+    assert np.array_equal(res, cres)
+    assert (res["status"] == 0).all() and (res["transition"] == 0).all()
