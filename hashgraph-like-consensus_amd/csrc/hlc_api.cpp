@@ -170,7 +170,7 @@ struct hlc_ctx {
   PBuf pin_in, pin_out;
   DBuf dev_in, dev_out;
   std::vector<hipEvent_t> ev_up, ev_main;  // per recovery range: inputs landed, main stage done
-  hipEvent_t ev_done = nullptr;
+  hipEvent_t ev_rest = nullptr, ev_done = nullptr;
   std::unique_ptr<HostPool> pool;  // staging workers (HLC_HOST_THREADS)
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
@@ -199,7 +199,8 @@ struct hlc_ctx {
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : ev_up) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_main) (void)hipEventDestroy(e);
-    if (ev_done) (void)hipEventDestroy(ev_done);
+    for (hipEvent_t e : {ev_rest, ev_done})
+      if (e) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -753,7 +754,8 @@ int host_resources(hlc_ctx* c) {
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   if (!c->copy) HIPCHK(hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, greatest));
   if (!c->aux2) HIPCHK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, least));
-  if (!c->ev_done) HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+  for (hipEvent_t* e : {&c->ev_rest, &c->ev_done})
+    if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   if (!c->pool || c->pool->parts() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
   CHK(ensure_recover_scratch(c));
   CHK(c->rec_scratch2.ensure(c->rec_lanes * hlc::recover_scratch_words() * sizeof(uint32_t)));
@@ -904,22 +906,67 @@ int stage_span(Staging& st, HostPool& pool, const uint8_t* bytes, bool pinned, s
   return st.up(o_arena + lo, hi - lo);
 }
 
+// Pieces the inputs other than the signatures are staged and uploaded in (HLC_REST_PIECES, default 3):
+// piece k+1 is copied into page-locked memory while piece k's DMA runs.
+int rest_pieces() {
+  const char* e = std::getenv("HLC_REST_PIECES");
+  const int k = e ? std::atoi(e) : 3;
+  return std::max(1, std::min(k, 64));
+}
+
+// The signatures of items [a0, a1) (sig_off / sig_len with stride `stride`) gathered by the host
+// pool into the dense staging array at o_sig (65 B per item; slots of other lengths left as they
+// are) and their lengths at o_len, then uploaded.  false (nothing read) when a 65-byte signature
+// lies outside the arena.
+bool stage_sigs(Staging& st, HostPool& pool, const uint8_t* bytes, uint64_t bytes_len, const uint64_t* sig_off,
+                const uint32_t* sig_len, size_t stride, size_t o_sig, size_t o_len, uint64_t a0, uint64_t a1,
+                int* rc) {
+  const uint64_t m = a1 - a0;
+  std::vector<int> bad(pool.parts(), 0);
+  pool.run([&](int t, int T) {
+    const uint64_t b0 = a0 + m * t / T, b1 = a0 + m * (t + 1) / T;
+    uint8_t* sg = st.P + o_sig;
+    uint32_t* sl = reinterpret_cast<uint32_t*>(st.P + o_len);
+    for (uint64_t i = b0; i < b1; ++i) {
+      const uint64_t off = sig_off[i * stride];
+      const uint32_t len = sig_len[i * stride];
+      sl[i] = len;
+      if (len != 65) continue;  // the prep stage skips it (a length error decided elsewhere)
+      if (!bytes || off + 65 > bytes_len || off + 65 < off) {
+        bad[t] = 1;
+        return;
+      }
+      std::memcpy(sg + 65 * i, bytes + off, 65);
+    }
+  });
+  for (int x : bad)
+    if (x) return false;
+  *rc = st.up(o_sig + 65 * a0, 65 * m);
+  if (*rc == 0) *rc = st.up(o_len + 4 * a0, 4 * m);
+  return true;
+}
+
 // hlc_validate_proposals over host buffers (what INTEGRATION.md's process_incoming_proposals calls).
-// The batch goes to the device in the recovery ranges of split_ranges(n) (small ones first) on the
-// context's upload stream: for range k the host pool copies the votes' SoA rows into page-locked
-// staging (checking every field's (offset, length) on the way and finding the arena span the
-// range's fields use), then that span; each is uploaded as soon as it is staged, and range k's
-// k_rec_prep + k_rec_main are enqueued behind its upload, on the two aux streams in turn (each with
-// its own per-lane scratch), so range k's k_rec_main waves take the SIMD slots range k-1's waves free
-// (one grid tail per call, as in the device-resident call) while the host stages range k+1.  Once
-// the last range has landed, the launch stream runs the prehash and chain kernels over the whole
-// batch, each range's finish (u1 G, Z^-1, address) after its main stage, the statuses, tables and
-// finalize, and one D2H of every output into page-locked memory.  An array the caller holds in
-// page-locked memory (hlc_host_alloc) is uploaded straight from there.  A field outside the arena
-// returns HLC_EINVAL before anything reaches the caller's outputs (device work already enqueued is
-// drained and discarded).  Only stream / event dependencies order the stages: no kernel waits on a
-// flag, so any mapping of the streams onto hardware queues is correct (one that serialises them is
-// only slower).
+// The caller's votes go to the device through page-locked staging on the context's upload stream,
+// ordered by what the kernels need first, so that the VALU-bound recovery starts long before the
+// whole batch has landed:
+//   1. per recovery range of split_ranges(n) (small ones first), the votes' signatures gathered
+//      into a dense array (65 B per vote) with their lengths; behind each range's upload, its
+//      k_rec_prep + k_rec_main on the two aux streams in turn (each with its own per-lane scratch),
+//      so range k's grid waves take the SIMD slots range k-1's waves free (one grid tail per call,
+//      as in the device-resident call), and every range's signatures are on the device after
+//      ~69 B per vote of DMA;
+//   2. every other input (SoA arrays, proposals, the byte arena) in rest_pieces() pieces, each
+//      copied into page-locked memory by the host pool (every field's (offset, length) checked on
+//      the way) while the previous piece's DMA runs -> once they have landed, the prehash, chain /
+//      duplicate / YES kernels on the launch stream, each range's finish (u1 G, Z^-1, address) after
+//      its main stage, the statuses, tables, finalize, and one D2H of every output into page-locked
+//      memory.
+// An array the caller holds in page-locked memory (hlc_host_alloc) is uploaded straight from there
+// (the signatures are still gathered).  A field outside the arena returns HLC_EINVAL before anything
+// reaches the caller's outputs (device work already enqueued is drained and discarded).  Only
+// stream / event dependencies order the stages: no kernel waits on a flag, so any mapping of the
+// streams onto hardware queues is correct (one that serialises them is only slower).
 int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
                   hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec) {
   const uint64_t n = v->n;
@@ -929,18 +976,20 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   HostTrace tr;
   if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
   tr.start(c->copy);
-  // inputs, page-locked and on the device alike: vote_id | proposal_id | timestamp | vote |
-  // field_off | field_len | proposals | arena
-  size_t o[9];
+  // inputs, page-locked and on the device alike: dense signatures | signature lengths | vote_id |
+  // proposal_id | timestamp | vote | field_off | field_len | proposals | arena
+  size_t o[11];
   o[0] = 0;
-  o[1] = o[0] + al256(n * 4);
+  o[1] = o[0] + al256(n * 65);
   o[2] = o[1] + al256(n * 4);
-  o[3] = o[2] + al256(n * 8);
-  o[4] = o[3] + al256(n);
-  o[5] = o[4] + al256(n * 8 * HLC_NFIELDS);
-  o[6] = o[5] + al256(n * 4 * HLC_NFIELDS);
-  o[7] = o[6] + al256(np * sizeof(hlc_proposal));
-  o[8] = o[7] + blen;
+  o[3] = o[2] + al256(n * 4);
+  o[4] = o[3] + al256(n * 4);
+  o[5] = o[4] + al256(n * 8);
+  o[6] = o[5] + al256(n);
+  o[7] = o[6] + al256(n * 8 * HLC_NFIELDS);
+  o[8] = o[7] + al256(n * 4 * HLC_NFIELDS);
+  o[9] = o[8] + al256(np * sizeof(hlc_proposal));
+  o[10] = o[9] + blen;
   // outputs: results | status | reason | recovered
   size_t r[5];
   r[0] = 0;
@@ -948,83 +997,77 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   r[2] = r[1] + al256(n + 1);
   r[3] = r[2] + al256(n + 1);
   r[4] = r[3] + (out_rec ? al256(n * 20 + 20) : 0);
-  CHK(c->pin_in.ensure(o[8] + 16));
-  CHK(c->dev_in.ensure(o[8] + 16));
+  CHK(c->pin_in.ensure(o[10] + 16));
+  CHK(c->dev_in.ensure(o[10] + 16));
   CHK(c->pin_out.ensure(r[4] + 16));
   CHK(c->dev_out.ensure(r[4] + 16));
   CHK(reserve_validate(c, n, np));
   std::vector<uint64_t> rb;
   CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
-  Arr arr[6] = {{reinterpret_cast<const uint8_t*>(v->vote_id), o[0], 4, false},
-                {reinterpret_cast<const uint8_t*>(v->proposal_id), o[1], 4, false},
-                {reinterpret_cast<const uint8_t*>(v->timestamp), o[2], 8, false},
-                {v->vote, o[3], 1, false},
-                {reinterpret_cast<const uint8_t*>(v->field_off), o[4], 8 * HLC_NFIELDS, false},
-                {reinterpret_cast<const uint8_t*>(v->field_len), o[5], 4 * HLC_NFIELDS, false}};
-  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
-  Arr parr{reinterpret_cast<const uint8_t*>(props), o[6], sizeof(hlc_proposal), false};
-  parr.pinned = is_pinned(props, np * sizeof(hlc_proposal));
-  const bool arena_pinned = is_pinned(v->bytes, blen);
   const uint8_t* D = st.D;
   const int parts = pool.parts();
   std::vector<RecFront> fronts;
-  CHK(stage_rows(st, pool, &parr, 1, 0, np));
   for (size_t k = 0; k + 1 < rb.size(); ++k) {
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
-    // the SoA rows' staging copies, with the field checks and the range's arena span riding along
-    // (the uploads of the rows are enqueued before the checks' verdict: a bad field is reported
-    // before anything reaches the caller's outputs, and the enqueued work is drained)
-    std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
-    std::vector<int> bad(parts, 0);
-    CHK(stage_rows(st, pool, arr, 6, a0, a1, [&](int t, uint64_t b0, uint64_t b1) {
-      uint64_t l = UINT64_MAX, h = 0;
+    int rc = 0;
+    if (!stage_sigs(st, pool, v->bytes, v->bytes_len, v->field_off + HLC_F_SIGNATURE, v->field_len + HLC_F_SIGNATURE,
+                    HLC_NFIELDS, o[0], o[1], a0, a1, &rc)) {
+      st.drain();
+      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+    }
+    CHK(rc);
+    HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
+    tr.mark("sigs_staged_" + std::to_string(k));
+    tr.ev("sigs_landed_" + std::to_string(k), c->copy);
+    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[0] + 65 * a0, nullptr, 0,
+                     reinterpret_cast<const uint32_t*>(D + o[1]) + a0, 1, fronts));
+  }
+  // everything else, piece by piece; the field checks ride along with the rows' staging copies
+  Arr arr[6] = {{reinterpret_cast<const uint8_t*>(v->vote_id), o[2], 4, false},
+                {reinterpret_cast<const uint8_t*>(v->proposal_id), o[3], 4, false},
+                {reinterpret_cast<const uint8_t*>(v->timestamp), o[4], 8, false},
+                {v->vote, o[5], 1, false},
+                {reinterpret_cast<const uint8_t*>(v->field_off), o[6], 8 * HLC_NFIELDS, false},
+                {reinterpret_cast<const uint8_t*>(v->field_len), o[7], 4 * HLC_NFIELDS, false}};
+  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
+  Arr parr{reinterpret_cast<const uint8_t*>(props), o[8], sizeof(hlc_proposal), false};
+  parr.pinned = is_pinned(props, np * sizeof(hlc_proposal));
+  const bool arena_pinned = is_pinned(v->bytes, blen);
+  CHK(stage_rows(st, pool, &parr, 1, 0, np));
+  std::vector<int> bad(parts, 0);
+  const int K = rest_pieces();
+  for (int k = 0; k < K; ++k) {
+    const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K;
+    CHK(stage_rows(st, pool, arr, 6, v0, v1, [&](int t, uint64_t b0, uint64_t b1) {
       for (uint64_t i = b0 * HLC_NFIELDS; i < b1 * HLC_NFIELDS; ++i) {
         const uint64_t off = v->field_off[i], len = v->field_len[i];
-        if (!len) continue;
-        if (!v->bytes || off + len > v->bytes_len || off + len < off) {
+        if (len && (!v->bytes || off + len > v->bytes_len || off + len < off)) {
           bad[t] = 1;
           return;
         }
-        l = std::min(l, off);
-        h = std::max(h, off + len);
       }
-      lo[t] = l;
-      hi[t] = h;
     }));
-    uint64_t slo = UINT64_MAX, shi = 0;
-    for (int t = 0; t < parts; ++t) {
-      if (bad[t]) {
-        st.drain();
-        return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-      }
-      slo = std::min(slo, lo[t]);
-      shi = std::max(shi, hi[t]);
-    }
-    if (slo < shi) CHK(stage_span(st, pool, v->bytes, arena_pinned, o[7], slo, shi));
-    HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
-    tr.mark("staged_" + std::to_string(k));
-    tr.ev("landed_" + std::to_string(k), c->copy);
-    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[7],
-                     reinterpret_cast<const uint64_t*>(D + o[4]) + a0 * HLC_NFIELDS + HLC_F_SIGNATURE, HLC_NFIELDS,
-                     reinterpret_cast<const uint32_t*>(D + o[5]) + a0 * HLC_NFIELDS + HLC_F_SIGNATURE, HLC_NFIELDS,
-                     fronts));
+    CHK(stage_span(st, pool, v->bytes, arena_pinned, o[9], blen * k / K, blen * (k + 1) / K));
   }
-  // the validation on the launch stream, once every range has landed (the upload stream is in order)
+  tr.mark("rest_staged");
+  HIPCHK(hipEventRecord(c->ev_rest, c->copy));
+  tr.ev("rest_landed", c->copy);
+  // the validation on the launch stream, the recovery ranges joined in by their events
   hipStream_t s = c->stream;
-  HIPCHK(hipStreamWaitEvent(s, c->ev_up[rb.size() - 2], 0));  // split_ranges gives >= 1 range
+  HIPCHK(hipStreamWaitEvent(s, c->ev_rest, 0));
   hlc_votes dv;
   dv.n = n;
-  dv.vote_id = reinterpret_cast<const uint32_t*>(D + o[0]);
-  dv.proposal_id = reinterpret_cast<const uint32_t*>(D + o[1]);
-  dv.timestamp = reinterpret_cast<const uint64_t*>(D + o[2]);
-  dv.vote = D + o[3];
-  dv.field_off = reinterpret_cast<const uint64_t*>(D + o[4]);
-  dv.field_len = reinterpret_cast<const uint32_t*>(D + o[5]);
-  dv.bytes = D + o[7];
+  dv.vote_id = reinterpret_cast<const uint32_t*>(D + o[2]);
+  dv.proposal_id = reinterpret_cast<const uint32_t*>(D + o[3]);
+  dv.timestamp = reinterpret_cast<const uint64_t*>(D + o[4]);
+  dv.vote = D + o[5];
+  dv.field_off = reinterpret_cast<const uint64_t*>(D + o[6]);
+  dv.field_len = reinterpret_cast<const uint32_t*>(D + o[7]);
+  dv.bytes = D + o[9];
   dv.bytes_len = blen;
   uint8_t* ob = c->dev_out.as<uint8_t>();
-  CHK(validate_device(c, &dv, reinterpret_cast<const hlc_proposal*>(D + o[6]), np, now,
+  CHK(validate_device(c, &dv, reinterpret_cast<const hlc_proposal*>(D + o[8]), np, now,
                       reinterpret_cast<hlc_result*>(ob + r[0]), ob + r[1], ob + r[2], out_rec ? ob + r[3] : nullptr, s,
                       fronts.data(), (int)fronts.size()));
   tr.ev("kernels_end", s);
@@ -1032,6 +1075,12 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   HIPCHK(hipEventRecord(c->ev_done, s));
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
+  for (int x : bad) {
+    if (x) {
+      st.drain();
+      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+    }
+  }
   HIPCHK(hipEventSynchronize(c->ev_done));
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);
@@ -1048,11 +1097,11 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   return 0;
 }
 
-// hlc_eth_verify_batch over host buffers: the same schedule as validate_host -- the items in
-// recovery ranges (per-item offset / length rows and the range's arena span, staged unless
-// page-locked), each range's k_rec_prep + k_rec_main behind its upload on the aux streams in turn --
-// with the verify byte stage (length checks + EIP-191 keccak of each payload, k_verify_prehash) on the
-// launch stream once every range has landed, each range's finish after its main stage, one D2H of
+// hlc_eth_verify_batch over host buffers: the same schedule as validate_host -- the signatures
+// first (dense, per recovery range, each range's k_rec_prep + k_rec_main behind its upload on the aux
+// streams in turn), then the per-item offsets / lengths and the arena in pieces, field checks on the
+// way -- with the verify byte stage (length checks + EIP-191 keccak of each payload, k_verify_prehash)
+// on the launch stream once they have landed, each range's finish after its main stage, one D2H of
 // the statuses (and addresses).  An (offset, length) outside the arena returns HLC_EINVAL before
 // anything reaches the caller's outputs.
 int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len, const uint64_t* id_off,
@@ -1064,13 +1113,14 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   HostTrace tr;
   if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
   tr.start(c->copy);
-  // inputs: identity / payload / signature lengths | their offsets | arena
+  // inputs: dense signatures | signature lengths | identity / payload lengths | identity / payload
+  // offsets | arena
   size_t o[8];
   o[0] = 0;
-  o[1] = o[0] + al256(n * 4);
+  o[1] = o[0] + al256(n * 65);
   o[2] = o[1] + al256(n * 4);
   o[3] = o[2] + al256(n * 4);
-  o[4] = o[3] + al256(n * 8);
+  o[4] = o[3] + al256(n * 4);
   o[5] = o[4] + al256(n * 8);
   o[6] = o[5] + al256(n * 8);
   o[7] = o[6] + blen;
@@ -1084,23 +1134,34 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   std::vector<uint64_t> rb;
   CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
-  Arr arr[6] = {{reinterpret_cast<const uint8_t*>(id_len), o[0], 4, false},
-                {reinterpret_cast<const uint8_t*>(pay_len), o[1], 4, false},
-                {reinterpret_cast<const uint8_t*>(sig_len), o[2], 4, false},
-                {reinterpret_cast<const uint8_t*>(id_off), o[3], 8, false},
-                {reinterpret_cast<const uint8_t*>(pay_off), o[4], 8, false},
-                {reinterpret_cast<const uint8_t*>(sig_off), o[5], 8, false}};
-  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
-  const bool arena_pinned = is_pinned(bytes, blen);
   const uint8_t* D = st.D;
   const int parts = pool.parts();
   std::vector<RecFront> fronts;
   for (size_t k = 0; k + 1 < rb.size(); ++k) {
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
-    std::vector<uint64_t> lo(parts, UINT64_MAX), hi(parts, 0);
-    std::vector<int> bad(parts, 0);
-    CHK(stage_rows(st, pool, arr, 6, a0, a1, [&](int t, uint64_t b0, uint64_t b1) {
-      uint64_t l = UINT64_MAX, h = 0;
+    int rc = 0;
+    if (!stage_sigs(st, pool, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], a0, a1, &rc)) {
+      st.drain();
+      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
+    }
+    CHK(rc);
+    HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
+    tr.mark("sigs_staged_" + std::to_string(k));
+    tr.ev("sigs_landed_" + std::to_string(k), c->copy);
+    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[0] + 65 * a0, nullptr, 0,
+                     reinterpret_cast<const uint32_t*>(D + o[1]) + a0, 1, fronts));
+  }
+  Arr arr[4] = {{reinterpret_cast<const uint8_t*>(id_len), o[2], 4, false},
+                {reinterpret_cast<const uint8_t*>(pay_len), o[3], 4, false},
+                {reinterpret_cast<const uint8_t*>(id_off), o[4], 8, false},
+                {reinterpret_cast<const uint8_t*>(pay_off), o[5], 8, false}};
+  for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
+  const bool arena_pinned = is_pinned(bytes, blen);
+  std::vector<int> bad(parts, 0);
+  const int K = rest_pieces();
+  for (int k = 0; k < K; ++k) {
+    const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K;
+    CHK(stage_rows(st, pool, arr, 4, v0, v1, [&](int t, uint64_t b0, uint64_t b1) {
       for (uint64_t i = b0; i < b1; ++i) {
         const uint64_t f[3][2] = {{id_off[i], id_len[i]}, {pay_off[i], pay_len[i]}, {sig_off[i], sig_len[i]}};
         for (const auto& x : f) {
@@ -1108,41 +1169,24 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
             bad[t] = 1;
             return;
           }
-          if (x[1]) {
-            l = std::min(l, x[0]);
-            h = std::max(h, x[0] + x[1]);
-          }
         }
       }
-      lo[t] = l;
-      hi[t] = h;
     }));
-    uint64_t slo = UINT64_MAX, shi = 0;
-    for (int t = 0; t < parts; ++t) {
-      if (bad[t]) {
-        st.drain();
-        return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
-      }
-      slo = std::min(slo, lo[t]);
-      shi = std::max(shi, hi[t]);
-    }
-    if (slo < shi) CHK(stage_span(st, pool, bytes, arena_pinned, o[6], slo, shi));
-    HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
-    tr.mark("staged_" + std::to_string(k));
-    tr.ev("landed_" + std::to_string(k), c->copy);
-    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[6], reinterpret_cast<const uint64_t*>(D + o[5]) + a0, 1,
-                     reinterpret_cast<const uint32_t*>(D + o[2]) + a0, 1, fronts));
+    CHK(stage_span(st, pool, bytes, arena_pinned, o[6], blen * k / K, blen * (k + 1) / K));
   }
+  tr.mark("rest_staged");
+  HIPCHK(hipEventRecord(c->ev_rest, c->copy));
+  tr.ev("rest_landed", c->copy);
   hipStream_t s = c->stream;
-  HIPCHK(hipStreamWaitEvent(s, c->ev_up[rb.size() - 2], 0));
+  HIPCHK(hipStreamWaitEvent(s, c->ev_rest, 0));
   const uint8_t* dbytes = D + o[6];
-  const uint64_t* did_off = reinterpret_cast<const uint64_t*>(D + o[3]);
+  const uint64_t* did_off = reinterpret_cast<const uint64_t*>(D + o[4]);
   uint8_t* ob = c->dev_out.as<uint8_t>();
   uint8_t* dstat = ob;
   uint8_t* daddr = out_addr ? ob + r1 : nullptr;
-  hlc::launch_verify_prehash(n, dbytes, reinterpret_cast<const uint64_t*>(D + o[4]),
-                             reinterpret_cast<const uint32_t*>(D + o[1]), reinterpret_cast<const uint32_t*>(D + o[2]),
-                             reinterpret_cast<const uint32_t*>(D + o[0]), c->kec_dig.as<uint32_t>(),
+  hlc::launch_verify_prehash(n, dbytes, reinterpret_cast<const uint64_t*>(D + o[5]),
+                             reinterpret_cast<const uint32_t*>(D + o[3]), reinterpret_cast<const uint32_t*>(D + o[1]),
+                             reinterpret_cast<const uint32_t*>(D + o[2]), c->kec_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), dstat, s);
   if (daddr) HIPCHK(hipMemsetAsync(daddr, 0, n * 20, s));
   for (const RecFront& f : fronts) {
@@ -1157,6 +1201,12 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   HIPCHK(hipEventRecord(c->ev_done, s));
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
+  for (int x : bad) {
+    if (x) {
+      st.drain();
+      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
+    }
+  }
   HIPCHK(hipEventSynchronize(c->ev_done));
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);

@@ -1,13 +1,13 @@
-"""The host-buffer entry hlc_validate_proposals (hlc_api.cpp validate_host: the batch staged and
-uploaded in recovery ranges, each range's k_rec_prep + k_rec_main behind its upload on two streams in
-turn, the rest of the validation once every range has landed) equals the single-range schedule and
-the C oracle bit for bit:
+"""The host-buffer entry hlc_validate_proposals (hlc_api.cpp validate_host: the signatures staged
+and uploaded first as a dense array, range by range, each range's k_rec_prep + k_rec_main behind its
+upload on two streams in turn, the other inputs in pieces behind them) equals the single-range
+schedule and the C oracle bit for bit:
 per-proposal results, per-vote statuses, scheme reasons and recovered addresses, on a Byzantine
 batch; also with empty proposals, votes no proposal covers (status 0xFF), proposals listed out of
 vote order, and an out-of-arena field -- a signature in the second range or another field in a late
 piece -- which returns HLC_EINVAL with the caller's outputs untouched (the device work already
-enqueued is drained and discarded).  Schedule knob: HLC_SPLIT_VOTES (sizes of the recovery ranges
-before the last, "0" = one range)."""
+enqueued is drained and discarded).  Schedule knobs: HLC_SPLIT_VOTES (sizes of the recovery ranges
+before the last, "0" = one range), HLC_REST_PIECES."""
 import ctypes
 import os
 
@@ -24,12 +24,15 @@ pytestmark = pytest.mark.gpu
 HLC_EINVAL = -1  # include/hlc.h
 
 
-def _run(engine, batch, desc, now, split):
+def _run(engine, batch, desc, now, split, pieces=None):
     os.environ["HLC_SPLIT_VOTES"] = str(split)
+    if pieces is not None:
+        os.environ["HLC_REST_PIECES"] = str(pieces)
     try:
         return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
     finally:
         os.environ.pop("HLC_SPLIT_VOTES", None)
+        os.environ.pop("HLC_REST_PIECES", None)
 
 
 @pytest.fixture(scope="module")
@@ -39,11 +42,12 @@ def byz():
     return b, d, w.now
 
 
-@pytest.mark.parametrize("split", ["100", "240", "333", "1", "1,1,1,1", "64,128", "100,150,90", "32,32,32,32,32,32,32"])
-def test_gpu_host_entry_equals_single_range_and_oracle(engine, byz, split):
+@pytest.mark.parametrize("split,pieces", [("100", 3), ("240", 1), ("333", 7), ("1", 2), ("1,1,1,1", 64), ("64,128", 3),
+                                          ("100,150,90", 5), ("32,32,32,32,32,32,32", 1)])
+def test_gpu_host_entry_equals_single_range_and_oracle(engine, byz, split, pieces):
     b, d, now = byz
-    one = _run(engine, b, d, now, 0)
-    got = _run(engine, b, d, now, split)
+    one = _run(engine, b, d, now, 0, 1)
+    got = _run(engine, b, d, now, split, pieces)
     for x, y in zip(one, got):
         assert np.array_equal(x, y)
     cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
