@@ -166,7 +166,7 @@ struct hlc_ctx {
   // the page-locked staging of the inputs and outputs and their device copies (allocated on first use)
   hipStream_t aux2 = nullptr, copy = nullptr;
   DBuf rec_scratch2;
-  std::vector<std::unique_ptr<DBuf>> rec_works;  // per-vote records of each recovery range but the first
+  std::vector<std::unique_ptr<DBuf>> rec_works;  // each recovery range's work list, prefix products, counters
   PBuf pin_in, pin_out;
   DBuf dev_in, dev_out;
   std::vector<hipEvent_t> ev_up, ev_main;  // per recovery range: inputs landed, main stage done
@@ -297,11 +297,11 @@ int ensure_fbtab(hlc_ctx* c) {
   return 0;
 }
 
-// A recovery range whose front half (k_rec_prep + k_rec_main over votes [v0, v1), records in `work`)
-// the caller has already enqueued on a stream of its own; `done` fires when that main stage ends.
+// A recovery range whose front half (k_rec_prep + k_rec_main over votes [v0, v1), records in the
+// call's rec_work) the caller has already enqueued on a stream of its own; `done` fires when that
+// main stage ends.
 struct RecFront {
   uint64_t v0, v1;
-  uint32_t* work;
   hipEvent_t done;
 };
 
@@ -314,7 +314,9 @@ struct RecFront {
 // chain_code != nullptr: also the small proposals' chain / duplicate / YES kernel (it needs no
 // vote statuses), on `s` beside the recovery's main stage.
 // fronts != nullptr (hlc_validate_proposals over host buffers): the recovery's front halves are
-// already in flight over those ranges (validate_host); each range's finish waits for its event.
+// already in flight over those ranges (validate_host); one finish over all votes waits for them.
+// (One finish, not one per range: its k_rec_final / k_rec_addr are short low-occupancy kernels, and
+// per range they cost 0.95 ms against 0.67 ms for one launch over 640k votes.)
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t np,
                uint64_t now, uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, uint8_t* chain_code,
                hipStream_t s, const RecFront* fronts = nullptr, int nfronts = 0) {
@@ -324,7 +326,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   CHK(c->verify.ensure(n));
   CHK(c->kec_dig.ensure(n * 32));
   CHK(ensure_recover_scratch(c));
-  // (fronts: range 0's records are in flight in rec_work, sized by the caller)
+  // (fronts: the ranges' records are in flight in rec_work, sized by the caller)
   if (!fronts) CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   // The recovery's prep stage (signature parse, batched r^-1, GLV digits) and main stage (R, its
   // table, the u2 R chain: ~93% of the recovery) need only the signatures, so they run on the
@@ -364,14 +366,10 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   };
   if (fronts) {
     CHK(prehash_and_chain());
-    for (int k = 0; k < nfronts; ++k) {
-      const RecFront& f = fronts[k];
-      HIPCHK(hipStreamWaitEvent(s, f.done, 0));
-      hlc::launch_recover_finish(f.v1 - f.v0, c->pre.as<uint8_t>() + f.v0, c->kec_dig.as<uint32_t>() + 8 * f.v0,
-                                 dv->bytes, dv->field_off + f.v0 * HLC_NFIELDS + HLC_F_OWNER, HLC_NFIELDS,
-                                 c->gtab.as<uint32_t>(), f.work, c->verify.as<uint8_t>() + f.v0,
-                                 drec ? drec + 20 * f.v0 : nullptr, s, c->rec_force_exact);
-    }
+    for (int k = 0; k < nfronts; ++k) HIPCHK(hipStreamWaitEvent(s, fronts[k].done, 0));
+    hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
+                               dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(),
+                               c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact);
     hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
                             c->verify.as<uint8_t>(), status, reason, red, s);
     HIPCHK(hipGetLastError());
@@ -700,14 +698,14 @@ int host_threads() {
 }
 
 // The recovery ranges of a host-buffer call of n items (HLC_SPLIT_VOTES="a,b,...", default
-// "131072,196608"; "0" = one range): a range of each listed size while at least twice that many
+// "65536,196608"; "0" = one range): a range of each listed size while at least twice that many
 // items remain, then one range for the rest.  Range k's k_rec_main grid starts once its signatures
 // have landed; ranges alternate between two streams (and two per-lane scratch buffers), so each
 // range's waves take the SIMD slots the previous range's waves free.
 std::vector<uint64_t> split_ranges(uint64_t n) {
   std::vector<uint64_t> sizes, b{0};
   const char* e = std::getenv("HLC_SPLIT_VOTES");
-  const char* p = e ? e : "131072,196608";
+  const char* p = e ? e : "65536,196608";
   while (*p) {
     char* end = nullptr;
     const uint64_t x = std::strtoull(p, &end, 10);
@@ -830,7 +828,8 @@ struct Staging {
 int prepare_ranges(hlc_ctx* c, uint64_t n, std::vector<uint64_t>& rb) {
   rb = split_ranges(n);
   const size_t R = rb.size() - 1;
-  while (c->rec_works.size() + 1 < R) c->rec_works.emplace_back(new DBuf());
+  CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
+  while (c->rec_works.size() < R) c->rec_works.emplace_back(new DBuf());
   while (c->ev_up.size() < R) {
     hipEvent_t a = nullptr, b = nullptr;
     HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
@@ -838,31 +837,30 @@ int prepare_ranges(hlc_ctx* c, uint64_t n, std::vector<uint64_t>& rb) {
     HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
     c->ev_main.push_back(b);
   }
-  for (size_t k = 0; k < R; ++k) {
-    DBuf& wb = k == 0 ? c->rec_work : *c->rec_works[k - 1];
-    CHK(wb.ensure(hlc::recover_work_words(rb[k + 1] - rb[k]) * sizeof(uint32_t)));
-  }
+  for (size_t k = 0; k < R; ++k) CHK(c->rec_works[k]->ensure(hlc::recover_range_words(rb[k + 1] - rb[k]) * 4));
   return 0;
 }
 
 // Range k's front half of the recovery -- k_rec_prep + k_rec_main over its m items, signatures read
 // through (sig_off, sig_len) from the device arena -- on the aux streams in turn (k even: aux, odd:
 // aux2, each with its own per-lane scratch), once its upload (ev_up[k]) has landed.
-int launch_front(hlc_ctx* c, HostTrace& tr, size_t k, uint64_t a0, uint64_t m, const uint8_t* dbytes,
+int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, uint64_t m, const uint8_t* dbytes,
                  const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len, size_t len_stride,
                  std::vector<RecFront>& fronts) {
   if (!m) return 0;
-  DBuf& wb = k == 0 ? c->rec_work : *c->rec_works[k - 1];
-  hipStream_t a = k % 2 ? c->aux2 : c->aux;
-  uint32_t* scratch = (k % 2 ? c->rec_scratch2 : c->rec_scratch).as<uint32_t>();
+  const hlc::RecRange range{a0, m, c->rec_works[k]->as<uint32_t>()};
+  const bool odd = k % 2;
+  hipStream_t a = odd ? c->aux2 : c->aux;
+  uint32_t* scratch = (odd ? c->rec_scratch2 : c->rec_scratch).as<uint32_t>();
   HIPCHK(hipStreamWaitEvent(a, c->ev_up[k], 0));
-  hlc::launch_recover_prep(m, dbytes, sig_off, off_stride, sig_len, len_stride, wb.as<uint32_t>(), a);
-  hlc::launch_recover_main(m, dbytes, sig_off, off_stride, scratch, c->rec_lanes, wb.as<uint32_t>(), a,
-                           c->rec_force_exact);
+  hlc::launch_recover_prep(n, dbytes, sig_off, off_stride, sig_len, len_stride, c->rec_work.as<uint32_t>(), a,
+                           nullptr, &range);
+  hlc::launch_recover_main(n, dbytes, sig_off, off_stride, scratch, c->rec_lanes, c->rec_work.as<uint32_t>(), a,
+                           c->rec_force_exact, &range);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_main[k], a));
   tr.ev("main_end_" + std::to_string(k), a);
-  fronts.push_back(RecFront{a0, a0 + m, wb.as<uint32_t>(), c->ev_main[k]});
+  fronts.push_back(RecFront{a0, a0 + m, c->ev_main[k]});
   return 0;
 }
 
@@ -1020,7 +1018,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
     HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
     tr.mark("sigs_staged_" + std::to_string(k));
     tr.ev("sigs_landed_" + std::to_string(k), c->copy);
-    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[0] + 65 * a0, nullptr, 0,
+    CHK(launch_front(c, tr, n, k, a0, a1 - a0, D + o[0] + 65 * a0, nullptr, 0,
                      reinterpret_cast<const uint32_t*>(D + o[1]) + a0, 1, fronts));
   }
   // everything else, piece by piece; the field checks ride along with the rows' staging copies
@@ -1148,7 +1146,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
     HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
     tr.mark("sigs_staged_" + std::to_string(k));
     tr.ev("sigs_landed_" + std::to_string(k), c->copy);
-    CHK(launch_front(c, tr, k, a0, a1 - a0, D + o[0] + 65 * a0, nullptr, 0,
+    CHK(launch_front(c, tr, n, k, a0, a1 - a0, D + o[0] + 65 * a0, nullptr, 0,
                      reinterpret_cast<const uint32_t*>(D + o[1]) + a0, 1, fronts));
   }
   Arr arr[4] = {{reinterpret_cast<const uint8_t*>(id_len), o[2], 4, false},
@@ -1189,12 +1187,9 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
                              reinterpret_cast<const uint32_t*>(D + o[2]), c->kec_dig.as<uint32_t>(),
                              c->pre.as<uint8_t>(), dstat, s);
   if (daddr) HIPCHK(hipMemsetAsync(daddr, 0, n * 20, s));
-  for (const RecFront& f : fronts) {
-    HIPCHK(hipStreamWaitEvent(s, f.done, 0));
-    hlc::launch_recover_finish(f.v1 - f.v0, c->pre.as<uint8_t>() + f.v0, c->kec_dig.as<uint32_t>() + 8 * f.v0, dbytes,
-                               did_off + f.v0, 1, c->gtab.as<uint32_t>(), f.work, dstat + f.v0,
-                               daddr ? daddr + 20 * f.v0 : nullptr, s, c->rec_force_exact);
-  }
+  for (const RecFront& f : fronts) HIPCHK(hipStreamWaitEvent(s, f.done, 0));
+  hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dbytes, did_off, 1,
+                             c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), dstat, daddr, s, c->rec_force_exact);
   HIPCHK(hipGetLastError());
   tr.ev("kernels_end", s);
   HIPCHK(hipMemcpyAsync(c->pin_out.p, ob, r2, hipMemcpyDeviceToHost, s));

@@ -77,17 +77,27 @@ struct RecSkip {
   const uint32_t* proposal_id; // per vote
   const uint32_t* field_len;   // hlc_votes.field_len
 };
+// range != nullptr: the front half over items [v0, v0 + m) only (bytes / sig_off / sig_len already
+// at item v0), records in the call's `work` (sized for all n items, so that one finish covers every
+// range); the range's work list, prefix products and counters in range->work
+// (recover_range_words(m)), so ranges may run on different streams at once.
+struct RecRange {
+  uint64_t v0, m;
+  uint32_t* work;
+};
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s,
-                         const RecSkip* skip = nullptr);
+                         const RecSkip* skip = nullptr, const RecRange* range = nullptr);
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
-                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact = 0);
+                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact = 0,
+                         const RecRange* range = nullptr);
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gtab, uint32_t* work,
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0);
 uint64_t recover_grid_lanes();
 uint64_t recover_scratch_words();  // per-lane workspace words of k_rec_main
 uint64_t recover_work_words(uint64_t n);
+uint64_t recover_range_words(uint64_t m);  // RecRange::work words for m items
 void launch_build_gcomb(uint32_t* gcomb, const uint32_t* fbtab, hipStream_t s);  // needs fbtab
 size_t gcomb_words();
 

@@ -69,13 +69,18 @@ HLC_DEV bool pre_rejected(const RecSkip& k, uint64_t i) {
   return fl[HLC_F_OWNER] == 0 || fl[HLC_F_VOTE_HASH] == 0;
 }
 
-__global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, const uint8_t* bytes,
+// n votes; records rec / mst of vote i at rec + i (stride `st` words between a record's rows), mst[i].
+__global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t st, uint64_t L, const uint8_t* bytes,
                                                        const uint64_t* sig_off, size_t off_stride,
                                                        const uint32_t* sig_len, size_t len_stride, uint32_t* rec,
                                                        uint32_t* pfx, uint8_t* mst, uint32_t* list,
                                                        unsigned long long* list_len, RecSkip sk) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= L) return;
+  // a few long dependent chains per lane at low occupancy: when it shares the SIMDs with a k_rec_main
+  // grid (host-buffer ranges: the next range's prep beside this range's main), the arbiter serves its
+  // waves first -- measured without this, a 196k-vote prep took 1.18 ms beside a main vs 0.25 alone
+  __builtin_amdgcn_s_setprio(2);
   fe acc;
   fe_set(acc, 1);
   uint32_t active = 0;  // bit k: vote t + k L goes to k_rec_main
@@ -86,12 +91,12 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
     fe r, s;
     int parity, code;
     if (pre_rejected(sk, i) || !prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) {
-      rec[(size_t)REC_FLAGS * n + i] = PREP_SKIP << 8;
+      rec[(size_t)REC_FLAGS * st + i] = PREP_SKIP << 8;
       mst[i] = MST_SKIP;
       continue;
     }
     if (code != SCHEME_NONE) {
-      rec[(size_t)REC_FLAGS * n + i] = (uint32_t)code << 8;
+      rec[(size_t)REC_FLAGS * st + i] = (uint32_t)code << 8;
       mst[i] = (uint8_t)(1 + code);
       continue;
     }
@@ -111,7 +116,7 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
     sc_mont_mul(rinv, prev, cur);  // r_k^-1
     sc_mont_mul(cur, cur, r);      // acc_{k-1}^-1
-    rec_prep_scalars(s, rinv, parity, rec + i, n);
+    rec_prep_scalars(s, rinv, parity, rec + i, st);
   }
   // the work list: per k, the wave's active votes (64 consecutive indices) in one run, one atomic
   const unsigned lane = threadIdx.x & 63u;
@@ -137,7 +142,7 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t L, c
 // the 3 resident waves finishes its share long before the youngest, which then runs alone at
 // lone-wave efficiency (measured with HLC_CLOCK_PROBE: 4-vote blocks done at 3.5 ms, the last
 // 3-vote blocks at 7.0 ms of one launch); grabbing keeps every wave busy until the work runs out.
-__global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_t n, const uint8_t* bytes,
+__global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_t st, const uint8_t* bytes,
                                                                      const uint64_t* sig_off, size_t off_stride,
                                                                      uint32_t* scratch, uint64_t lanes,
                                                                      const uint32_t* rec, uint32_t* q, uint8_t* mst,
@@ -169,15 +174,15 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
     fe r, qx, qy, qz;
     bool inf = false;
     fe_load_be(r, sig_at(bytes, sig_off, off_stride, i));
-    const int code = rec_u2r29(r, rec + i, n, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0);
+    const int code = rec_u2r29(r, rec + i, st, qx, qy, qz, inf, ws, lanes, tab, force_exact != 0);
     if (code != SCHEME_NONE) {
       mst[i] = (uint8_t)(1 + code);
       continue;
     }
     mst[i] = inf ? MST_INF : MST_OK;
-    store_fe_ws(qx, q + i, n);
-    store_fe_ws(qy, q + (size_t)8 * n + i, n);
-    store_fe_ws(qz, q + (size_t)16 * n + i, n);
+    store_fe_ws(qx, q + i, st);
+    store_fe_ws(qy, q + (size_t)8 * st + i, st);
+    store_fe_ws(qz, q + (size_t)16 * st + i, st);
   }
 #ifdef HLC_CLOCK_PROBE
   if (threadIdx.x == 0 && blockIdx.x % 61 == 0) {
@@ -405,6 +410,11 @@ uint64_t recover_grid_lanes() {
   return (uint64_t)cus * (uint64_t)per_cu * REC_TPB;
 }
 
+uint64_t recover_range_words(uint64_t m) {
+  const uint64_t L = (m + REC_BATCH - 1) / REC_BATCH;
+  return m + L * REC_BATCH * 8 + 16;
+}
+
 namespace {
 struct RecBufs {
   uint32_t *rec, *q, *pfx, *list;
@@ -425,28 +435,54 @@ RecBufs rec_bufs(uint64_t n, uint32_t* work) {
   b.ctr = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(b.mst + n) + 7) & ~uintptr_t(7));
   return b;
 }
+// The front half's buffers for items [v0, v0 + m) of a call of n items: the per-vote records in the
+// call's `work` (row stride n), the work list, prefix products and counters in `range_work` (or, for
+// the whole call, in `work` too).
+struct FrontBufs {
+  RecBufs b;  // rec / q / mst at item v0
+  uint64_t st;
+};
+FrontBufs front_bufs(uint64_t n, uint64_t v0, uint64_t m, uint32_t* work, uint32_t* range_work) {
+  FrontBufs f{rec_bufs(n, work), n};
+  f.b.rec += v0;
+  f.b.q += v0;
+  f.b.mst += v0;
+  f.b.L = (m + REC_BATCH - 1) / REC_BATCH;
+  if (range_work) {
+    f.b.list = range_work;
+    f.b.pfx = range_work + m;
+    f.b.ctr = reinterpret_cast<unsigned long long*>(
+        (reinterpret_cast<uintptr_t>(f.b.pfx + f.b.L * REC_BATCH * 8) + 7) & ~uintptr_t(7));
+  }
+  return f;
+}
 }  // namespace
 
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
-                         const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s, const RecSkip* skip) {
-  if (!n) return;
-  const RecBufs b = rec_bufs(n, work);
-  const unsigned pb = (unsigned)((b.L + PREP_TPB - 1) / PREP_TPB);
-  (void)hipMemsetAsync(b.ctr, 0, 2 * sizeof(unsigned long long), s);  // grab counter, list length
+                         const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s, const RecSkip* skip,
+                         const RecRange* range) {
+  const uint64_t m = range ? range->m : n;
+  if (!m) return;
+  const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr);
+  const unsigned pb = (unsigned)((f.b.L + PREP_TPB - 1) / PREP_TPB);
+  (void)hipMemsetAsync(f.b.ctr, 0, 2 * sizeof(unsigned long long), s);  // grab counter, list length
   const RecSkip none{nullptr, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, n, b.L, bytes, sig_off, off_stride, sig_len,
-                     len_stride, b.rec, b.pfx, b.mst, b.list, b.ctr + 1, skip ? *skip : none);
+  hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, m, f.st, f.b.L, bytes, sig_off, off_stride, sig_len,
+                     len_stride, f.b.rec, f.b.pfx, f.b.mst, f.b.list, f.b.ctr + 1, skip ? *skip : none);
 }
 
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
-                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact) {
-  if (!n) return;
-  const RecBufs b = rec_bufs(n, work);
+                         uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact,
+                         const RecRange* range) {
+  const uint64_t m = range ? range->m : n;
+  if (!m) return;
+  const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr);
   uint64_t blocks = scratch_lanes / REC_TPB;
-  uint64_t need = (n + REC_TPB - 1) / REC_TPB;
+  uint64_t need = (m + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
-  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, n, bytes, sig_off, off_stride, scratch,
-                     (uint64_t)blocks * REC_TPB, b.rec, b.q, b.mst, force_exact, b.ctr, b.list, b.ctr + 1);
+  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, f.st, bytes, sig_off, off_stride,
+                     scratch, (uint64_t)blocks * REC_TPB, f.b.rec, f.b.q, f.b.mst, force_exact, f.b.ctr, f.b.list,
+                     f.b.ctr + 1);
 }
 
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
