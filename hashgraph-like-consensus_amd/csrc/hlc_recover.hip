@@ -35,6 +35,9 @@ constexpr int REC_TPB = HLC_REC_TPB;  // k_rec_main block size
 // signature -- writing its k_rec_main state byte, and appends the others to the work list that
 // k_rec_main's waves take their votes from (in runs of up to 64 consecutive votes).
 constexpr int PREP_TPB = 64;
+#ifndef HLC_PREP_PRIO
+#define HLC_PREP_PRIO 2  // k_rec_prep's wave issue priority (s_setprio; 0 = the default, 0)
+#endif
 constexpr uint32_t PREP_SKIP = 0xFFu;  // record flags bits 8-15: no 65-byte signature, not parsed
 // k_rec_main -> k_rec_comb, one byte per vote: u2 R finite / at infinity / nothing to recover, or
 // 1 + the scheme code (prep's v / r / s checks, or no point R)
@@ -80,7 +83,9 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t st, 
   // a few long dependent chains per lane at low occupancy: when it shares the SIMDs with a k_rec_main
   // grid (host-buffer ranges: the next range's prep beside this range's main), the arbiter serves its
   // waves first -- measured without this, a 196k-vote prep took 1.18 ms beside a main vs 0.25 alone
-  __builtin_amdgcn_s_setprio(2);
+#if HLC_PREP_PRIO
+  __builtin_amdgcn_s_setprio(HLC_PREP_PRIO);
+#endif
   fe acc;
   fe_set(acc, 1);
   uint32_t active = 0;  // bit k: vote t + k L goes to k_rec_main
