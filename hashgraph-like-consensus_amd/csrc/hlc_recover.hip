@@ -63,8 +63,11 @@ HLC_DEV bool prep_sig(const uint8_t* bytes, const uint64_t* sig_off, size_t off_
 // match, 133-140 empty owner / vote_hash; the empty signature is a length skip already), and votes no
 // proposal covers: such a vote's status never depends on its recovery (k_prehash_fused decides it
 // from the same fields), so k_rec_main does not run its u2 R chain.
+#ifndef HLC_PRE_SKIP
+#define HLC_PRE_SKIP 1  // 0: A/B arm without the skip (every parsed signature runs the chain)
+#endif
 HLC_DEV bool pre_rejected(const RecSkip& k, uint64_t i) {
-  if (!k.vote_prop) return false;
+  if (!HLC_PRE_SKIP || !k.vote_prop) return false;
   const uint32_t p = k.vote_prop[i];
   if (p == NO_PROP) return true;
   if (k.proposal_id[i] != k.props[p].proposal_id) return true;
