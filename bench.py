@@ -610,7 +610,9 @@ def main() -> int:
     gpu = 0 if os.environ.get("HLC_BENCH_SAME_GPU") == "1" else local_rank
     dist = None
     torch.cuda.set_device(gpu)
-    if world > 1:
+    # HLC_BENCH_DIST=1 at one rank: the N > 1 code path (process group, the RCCL exchange in the
+    # timed step, the gathered-rows check) on one GPU -- the rehearsal of the driver's multi-GPU run
+    if world > 1 or os.environ.get("HLC_BENCH_DIST") == "1":
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))

@@ -83,3 +83,63 @@ def test_gpu_sharded_paths_equal_single(engine):
     for rank, parts in got:
         for name, a, b in zip(names, parts, ref):
             assert a == b, f"rank {rank}: sharded {name} differ from the single call"
+
+
+def _rccl_worker(port, q):
+    """One rank over RCCL (world size 1): the exchange bench.py's N > 1 step runs on device tensors
+    (ShardExchange: all_gather_into_tensor of the result rows, all_reduce of the counters) and the
+    proposal-sharded entry (validate_shard), on the GPU."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "hashgraph-like-consensus_amd", "python"),
+              os.path.join(os.path.dirname(here), "oracle"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from hashgraph_like_consensus.device import DeviceBatch
+    from hashgraph_like_consensus.engine import Engine
+    from hashgraph_like_consensus.parallel import ShardExchange, validate_shard
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    eng = Engine(0)
+    try:
+        db = DeviceBatch.synthetic(eng, 300, 64, 64, True, 0x484C4352, device="cuda:0")
+        stream = torch.cuda.Stream(device="cuda:0")
+        ex = ShardExchange(300, 1, "cuda:0", engine=eng)
+        eng.validate_proposals_device(db, stream.cuda_stream)
+        with torch.cuda.stream(stream):
+            ex(db.results, db.status, 300, db.n)
+        torch.cuda.synchronize()
+        rows = ex.results([300])
+        same = rows.view(np.uint8).tobytes() == db.results_numpy().view(np.uint8).tobytes()
+        summ = ex.summary()
+        (batch, desc, now), _, _ = _inputs()
+        full, vst, summ2 = validate_shard(eng, batch, desc, now, device="cuda:0", want_votes=True)
+        q.put((same, summ, db.n, full.tobytes(), vst.tobytes(), summ2))
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+def test_gpu_rccl_exchange_one_rank(engine):
+    """The RCCL branch of the exchange (the driver's multi-GPU bench runs it at N = 2, 4, 8) at one
+    rank on the box's GPU: gathered rows equal the local results, counters count every vote, and the
+    proposal-sharded entry over RCCL equals the single call."""
+    (batch, desc, now), _, _ = _inputs()
+    res, vst, _, _ = engine.validate_proposals(batch, desc, now, want_votes=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    same, summ, n, full, vrows, summ2 = q.get(timeout=200)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert same, "RCCL-gathered rows differ from the local results"
+    assert summ["verified_votes"] == n and summ["proposals_ok"] == 300
+    assert full == res.tobytes()
+    idx = np.concatenate([np.arange(int(d["vote_begin"]), int(d["vote_begin"]) + int(d["vote_count"]))
+                          for d in desc])
+    assert vrows == np.asarray(vst, np.uint8)[idx].tobytes()
+    assert summ2["verified_votes"] == int((np.asarray(vst)[idx] == 0).sum())

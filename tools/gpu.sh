@@ -9,6 +9,7 @@
 #   bench      the driver's command: bench.py --gpus 1 --steps 20 --warmup 5 (every leg)
 #   qbench     headline leg only, 5 steps
 #   n2         N = 2 dry run of the sharded bench (gloo, both ranks on GPU 0): config-4 shards
+#   rccl1      the N > 1 bench path at one rank over RCCL (HLC_BENCH_DIST=1): config-4 shard, exchange on GPU
 #   pipe       tools/host_pipe.py sweep, arguments from $PIPE_ARGS
 #   pipetrace  rocprofv3 kernel + memory-copy trace of one host-buffer setting ($PIPE_ARGS)
 #   verify     tools/verify_latency.py (hlc_eth_verify_batch at the C ABI)
@@ -50,6 +51,11 @@ for step in "$@"; do
       --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --config 4 --proposals 20000 \
       --steps 5 --warmup 2 > $O/n2_$TAG.json 2> $O/n2_$TAG.err || fail n2 $O/n2_$TAG.err
     python tools/bench_summary.py $O/n2_$TAG.json ;;
+  rccl1)
+    HLC_BENCH_DIST=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+      --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 1 --config 4 --proposals 20000 --steps 5 --warmup 2 \
+      $LEGS > $O/rccl1_$TAG.json 2> $O/rccl1_$TAG.err || fail rccl1 $O/rccl1_$TAG.err
+    python tools/bench_summary.py $O/rccl1_$TAG.json ;;
   pipe)
     timeout -k 10 500 python tools/host_pipe.py $PIPE_ARGS > $O/pipe_$TAG.txt 2> $O/pipe_$TAG.err || fail pipe $O/pipe_$TAG.err
     cat $O/pipe_$TAG.txt ;;
