@@ -699,7 +699,9 @@ int host_threads() {
 
 // The recovery ranges of a host-buffer call of n items (HLC_SPLIT_VOTES="a,b,...", default
 // "65536,196608"; "0" = one range): a range of each listed size while at least twice that many
-// items remain, then one range for the rest.  Range k's k_rec_main grid starts once its signatures
+// items remain, then ranges of twice the previous size on the same rule (a large batch keeps the
+// device busy while the host gathers the next range's signatures; at most 16 ranges), then one
+// range for the rest.  Range k's k_rec_main grid starts once its signatures
 // have landed; ranges alternate between two streams (and two per-lane scratch buffers), so each
 // range's waves take the SIMD slots the previous range's waves free.
 std::vector<uint64_t> split_ranges(uint64_t n) {
@@ -713,8 +715,10 @@ std::vector<uint64_t> split_ranges(uint64_t n) {
     sizes.push_back(x);
     p = *end == ',' ? end + 1 : end;
   }
-  for (uint64_t x : sizes) {
-    if (!x || b.size() > 7 || n - b.back() < 2 * x) break;
+  uint64_t x = 0;
+  for (size_t k = 0; k < 15; ++k) {
+    x = k < sizes.size() ? sizes[k] : 2 * x;
+    if (!x || n - b.back() < 2 * x) break;
     b.push_back(b.back() + x);
   }
   if (n > b.back() || b.size() == 1) b.push_back(n);
