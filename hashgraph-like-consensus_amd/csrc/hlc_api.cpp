@@ -698,7 +698,7 @@ int host_threads() {
 }
 
 // The recovery ranges of a host-buffer call of n items (HLC_SPLIT_VOTES="a,b,...", default
-// "65536,196608"; "0" = one range): a range of each listed size while at least twice that many
+// "98304,196608"; "0" = one range): a range of each listed size while at least twice that many
 // items remain, then ranges of twice the previous size on the same rule (a large batch keeps the
 // device busy while the host gathers the next range's signatures; at most 16 ranges), then one
 // range for the rest.  Range k's k_rec_main grid starts once its signatures
@@ -707,7 +707,7 @@ int host_threads() {
 std::vector<uint64_t> split_ranges(uint64_t n) {
   std::vector<uint64_t> sizes, b{0};
   const char* e = std::getenv("HLC_SPLIT_VOTES");
-  const char* p = e ? e : "65536,196608";
+  const char* p = e ? e : "98304,196608";
   while (*p) {
     char* end = nullptr;
     const uint64_t x = std::strtoull(p, &end, 10);

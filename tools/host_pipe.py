@@ -35,7 +35,7 @@ def print_trace(path: str) -> None:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--split", default="65536,196608", help="'/'-separated HLC_SPLIT_VOTES settings (range sizes "
+    ap.add_argument("--split", default="98304,196608", help="'/'-separated HLC_SPLIT_VOTES settings (range sizes "
                     "before the last, e.g. 131072,196608/0; 0 = one recovery range)")
     ap.add_argument("--threads", default="4", help="HLC_HOST_THREADS settings")
     ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
