@@ -845,6 +845,12 @@ int prepare_ranges(hlc_ctx* c, uint64_t n, std::vector<uint64_t>& rb) {
   return 0;
 }
 
+// votes per k_rec_prep lane in the first recovery range (HLC_FIRST_BATCH, default 1; 8 = as the rest)
+int first_batch() {
+  const char* e = std::getenv("HLC_FIRST_BATCH");
+  return e ? std::atoi(e) : 1;
+}
+
 // Range k's front half of the recovery -- k_rec_prep + k_rec_main over its m items, signatures read
 // through (sig_off, sig_len) from the device arena -- on the aux streams in turn (k even: aux, odd:
 // aux2, each with its own per-lane scratch), once its upload (ev_up[k]) has landed.
@@ -852,7 +858,9 @@ int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, u
                  const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len, size_t len_stride,
                  std::vector<RecFront>& fronts) {
   if (!m) return 0;
-  const hlc::RecRange range{a0, m, c->rec_works[k]->as<uint32_t>()};
+  // the first range's prep is on the call's critical path with the device otherwise idle: one vote
+  // per lane (no batched inversion), so its dependent chain is an eighth as long
+  const hlc::RecRange range{a0, m, c->rec_works[k]->as<uint32_t>(), k == 0 ? first_batch() : 0};
   const bool odd = k % 2;
   hipStream_t a = odd ? c->aux2 : c->aux;
   uint32_t* scratch = (odd ? c->rec_scratch2 : c->rec_scratch).as<uint32_t>();

@@ -84,6 +84,7 @@ struct RecSkip {
 struct RecRange {
   uint64_t v0, m;
   uint32_t* work;
+  int batch;  // votes per k_rec_prep lane (one inversion each): 0 = the default (8)
 };
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s,

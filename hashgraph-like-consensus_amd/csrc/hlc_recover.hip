@@ -418,10 +418,7 @@ uint64_t recover_grid_lanes() {
   return (uint64_t)cus * (uint64_t)per_cu * REC_TPB;
 }
 
-uint64_t recover_range_words(uint64_t m) {
-  const uint64_t L = (m + REC_BATCH - 1) / REC_BATCH;
-  return m + L * REC_BATCH * 8 + 16;
-}
+uint64_t recover_range_words(uint64_t m) { return m + (m + REC_BATCH) * 8 + 16; }
 
 namespace {
 struct RecBufs {
@@ -450,17 +447,21 @@ struct FrontBufs {
   RecBufs b;  // rec / q / mst at item v0
   uint64_t st;
 };
-FrontBufs front_bufs(uint64_t n, uint64_t v0, uint64_t m, uint32_t* work, uint32_t* range_work) {
+FrontBufs front_bufs(uint64_t n, uint64_t v0, uint64_t m, uint32_t* work, uint32_t* range_work,
+                     const RecRange* range) {
   FrontBufs f{rec_bufs(n, work), n};
   f.b.rec += v0;
   f.b.q += v0;
   f.b.mst += v0;
-  f.b.L = (m + REC_BATCH - 1) / REC_BATCH;
+  // votes per prep lane: REC_BATCH, or fewer for a range that must start soon (more lanes, shorter
+  // dependent chains; k_rec_prep's loops stop at the first vote index >= m)
+  const uint64_t per = range && range->batch > 0 && range->batch < REC_BATCH ? (uint64_t)range->batch : REC_BATCH;
+  f.b.L = (m + per - 1) / per;
   if (range_work) {
     f.b.list = range_work;
-    f.b.pfx = range_work + m;
+    f.b.pfx = range_work + m;  // (m + REC_BATCH) * 8 words >= per * L * 8
     f.b.ctr = reinterpret_cast<unsigned long long*>(
-        (reinterpret_cast<uintptr_t>(f.b.pfx + f.b.L * REC_BATCH * 8) + 7) & ~uintptr_t(7));
+        (reinterpret_cast<uintptr_t>(f.b.pfx + (m + REC_BATCH) * 8) + 7) & ~uintptr_t(7));
   }
   return f;
 }
@@ -471,7 +472,7 @@ void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
                          const RecRange* range) {
   const uint64_t m = range ? range->m : n;
   if (!m) return;
-  const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr);
+  const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr, range);
   const unsigned pb = (unsigned)((f.b.L + PREP_TPB - 1) / PREP_TPB);
   (void)hipMemsetAsync(f.b.ctr, 0, 2 * sizeof(unsigned long long), s);  // grab counter, list length
   const RecSkip none{nullptr, nullptr, nullptr, nullptr};
@@ -484,7 +485,7 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
                          const RecRange* range) {
   const uint64_t m = range ? range->m : n;
   if (!m) return;
-  const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr);
+  const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr, range);
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (m + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;

@@ -7,7 +7,7 @@ batch; also with empty proposals, votes no proposal covers (status 0xFF), propos
 vote order, and an out-of-arena field -- a signature in the second range or another field in a late
 piece -- which returns HLC_EINVAL with the caller's outputs untouched (the device work already
 enqueued is drained and discarded).  Schedule knobs: HLC_SPLIT_VOTES (sizes of the recovery ranges
-before the last, "0" = one range), HLC_REST_PIECES."""
+before the last, "0" = one range), HLC_REST_PIECES, HLC_FIRST_BATCH."""
 import ctypes
 import os
 
@@ -54,6 +54,24 @@ def test_gpu_host_entry_equals_single_range_and_oracle(engine, byz, split, piece
     assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
     assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec)
     assert len({int(s) for s in got[0]["status"]}) > 3
+
+
+@pytest.mark.parametrize("first_batch", ["1", "2", "3", "8"])
+def test_gpu_host_entry_first_range_prep_batch(engine, byz, first_batch):
+    """The first range's k_rec_prep with 1, 2, 3 or 8 votes per lane (HLC_FIRST_BATCH: the lane count
+    and the prefix-product layout follow it) equals the oracle bit for bit."""
+    b, d, now = byz
+    os.environ["HLC_FIRST_BATCH"] = first_batch
+    try:
+        got = _run(engine, b, d, now, "100,150")
+        one = _run(engine, b, d, now, "0")
+    finally:
+        os.environ.pop("HLC_FIRST_BATCH", None)
+    for x, y in zip(one, got):
+        assert np.array_equal(x, y)
+    cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
+    assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
+    assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec)
 
 
 def test_gpu_host_entry_gaps_and_empty_proposals(engine, byz):
