@@ -1,10 +1,17 @@
 #!/bin/bash
-# Long A/B over named arms (150 timed steps after 50 warm-up, headline leg, arms alternating for 3
-# rounds on one box).  An arm is NAME or NAME=ENV...: NAME alone loads lib/variants/libhlc_NAME.so
-# (default: the shipped lib); NAME=ENV runs the shipped lib under that env (e.g. notail=HLC_REC_TAIL=0).
-# Names starting with probe/nofence/norel mark timing probes (HLC_BENCH_PROBE=1 skips the guard).
+# A/B over named arms, arms alternating for 3 rounds on one box.
+#   bash tools/ab_arms.sh ARM [ARM ...]           (the shipped library runs as arm "default" first)
+# An arm is NAME or NAME=ENV...: NAME alone loads lib/variants/libhlc_NAME.so (make variant NAME=...);
+# NAME=ENV runs the shipped lib under that env (e.g. one=HLC_SPLIT_VOTES=0).  Names starting with
+# probe/nofence/norel mark timing probes (HLC_BENCH_PROBE=1 skips bench.py's outcome guard).
+# AB_MODE selects what each arm runs:
+#   headline (default)  bench.py headline leg, 150 timed steps after 50 warm-up
+#   legs                bench.py headline + config-5 legs, 20 steps
+#   host                tools/host_pipe.py (host-buffer entry, default schedule, 8 host threads), 20 calls
+#                       (host_pipe.py sets HLC_SPLIT_VOTES / HLC_HOST_THREADS itself: vary those with its flags)
 set -o pipefail
 mkdir -p gpurun_out
+MODE=${AB_MODE:-headline}
 LEGS="--no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e"
 for round in 1 2 3; do
   for arm in default "$@"; do
@@ -12,7 +19,19 @@ for round in 1 2 3; do
     if [ "$arm" != "$v" ]; then ENVS="${arm#*=}"
     elif [ "$v" != default ]; then ENVS="HLC_LIB=$PWD/hashgraph-like-consensus_amd/lib/variants/libhlc_$v.so"; fi
     case $v in probe*|nofence*|norel*) ENVS="$ENVS HLC_BENCH_PROBE=1";; esac
-    env $ENVS timeout -k 10 200 python bench.py --steps 150 --warmup 50 $LEGS > gpurun_out/aba_$v.json 2> gpurun_out/aba_$v.err || { tail gpurun_out/aba_$v.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/aba_$v.json'));print('$round $v', round(d['value']), 'votes/s rec_ms', round(d['roofline']['kernel_ms_avg'],3), 'step_ms', round(d['ms_per_step'],3))"
+    O=gpurun_out/ab_${MODE}_$v
+    case $MODE in
+    headline)
+      env $ENVS timeout -k 10 200 python bench.py --steps 150 --warmup 50 $LEGS > $O.json 2> $O.err || { tail $O.err; exit 1; }
+      python -c "import json;d=json.load(open('$O.json'));print('$round $v', round(d['value']), 'votes/s rec_ms', round(d['roofline']['kernel_ms_avg'],3), 'step_ms', round(d['ms_per_step'],3))" ;;
+    legs)
+      env $ENVS timeout -k 10 300 python bench.py --steps 20 --warmup 5 ${LEGS/--no-config5/} > $O.json 2> $O.err || { tail $O.err; exit 1; }
+      python -c "import json;d=json.load(open('$O.json'));print('$round $v headline', round(d['value']), 'config5', round(d['config5']['value']), 'votes/s')" ;;
+    host)
+      env $ENVS timeout -k 10 200 python tools/host_pipe.py --threads 8 --steps 20 > $O.txt 2> $O.err || { tail $O.err; exit 1; }
+      python -c "import json;d=json.loads(open('$O.txt').read().splitlines()[-1]);print('$round $v host', round(d['votes_per_s']), 'votes/s', round(d['ms_per_call'],3), 'ms')" ;;
+    *)
+      echo "unknown AB_MODE $MODE"; exit 2 ;;
+    esac
   done
 done

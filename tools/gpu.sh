@@ -14,7 +14,8 @@
 #   pipetrace  rocprofv3 kernel + memory-copy trace of one host-buffer setting ($PIPE_ARGS)
 #   verify     tools/verify_latency.py (hlc_eth_verify_batch at the C ABI)
 #   profile    tools/profile.sh TAG (kernel trace + PMC passes of the headline leg)
-#   ab         tools/ab_arms.sh $AB_ARMS (alternating A/B arms: lib/variants builds or env settings)
+#   ab         tools/ab_arms.sh $AB_ARMS (alternating A/B arms: lib/variants builds or env settings;
+#              $AB_MODE = headline / legs / host)
 #   clock      tools/clock_probe.py over the HLC_CLOCK_PROBE builds in $CLOCK_VARIANTS, two alternating rounds
 set -o pipefail
 TAG=$1
