@@ -960,21 +960,22 @@ bool stage_sigs(Staging& st, HostPool& pool, const uint8_t* bytes, uint64_t byte
 // The caller's votes go to the device through page-locked staging on the context's upload stream,
 // ordered by what the kernels need first, so that the VALU-bound recovery starts long before the
 // whole batch has landed:
-//   1. per recovery range of split_ranges(n) (small ones first), the votes' signatures gathered
+//   1. per recovery range of split_ranges(n) (growing sizes), the votes' signatures gathered
 //      into a dense array (65 B per vote) with their lengths; behind each range's upload, its
 //      k_rec_prep + k_rec_main on the two aux streams in turn (each with its own per-lane scratch),
-//      so range k's grid waves take the SIMD slots range k-1's waves free (one grid tail per call,
-//      as in the device-resident call), and every range's signatures are on the device after
-//      ~69 B per vote of DMA;
+//      so range k's grid waves take the SIMD slots range k-1's waves free (the ranges' grid tails
+//      overlap the next range's work), and every range's signatures are on the device after ~69 B
+//      per vote of DMA;
 //   2. every other input (SoA arrays, proposals, the byte arena) in rest_pieces() pieces, each
 //      copied into page-locked memory by the host pool (every field's (offset, length) checked on
 //      the way) while the previous piece's DMA runs -> once they have landed, the prehash, chain /
-//      duplicate / YES kernels on the launch stream, each range's finish (u1 G, Z^-1, address) after
-//      its main stage, the statuses, tables, finalize, and one D2H of every output into page-locked
-//      memory.
+//      duplicate / YES kernels on the launch stream, one recovery finish (u1 G, Z^-1, address) after
+//      the last main stage, the statuses, tables, finalize, and one D2H of every output into
+//      page-locked memory.
 // An array the caller holds in page-locked memory (hlc_host_alloc) is uploaded straight from there
-// (the signatures are still gathered).  A field outside the arena returns HLC_EINVAL before anything
-// reaches the caller's outputs (device work already enqueued is drained and discarded).  Only
+// (the signatures are still gathered).  A field outside the arena returns HLC_EINVAL before any
+// kernel that reads it is enqueued and before anything reaches the caller's outputs (the recovery
+// ranges already in flight are drained and discarded).  Only
 // stream / event dependencies order the stages: no kernel waits on a flag, so any mapping of the
 // streams onto hardware queues is correct (one that serialises them is only slower).
 int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint64_t now,
@@ -1060,6 +1061,14 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
     }));
     CHK(stage_span(st, pool, v->bytes, arena_pinned, o[9], blen * k / K, blen * (k + 1) / K));
   }
+  // a field outside the arena: nothing that reads the fields is enqueued (the recovery ranges
+  // already in flight read only the signatures, checked when they were gathered)
+  for (int x : bad) {
+    if (x) {
+      st.drain();
+      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
+    }
+  }
   tr.mark("rest_staged");
   HIPCHK(hipEventRecord(c->ev_rest, c->copy));
   tr.ev("rest_landed", c->copy);
@@ -1085,12 +1094,6 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   HIPCHK(hipEventRecord(c->ev_done, s));
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
-  for (int x : bad) {
-    if (x) {
-      st.drain();
-      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-    }
-  }
   HIPCHK(hipEventSynchronize(c->ev_done));
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);
@@ -1184,6 +1187,12 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
     }));
     CHK(stage_span(st, pool, bytes, arena_pinned, o[6], blen * k / K, blen * (k + 1) / K));
   }
+  for (int x : bad) {  // nothing that reads identities / payloads is enqueued
+    if (x) {
+      st.drain();
+      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
+    }
+  }
   tr.mark("rest_staged");
   HIPCHK(hipEventRecord(c->ev_rest, c->copy));
   tr.ev("rest_landed", c->copy);
@@ -1208,12 +1217,6 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   HIPCHK(hipEventRecord(c->ev_done, s));
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
-  for (int x : bad) {
-    if (x) {
-      st.drain();
-      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
-    }
-  }
   HIPCHK(hipEventSynchronize(c->ev_done));
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);

@@ -120,13 +120,17 @@ def _raw_call(engine, batch, desc, now, split):
     return rc, (res.view(np.uint8), st, rs, rec)
 
 
-@pytest.mark.parametrize("field,where", [(4, "second range"), (2, "late piece"), (0, "late piece")])
-def test_gpu_host_entry_rejects_bad_field_outputs_untouched(engine, byz, field, where):
+@pytest.mark.parametrize("field,where,far", [(4, "second range", False), (2, "late piece", False),
+                                             (0, "late piece", False), (4, "second range", True),
+                                             (1, "late piece", True), (3, "late piece", True)])
+def test_gpu_host_entry_rejects_bad_field_outputs_untouched(engine, byz, field, where, far):
+    """far: an offset of 2^40, which a kernel reading the field would fault on -- the check must come
+    before any kernel that reads the field is enqueued."""
     b, d, now = byz
     off = b.field_off.copy()
     # a vote in the second recovery range and in the last staging piece whose field is non-empty
     i = max(j for j in range(b.n - 20, b.n) if int(b.field_len[j, field]) > 0)
-    off[i, field] = b.arena.size + 10
+    off[i, field] = (1 << 40) if far else b.arena.size + 10
     bad = b.__class__(b.vote_id, b.proposal_id, b.timestamp, b.vote, b.arena, off, b.field_len)
     rc, outs = _raw_call(engine, bad, d, now, 100)
     assert rc == HLC_EINVAL, where

@@ -167,9 +167,10 @@ def test_gpu_verify_batch_rejects_out_of_arena_outputs_untouched(engine):
     lens = np.array([len(x) for x in ids + pays + sigs], np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
     n = len(ids)
-    for which in (0, 1, 2):  # identity, payload, signature of the last item
+    for which, far in ((0, False), (1, False), (2, False), (0, True), (1, True), (2, True)):
+        # identity, payload, signature of the last item; far: 2^40, which a kernel would fault on
         o = offs.copy()
-        o[which * n + n - 1] = arena.size + 1
+        o[which * n + n - 1] = (1 << 40) if far else arena.size + 1
         st = np.full(n, 0xAB, np.uint8)
         addr = np.full((n, 20), 0xAB, np.uint8)
         os.environ["HLC_SPLIT_VOTES"] = "100"
