@@ -286,7 +286,10 @@ int hlc_outcome_counts_device(hlc_ctx* ctx, const uint8_t* vote_status, uint64_t
  * resident in HBM (bench.py).  The recovery's signature-only stage runs on a second stream the
  * context owns, forked from and joined back into `stream` by events.  A context's workspace
  * serves one call at a time: successive calls on one context must be ordered (the same stream,
- * or the caller's own synchronisation between streams). */
+ * or the caller's own synchronisation between streams).  Every field's (offset, length) must lie
+ * inside votes->bytes[0, bytes_len): the device entry reads them without a host-side check (the
+ * host-buffer entry checks every one and returns HLC_EINVAL; the device decoders and generators
+ * only produce in-arena fields). */
 int hlc_validate_proposals_device(hlc_ctx* ctx, const hlc_votes* votes,
                                   const hlc_proposal* proposals, uint64_t n_proposals,
                                   uint64_t now, hlc_result* out_results,
