@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -94,11 +95,14 @@ struct PBuf {
 };
 
 // A small host worker pool for the host-buffer entries' field checks and staging copies: run(fn) calls
-// fn(part, parts) for every part on the workers and the calling thread and returns when all are done.
+// fn(chunk, chunks()) once for every chunk, on the workers and the calling thread, and returns when all
+// are done.  Threads take chunks (4 per thread) from a shared counter, so a thread the OS holds back
+// (the box's CPU quota is shared with the caller's own threads) delays one chunk, not 1/threads of
+// the job.
 class HostPool {
  public:
   explicit HostPool(int workers) {
-    for (int i = 0; i < workers; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
   }
   ~HostPool() {
     {
@@ -108,23 +112,30 @@ class HostPool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  int parts() const { return (int)th_.size() + 1; }
+  int threads() const { return (int)th_.size() + 1; }
+  int chunks() const { return 4 * threads(); }
   void run(const std::function<void(int, int)>& fn) {
     {
       std::lock_guard<std::mutex> l(m_);
       fn_ = &fn;
+      next_.store(0, std::memory_order_relaxed);
       pending_ = (int)th_.size();
       ++gen_;
     }
     cv_.notify_all();
-    fn(0, parts());
+    work(fn);
     std::unique_lock<std::mutex> l(m_);
     done_.wait(l, [&] { return pending_ == 0; });
     fn_ = nullptr;
   }
 
  private:
-  void loop(int part) {
+  void work(const std::function<void(int, int)>& fn) {
+    const int C = chunks();
+    for (int k = next_.fetch_add(1, std::memory_order_relaxed); k < C; k = next_.fetch_add(1, std::memory_order_relaxed))
+      fn(k, C);
+  }
+  void loop() {
     uint64_t seen = 0;
     for (;;) {
       const std::function<void(int, int)>* f;
@@ -135,11 +146,12 @@ class HostPool {
         seen = gen_;
         f = fn_;
       }
-      (*f)(part, parts());
+      work(*f);
       std::lock_guard<std::mutex> l(m_);
       if (--pending_ == 0) done_.notify_one();
     }
   }
+  std::atomic<int> next_{0};
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_;
@@ -758,7 +770,7 @@ int host_resources(hlc_ctx* c) {
   if (!c->aux2) HIPCHK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, least));
   for (hipEvent_t* e : {&c->ev_rest, &c->ev_done})
     if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  if (!c->pool || c->pool->parts() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
+  if (!c->pool || c->pool->threads() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
   CHK(ensure_recover_scratch(c));
   CHK(c->rec_scratch2.ensure(c->rec_lanes * hlc::recover_scratch_words() * sizeof(uint32_t)));
   return 0;
@@ -932,7 +944,7 @@ bool stage_sigs(Staging& st, HostPool& pool, const uint8_t* bytes, uint64_t byte
                 const uint32_t* sig_len, size_t stride, size_t o_sig, size_t o_len, uint64_t a0, uint64_t a1,
                 int* rc) {
   const uint64_t m = a1 - a0;
-  std::vector<int> bad(pool.parts(), 0);
+  std::vector<int> bad(pool.chunks(), 0);
   pool.run([&](int t, int T) {
     const uint64_t b0 = a0 + m * t / T, b1 = a0 + m * (t + 1) / T;
     uint8_t* sg = st.P + o_sig;
@@ -1017,7 +1029,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
   const uint8_t* D = st.D;
-  const int parts = pool.parts();
+  const int parts = pool.chunks();
   std::vector<RecFront> fronts;
   for (size_t k = 0; k + 1 < rb.size(); ++k) {
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
@@ -1148,7 +1160,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
   const uint8_t* D = st.D;
-  const int parts = pool.parts();
+  const int parts = pool.chunks();
   std::vector<RecFront> fronts;
   for (size_t k = 0; k + 1 < rb.size(); ++k) {
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
