@@ -206,7 +206,7 @@ typedef struct hlc_ctx hlc_ctx;
  * largest batch) are allocated on first use (or hlc_ctx_reserve).
  * The host-buffer entries (hlc_validate_proposals, hlc_eth_verify_batch) add on their first call:
  * a second per-lane recovery workspace (~205 MB; their recovery ranges alternate over two streams),
- * the per-vote records of each recovery range (~0.3 KB per vote), page-locked staging of the
+ * each recovery range's work list and prefix products (~0.15 KB per vote), page-locked staging of the
  * inputs (the call's input bytes + 69 B per vote of dense signatures) and of the outputs, and a
  * device copy of each; all are kept for later calls of the same or smaller size. */
 int hlc_ctx_create(int device, hlc_ctx** out);
