@@ -1,0 +1,59 @@
+"""Randomised schedules of the host-buffer entries (hlc_api.cpp validate_host / verify_host): for a
+Byzantine batch, random proposal subsets in random order, random recovery ranges
+(HLC_SPLIT_VOTES), staging pieces (HLC_REST_PIECES), first-range prep batches (HLC_FIRST_BATCH)
+and host pool sizes (HLC_HOST_THREADS) must give exactly the single-range result -- itself pinned to
+the C oracle in test_gpu_host_pipeline.py -- and, for a sample of the settings, the oracle again."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import coracle
+from adversarial import byzantine
+from helpers import oracle_workload
+
+pytestmark = pytest.mark.gpu
+KNOBS = ("HLC_SPLIT_VOTES", "HLC_REST_PIECES", "HLC_FIRST_BATCH", "HLC_HOST_THREADS")
+
+
+def _call(engine, batch, desc, now, env):
+    old = {k: os.environ.get(k) for k in KNOBS}
+    os.environ.update(env)
+    try:
+        return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def big_byz():
+    w = oracle_workload(120, 24, 24, True, 0x484C4360, name="fuzz")
+    b, d, _ = byzantine(w, fraction=1 / 4, seed=0x60)
+    return b, d, w.now
+
+
+def test_gpu_host_entry_random_schedules(engine, big_byz):
+    b, d, now = big_byz
+    rnd = random.Random(0x484C)
+    for trial in range(16):
+        p0 = rnd.randrange(0, d.shape[0] - 1)
+        p1 = rnd.randrange(p0 + 1, d.shape[0] + 1)
+        sub = d[p0:p1].copy()
+        if rnd.random() < 0.5:
+            sub = sub[np.array(rnd.sample(range(sub.shape[0]), sub.shape[0]))]
+        sizes = [rnd.choice([1, 7, 64, 65, 100, 333, 640, 1000]) for _ in range(rnd.randrange(1, 4))]
+        env = {"HLC_SPLIT_VOTES": ",".join(map(str, sizes)), "HLC_REST_PIECES": str(rnd.randrange(1, 9)),
+               "HLC_FIRST_BATCH": str(rnd.randrange(1, 9)), "HLC_HOST_THREADS": str(rnd.randrange(1, 13))}
+        ref = _call(engine, b, sub, now, {"HLC_SPLIT_VOTES": "0"})
+        got = _call(engine, b, sub, now, env)
+        for x, y in zip(ref, got):
+            assert np.array_equal(x, y), (trial, env, p0, p1)
+        if trial % 5 == 0:
+            cres, cvst, cvrs, crec = coracle.validate_proposals(b, sub, now, threads=8)
+            assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst), (trial, env)
+            assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec), (trial, env)
