@@ -57,3 +57,29 @@ def test_gpu_host_entry_random_schedules(engine, big_byz):
             cres, cvst, cvrs, crec = coracle.validate_proposals(b, sub, now, threads=8)
             assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst), (trial, env)
             assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec), (trial, env)
+
+
+def test_gpu_verify_batch_random_schedules(engine):
+    """hlc_eth_verify_batch under random ranges / pieces / first-range batch / pool size: every item
+    equals the oracle (adversarial items: bad lengths, high s, bad v, no point, wrong key)."""
+    from test_gpu_parity import _mutated_items, _oracle_verify
+    ids, pays, sigs = _mutated_items(900, 0x61)
+    exp_st, exp_addr = _oracle_verify(ids, pays, sigs)
+    rnd = random.Random(0x61)
+    for trial in range(10):
+        n = rnd.randrange(1, len(ids) + 1)
+        sizes = [rnd.choice([1, 5, 64, 100, 257]) for _ in range(rnd.randrange(1, 4))]
+        env = {"HLC_SPLIT_VOTES": ",".join(map(str, sizes)), "HLC_REST_PIECES": str(rnd.randrange(1, 9)),
+               "HLC_FIRST_BATCH": str(rnd.randrange(1, 9)), "HLC_HOST_THREADS": str(rnd.randrange(1, 13))}
+        old = {k: os.environ.get(k) for k in KNOBS}
+        os.environ.update(env)
+        try:
+            st, addr = engine.eth_verify_batch(ids[:n], pays[:n], sigs[:n])
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        assert [int(x) for x in st] == exp_st[:n], (trial, env, n)
+        assert [a.tobytes() for a in addr] == exp_addr[:n], (trial, env, n)
