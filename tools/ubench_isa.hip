@@ -126,6 +126,43 @@ __global__ void k_mix_col(uint32_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3) ^ l0 ^ l1 ^ l2 ^ l3;
 }
 
+// the same mix with the 29-bit mask in a VGPR (%10) instead of a literal
+__global__ void k_mix_col_vmask(uint32_t* out, uint32_t seed) {
+  uint64_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;
+  uint32_t l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+  uint32_t b = seed | 1, c = seed * 3u + 7u, mask = 0x1fffffffu ^ (seed & 0x40000000u);
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+        "v_mad_u64_u32 %0, s[0:1], %8, %9, %0\n v_mad_u64_u32 %1, s[0:1], %8, %9, %1\n"
+        "v_mad_u64_u32 %2, s[0:1], %8, %9, %2\n v_mad_u64_u32 %3, s[0:1], %8, %9, %3\n"
+        "v_and_b32 %4, %10, %4\n v_and_b32 %5, %10, %5\n"
+        "v_add_u32 %6, %6, %8\n v_add_u32 %7, %7, %8\n"
+        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3)
+        : "v"(b), "v"(c), "v"(mask)
+        : "s0", "s1");
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3) ^ l0 ^ l1 ^ l2 ^ l3;
+}
+
+// v_mad_u64_u32 with one SGPR source (a wave-uniform constant, as in the field layer's folds)
+__global__ void k_mad64_sgpr(uint32_t* out, uint32_t seed) {
+  uint64_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+           a7 = a0 + 7;
+  uint32_t b = seed | 1;
+  for (int i = 0; i < ITERS; ++i) {
+    asm volatile(
+        "s_mov_b32 s2, 31264\n"
+        "v_mad_u64_u32 %0, s[0:1], %8, s2, %0\n v_mad_u64_u32 %1, s[0:1], %8, s2, %1\n"
+        "v_mad_u64_u32 %2, s[0:1], %8, s2, %2\n v_mad_u64_u32 %3, s[0:1], %8, s2, %3\n"
+        "v_mad_u64_u32 %4, s[0:1], %8, s2, %4\n v_mad_u64_u32 %5, s[0:1], %8, s2, %5\n"
+        "v_mad_u64_u32 %6, s[0:1], %8, s2, %6\n v_mad_u64_u32 %7, s[0:1], %8, s2, %7\n"
+        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+        : "v"(b)
+        : "s0", "s1", "s2");
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
+}
+
 __global__ void k_clock(unsigned long long* out) {
   unsigned long long t0 = clock64();
   unsigned long long w0 = wall_clock64();
@@ -206,6 +243,8 @@ int main() {
   rc |= run("add_f64", k_addf64, d);
   rc |= run("fma_f64", k_fmaf64, d);
   rc |= run("mix4mad+4cheap", k_mix_col, d);
+  rc |= run("mix4mad+4cheap vmask", k_mix_col_vmask, d);
+  rc |= run("mad_u64_u32 sgpr", k_mad64_sgpr, d);
   CHECK(hipFree(d));
   return rc;
 }
