@@ -144,6 +144,29 @@ __global__ void k_mix_col_vmask(uint32_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3) ^ l0 ^ l1 ^ l2 ^ l3;
 }
 
+// grouping: 8 mads then 8 cheap ops (ands / adds on other registers) vs mad / cheap alternating
+#define MIXK(NAME, BODY)                                                                            \
+  __global__ void NAME(uint32_t* out, uint32_t seed) {                                              \
+    uint64_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, \
+             a6 = a0 + 6, a7 = a0 + 7;                                                              \
+    uint32_t l0 = 0, l1 = 1, l2 = 2, l3 = 3, l4 = 4, l5 = 5, l6 = 6, l7 = 7;                         \
+    uint32_t b = seed | 1, c = seed * 3u + 7u;                                                      \
+    for (int i = 0; i < ITERS; ++i) {                                                               \
+      asm volatile(BODY                                                                             \
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), \
+                     "+v"(l0), "+v"(l1), "+v"(l2), "+v"(l3), "+v"(l4), "+v"(l5), "+v"(l6), "+v"(l7)  \
+                   : "v"(b), "v"(c)                                                                 \
+                   : "s0", "s1");                                                                   \
+    }                                                                                               \
+    out[blockIdx.x * blockDim.x + threadIdx.x] =                                                    \
+        (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7) ^ l0 ^ l1 ^ l2 ^ l3 ^ l4 ^ l5 ^ l6 ^ l7;  \
+  }
+#define M_(k) "v_mad_u64_u32 %" S(k) ", s[0:1], %16, %17, %" S(k) "\n"
+#define A_(k) "v_and_b32 %" S(k) ", 0x1fffffff, %" S(k) "\n"
+MIXK(k_grp8, M_(0) M_(1) M_(2) M_(3) M_(4) M_(5) M_(6) M_(7) A_(8) A_(9) A_(10) A_(11) A_(12) A_(13) A_(14) A_(15))
+MIXK(k_alt8, M_(0) A_(8) M_(1) A_(9) M_(2) A_(10) M_(3) A_(11) M_(4) A_(12) M_(5) A_(13) M_(6) A_(14) M_(7) A_(15))
+MIXK(k_grp2, M_(0) M_(1) A_(8) A_(9) M_(2) M_(3) A_(10) A_(11) M_(4) M_(5) A_(12) A_(13) M_(6) M_(7) A_(14) A_(15))
+
 // v_mad_u64_u32 with one SGPR source (a wave-uniform constant, as in the field layer's folds)
 __global__ void k_mad64_sgpr(uint32_t* out, uint32_t seed) {
   uint64_t a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
@@ -245,6 +268,9 @@ int main() {
   rc |= run("mix4mad+4cheap", k_mix_col, d);
   rc |= run("mix4mad+4cheap vmask", k_mix_col_vmask, d);
   rc |= run("mad_u64_u32 sgpr", k_mad64_sgpr, d);
+  rc |= run("8 mad, 8 and", k_grp8, d, 16);
+  rc |= run("mad/and alternating", k_alt8, d, 16);
+  rc |= run("2 mad, 2 and", k_grp2, d, 16);
   CHECK(hipFree(d));
   return rc;
 }
