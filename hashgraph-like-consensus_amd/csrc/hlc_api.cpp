@@ -1680,6 +1680,7 @@ int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_
   if (!ctx || (n && (!id_off || !id_len || !payload_off || !payload_len || !sig_off || !sig_len || !out_status)))
     return set_err(HLC_EINVAL, "NULL argument");
   if (!n) return 0;
+  if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many items in one call (max 2^32-16)");
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
   return verify_host(ctx, n, bytes, bytes_len, id_off, id_len, payload_off, payload_len, sig_off, sig_len, out_status,

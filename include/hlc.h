@@ -250,7 +250,9 @@ int hlc_compute_vote_hashes(hlc_ctx* ctx, const hlc_votes* votes, uint8_t* out_h
  * `ConsensusSignatureScheme::verify` of signing.rs:69-73, over a batch of n items.
  * Item i: identity = bytes[id_off[i] .. +id_len[i]], payload likewise, signature likewise.
  * out_status[i] = HLC_VERIFY_TRUE / HLC_VERIFY_FALSE / 1 + HLC_SCHEME_* (Err).
- * out_addr (optional, n*20) receives the recovered address when one exists. */
+ * out_addr (optional, n*20) receives the recovered address when one exists.  At most 2^32 - 16
+ * items per call; an item whose (offset, length) leaves the arena returns HLC_EINVAL with the
+ * outputs untouched. */
 int hlc_eth_verify_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* bytes, uint64_t bytes_len,
                          const uint64_t* id_off, const uint32_t* id_len,
                          const uint64_t* payload_off, const uint32_t* payload_len,
