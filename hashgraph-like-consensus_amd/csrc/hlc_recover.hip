@@ -143,9 +143,12 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t st, 
 
 // ---- main: decompress + u2 R, one vote per lane at a time (persistent grid) ----
 // Needs only the prep stage's records and the signatures, not the prehash: it runs beside the
-// prehash kernels (hlc_api.cpp vote_stage), on every vote with a parsed 65-byte signature (the
-// pre-checks' verdicts are not known yet; k_rec_comb discards the votes they reject).
-// Work is handed out dynamically, 64 consecutive votes per wave per grab (one atomic by lane 0).
+// prehash kernels (hlc_api.cpp vote_stage), on the votes k_rec_prep listed -- every parsed 65-byte
+// signature whose vote the checks before the signature do not reject (validate-many passes them;
+// the vote-hash check needs the prehash, so a vote it rejects is still recovered and k_rec_comb
+// discards it).  Records: row stride `st` (the call's vote count; a host-buffer range's pointers
+// start at its first vote).
+// Work is handed out dynamically, 64 listed votes per wave per grab (one atomic by lane 0).
 // The SIMD's arbiter favours its oldest wave, so with a static vote-per-lane stride the oldest of
 // the 3 resident waves finishes its share long before the youngest, which then runs alone at
 // lone-wave efficiency (measured with HLC_CLOCK_PROBE: 4-vote blocks done at 3.5 ms, the last
