@@ -664,7 +664,7 @@ def main() -> int:
         step()
     torch.cuda.synchronize()
     # guard: every synthetic vote is valid, every proposal validates (no silent breakage).  Timing
-    # probe builds that compute wrong results on purpose (HLC_PROBE_* variants, tools/) set
+    # probe builds that compute wrong results on purpose (timing probes built with make variant) set
     # HLC_BENCH_PROBE=1, which skips the guard and marks the line as a probe.
     probe = os.environ.get("HLC_BENCH_PROBE") == "1"
     res = db.results_numpy()
