@@ -470,6 +470,36 @@ def e2e_leg(eng, w, args, np, pinned=False):
     }
 
 
+def e2e_leg_sharded(eng, db, args, np, torch, dist, coll_dev, world):
+    """Secondary line at N > 1 (end-to-end at 1/2/4/8 GPUs): every rank's shard
+    through the host-buffer entry hlc_validate_proposals (its own votes copied to the host once,
+    before timing: what a rank holding its shard in host memory sees), the same barrier + max-over-
+    ranks timing as the headline, value = the votes all ranks processed / that time."""
+    b, d, _ = db.to_host()
+    eng.validate_proposals(b, d, db.now, want_votes=True)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, vst, _, _ = eng.validate_proposals(b, d, db.now, want_votes=True)
+    el = time.perf_counter() - t0
+    ok = bool((vst == 0).all() and (res["status"] == 0).all())
+    t = torch.tensor([el, 0.0 if ok else 1.0], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    nt = torch.tensor([b.n], dtype=torch.int64, device=coll_dev)
+    dist.all_reduce(nt)
+    assert float(t[1].item()) == 0.0, "a rank's host-buffer results differ from the expected outcomes"
+    el = float(t[0].item())
+    return {
+        "metric": "verified votes/s, host buffers in and out (PCIe-inclusive hlc_validate_proposals), every rank's "
+                  "shard, pageable inputs",
+        "value": int(nt.item()) * args.steps / el,
+        "unit": "votes/s",
+        "n_gpus": world,
+        "ms_per_call": el / args.steps * 1e3,
+        "votes_per_call_per_gpu": int(b.n),
+    }
+
+
 def config3_leg(eng, args, torch, synth, DeviceBatch, dev, ct):
     """Secondary line, SURVEY.md §8(d) config 3: one P2P proposal of 1,000,000 chained votes
     (n = 1.5M, so the ceil(2n/3) round cap is exactly 1M), generated on the device: the global
@@ -821,6 +851,8 @@ def main() -> int:
     if w is not None and not args.no_e2e:
         out["end_to_end"] = e2e_leg(eng, w, args, np)
         out["end_to_end_pinned"] = e2e_leg(eng, w, args, np, pinned=True)
+    if dist is not None and not args.no_e2e:
+        out["end_to_end"] = e2e_leg_sharded(eng, db, args, np, torch, dist, coll_dev, world)
     if w is not None and not args.no_stream:
         out["stream"] = stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch)
     if world == 1 and not args.no_config3:
