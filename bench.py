@@ -474,20 +474,39 @@ def e2e_leg_sharded(eng, db, args, np, torch, dist, coll_dev, world):
     """Secondary line at N > 1 (end-to-end at 1/2/4/8 GPUs): every rank's shard
     through the host-buffer entry hlc_validate_proposals (its own votes copied to the host once,
     before timing: what a rank holding its shard in host memory sees), the same barrier + max-over-
-    ranks timing as the headline, value = the votes all ranks processed / that time."""
-    b, d, _ = db.to_host()
-    eng.validate_proposals(b, d, db.now, want_votes=True)
+    ranks timing as the headline, value = the votes all ranks processed / that time.  A failure on
+    any rank (host memory, page-locked staging) is reported in the line instead of ending the run:
+    every rank still takes part in the same collectives, so no rank is left waiting."""
+    def agree(flag: bool) -> bool:  # True when every rank's flag is True
+        t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    err = None
+    try:
+        b, d, _ = db.to_host()
+        eng.validate_proposals(b, d, db.now, want_votes=True)
+    except Exception as e:  # noqa: BLE001 -- reported in the line
+        err = f"{type(e).__name__}: {e}"
+    if not agree(err is None):
+        return {"metric": "end-to-end (host-buffer) leg", "error": err or "failed on another rank"}
     dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res, vst, _, _ = eng.validate_proposals(b, d, db.now, want_votes=True)
-    el = time.perf_counter() - t0
-    ok = bool((vst == 0).all() and (res["status"] == 0).all())
+    el, ok = 0.0, False
+    try:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res, vst, _, _ = eng.validate_proposals(b, d, db.now, want_votes=True)
+        el = time.perf_counter() - t0
+        ok = bool((vst == 0).all() and (res["status"] == 0).all())
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"
     t = torch.tensor([el, 0.0 if ok else 1.0], dtype=torch.float64, device=coll_dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     nt = torch.tensor([b.n], dtype=torch.int64, device=coll_dev)
     dist.all_reduce(nt)
-    assert float(t[1].item()) == 0.0, "a rank's host-buffer results differ from the expected outcomes"
+    if float(t[1].item()) != 0.0:
+        return {"metric": "end-to-end (host-buffer) leg",
+                "error": err or "a rank's host-buffer results differ from the expected outcomes"}
     el = float(t[0].item())
     return {
         "metric": "verified votes/s, host buffers in and out (PCIe-inclusive hlc_validate_proposals), every rank's "

@@ -16,7 +16,8 @@ def main() -> None:
                 parts.append(f"rec {rf['kernel_ms_avg']:.3f} ms frac {rf['frac']:.3f}")
             for k in ("wire", "end_to_end", "end_to_end_pinned", "stream", "config3", "config5"):
                 if k in d:
-                    parts.append(f"{k} {d[k]['value'] / 1e6:.1f} M")
+                    v = d[k].get("value")
+                    parts.append(f"{k} {v / 1e6:.1f} M" if v is not None else f"{k} error: {d[k].get('error')}")
             if "cpu_baseline" in d:
                 parts.append(f"cpu {d['cpu_baseline']['value'] / 1e3:.1f} k")
             if "gathered_results" in d:
