@@ -470,6 +470,62 @@ def e2e_leg(eng, w, args, np, pinned=False):
     }
 
 
+def e2e_leg_concurrent(eng, w, args, np, contexts: int = 3, threads: int = 4):
+    """Secondary line: the host-buffer entry with `contexts` callers at once, one context and one
+    thread each, every thread calling back to back on the same workload (include/hlc.h: one context
+    per thread for concurrency) -- an embedder validating several proposal batches in parallel.  One
+    call's lead-in (its first signatures' gather and upload) and its tail run beside the others'
+    recovery, so the aggregate approaches the device-resident rate.  Aggregate votes/s over the
+    slowest thread's time."""
+    import threading
+
+    from hashgraph_like_consensus.engine import Engine
+    b, d = w.batch, w.desc
+    old = os.environ.get("HLC_HOST_THREADS")
+    os.environ["HLC_HOST_THREADS"] = str(threads)
+    engs = [eng] + [Engine(eng.device) for _ in range(contexts - 1)]
+    try:
+        for e in engs:
+            e.validate_proposals(b, d, w.now, want_votes=True)
+        go = threading.Barrier(contexts + 1)
+        times = [0.0] * contexts
+        bad = []
+
+        def work(k):
+            go.wait()
+            t = time.perf_counter()
+            for _ in range(args.steps):
+                res, vst, _, _ = engs[k].validate_proposals(b, d, w.now, want_votes=True)
+            times[k] = time.perf_counter() - t
+            if not ((vst == 0).all() and (res["status"] == 0).all()):
+                bad.append(k)
+
+        th = [threading.Thread(target=work, args=(k,)) for k in range(contexts)]
+        for x in th:
+            x.start()
+        go.wait()
+        for x in th:
+            x.join()
+        assert not bad, f"contexts {bad}: results differ from the expected outcomes"
+        el = max(times)
+    finally:
+        for e in engs[1:]:
+            e.close()
+        if old is None:
+            os.environ.pop("HLC_HOST_THREADS", None)
+        else:
+            os.environ["HLC_HOST_THREADS"] = old
+    return {
+        "metric": "verified votes/s, host buffers in and out (PCIe-inclusive hlc_validate_proposals), "
+                  f"{contexts} callers at once (one context + one thread each, {threads} staging threads per "
+                  "context), aggregate",
+        "value": contexts * args.steps * b.n / el,
+        "unit": "votes/s",
+        "contexts": contexts,
+        "ms_per_call": el / args.steps * 1e3,
+    }
+
+
 def e2e_leg_sharded(eng, db, args, np, torch, dist, coll_dev, world):
     """Secondary line at N > 1 (end-to-end at 1/2/4/8 GPUs): every rank's shard
     through the host-buffer entry hlc_validate_proposals (its own votes copied to the host once,
@@ -870,6 +926,7 @@ def main() -> int:
     if w is not None and not args.no_e2e:
         out["end_to_end"] = e2e_leg(eng, w, args, np)
         out["end_to_end_pinned"] = e2e_leg(eng, w, args, np, pinned=True)
+        out["end_to_end_concurrent"] = e2e_leg_concurrent(eng, w, args, np)
     if dist is not None and not args.no_e2e:
         out["end_to_end"] = e2e_leg_sharded(eng, db, args, np, torch, dist, coll_dev, world)
     if w is not None and not args.no_stream:

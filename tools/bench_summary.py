@@ -14,7 +14,7 @@ def main() -> None:
             rf = d.get("roofline", {})
             if rf.get("kernel_ms_avg"):
                 parts.append(f"rec {rf['kernel_ms_avg']:.3f} ms frac {rf['frac']:.3f}")
-            for k in ("wire", "end_to_end", "end_to_end_pinned", "stream", "config3", "config5"):
+            for k in ("wire", "end_to_end", "end_to_end_pinned", "end_to_end_concurrent", "stream", "config3", "config5"):
                 if k in d:
                     v = d[k].get("value")
                     parts.append(f"{k} {v / 1e6:.1f} M" if v is not None else f"{k} error: {d[k].get('error')}")

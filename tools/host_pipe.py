@@ -42,6 +42,9 @@ def main() -> int:
     ap.add_argument("--proposals", type=int, default=10_000)
     ap.add_argument("--pinned", action="store_true", help="the host batch in page-locked memory (hlc_host_alloc)")
     ap.add_argument("--print-trace", default=None, help="print an HLC_HOST_TRACE log as a table and exit")
+    ap.add_argument("--contexts", type=int, default=1,
+                    help="also time this many contexts, one caller thread each, every thread calling back to back "
+                         "(include/hlc.h: one context per thread for concurrency); aggregate votes/s")
     a = ap.parse_args()
     if a.print_trace:
         print_trace(a.print_trace)
@@ -78,6 +81,34 @@ def main() -> int:
         row = {"split": sp, "threads": int(th), "pinned": a.pinned, "ms_per_call": el * 1e3,
                "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in, "outputs_equal_first_setting": True}
         print(json.dumps(row), flush=True)
+    if a.contexts > 1:
+        import threading
+        engs = [eng] + [Engine(0) for _ in range(a.contexts - 1)]
+        for e in engs[1:]:
+            e.validate_proposals(b, d, db.now, want_votes=True)  # warm: workspace, staging, streams
+        go = threading.Barrier(a.contexts + 1)
+        times = [0.0] * a.contexts
+
+        def work(k):
+            go.wait()
+            t = time.perf_counter()
+            for _ in range(a.steps):
+                engs[k].validate_proposals(b, d, db.now, want_votes=True)
+            times[k] = time.perf_counter() - t
+
+        th = [threading.Thread(target=work, args=(k,)) for k in range(a.contexts)]
+        for x in th:
+            x.start()
+        go.wait()
+        for x in th:
+            x.join()
+        el = max(times)
+        print(json.dumps({"contexts": a.contexts, "threads_per_context": int(os.environ["HLC_HOST_THREADS"]),
+                          "split": os.environ["HLC_SPLIT_VOTES"], "calls": a.contexts * a.steps,
+                          "votes_per_s_aggregate": a.contexts * a.steps * b.n / el,
+                          "ms_per_call_mean": el / a.steps * 1e3}), flush=True)
+        for e in engs[1:]:
+            e.close()
     eng.close()
     return 0
 
