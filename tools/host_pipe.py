@@ -37,7 +37,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--split", default="98304,196608", help="'/'-separated HLC_SPLIT_VOTES settings (range sizes "
                     "before the last, e.g. 131072,196608/0; 0 = one recovery range)")
-    ap.add_argument("--threads", default="4", help="HLC_HOST_THREADS settings")
+    ap.add_argument("--threads", default="16", help="HLC_HOST_THREADS settings")
     ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
     ap.add_argument("--proposals", type=int, default=10_000)
     ap.add_argument("--pinned", action="store_true", help="the host batch in page-locked memory (hlc_host_alloc)")
