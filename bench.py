@@ -263,6 +263,33 @@ def _cpu_quota():
     return aff, quota
 
 
+def physical_cores() -> int:
+    """Physical cores of the host (distinct (physical id, core id) pairs of /proc/cpuinfo), not the
+    CPUs this process may use."""
+    try:
+        pairs, phys = set(), None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":")[1].strip()
+                elif line.startswith("core id"):
+                    pairs.add((phys, line.split(":")[1].strip()))
+        return len(pairs) or (os.cpu_count() or 1)
+    except OSError:
+        return os.cpu_count() or 1
+
+
+def whole_host_estimate(single: float, per_thread: float) -> dict:
+    """The CPU baseline scaled to every physical core of the host (keep the whole-host
+    comparison visible beside the quota-bound one): the measured per-thread rate (the slower of the
+    single-thread run and the quota run per thread) x physical cores, no SMT gain assumed."""
+    cores = physical_cores()
+    rate = min(single, per_thread)
+    return {"value": rate * cores, "unit": "votes/s", "physical_cores": cores,
+            "basis": "per-thread rate of this run x physical cores of the host (an estimate: linear scaling, "
+                     "no SMT gain, no memory-bandwidth limit)"}
+
+
 def cpu_baseline(batch, desc, now, sample_proposals: int, single_proposals: int) -> dict:
     """Times the oracle's C restatement (oracle/, the checker) on the host cores: the reference's
     per-vote validate_vote (utils.rs:127-171) with k256's recover + re-verify, on every host thread
@@ -317,6 +344,7 @@ def cpu_baseline(batch, desc, now, sample_proposals: int, single_proposals: int)
         "cgroup_cpu_quota": quota,
         "seconds": dt,
         "single_thread": {"value": v1 / dt1, "unit": "votes/s", "votes": v1, "seconds": dt1},
+        "whole_host_estimate": whole_host_estimate(v1 / dt1, votes / dt / max(threads, 1)),
         "two_pass_rate": {"value": votes / dt2, "unit": "proposal votes/s", "votes": votes, "seconds": dt2,
                           "what": "process_incoming_proposal equivalent: every vote validated twice "
                                   "(validate_proposal + initialize_with_votes, session.rs:203, 284-287)"},
@@ -941,6 +969,7 @@ def main() -> int:
         out["cpu_baseline"] = cpu_baseline(w.batch, w.desc, w.now, min(args.cpu_sample_proposals, P),
                                            min(args.cpu_single_proposals, P))
         out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        out["gpu_over_cpu_whole_host_estimate"] = value / out["cpu_baseline"]["whole_host_estimate"]["value"]
     if probe:
         out["probe"] = "HLC_BENCH_PROBE=1: a timing-probe build, results not checked (not a valid measurement)"
     if rank == 0:
