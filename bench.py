@@ -781,14 +781,22 @@ def main() -> int:
     from hashgraph_like_consensus.parallel import ShardExchange
     ex = ShardExchange(max_p, world, coll_dev, engine=eng)
 
-    def step():
+    ex_events = []  # (start, end) of the exchange on the launch stream, timed steps only
+
+    def step(timed=False):
         eng.validate_proposals_device(db, handle)
         if dist is None:  # one GPU: the same outcome counters, on the device, with no exchange
             with torch.cuda.stream(stream):
                 ex.local_counters(db.results, db.status, P, db.n)
         elif backend == "nccl":
             with torch.cuda.stream(stream):
+                if timed:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
                 ex(db.results, db.status, P, db.n)
+                if timed:
+                    e1.record(stream)
+                    ex_events.append((e0, e1))
         else:
             torch.cuda.synchronize()
             ex(db.results.cpu(), db.status.cpu(), P, db.n)
@@ -814,7 +822,7 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=True)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -835,6 +843,17 @@ def main() -> int:
     if not probe:
         assert counters["verified_votes"] == votes_per_step, "all-reduced verified-vote counter != votes processed"
     gathered_check = None
+    exchange = None
+    if ex_events:
+        # the exchange step's own time on the launch stream (counter kernel + all_gather + all_reduce),
+        # max over ranks: what the collective adds to a step
+        ms = sum(a.elapsed_time(b) for a, b in ex_events) / len(ex_events)
+        t = torch.tensor([ms], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        exchange = {"ms_per_step_max_over_ranks": float(t.item()),
+                    "bytes_gathered_per_step": int(ex.rows.numel()), "bytes_all_reduced_per_step": int(ex.counters.numel() * 8),
+                    "what": "outcome-counter kernel + RCCL all_gather_into_tensor of the 16-B result rows + "
+                            "all_reduce(sum) of the counters, HIP events on the launch stream"}
     if dist is not None:
         # the gathered per-proposal rows: every rank's slice of the all_gather equals that rank's own
         # results, byte for byte; the per-rank verdicts are all-reduced (MIN) so rank 0 reports all
@@ -893,6 +912,7 @@ def main() -> int:
         },
         "counters_per_step": counters,
         **({"gathered_results": gathered_check} if gathered_check is not None else {}),
+        **({"exchange": exchange} if exchange is not None else {}),
         "roofline": {
             "bound": "valu",
             "kernel": "recovery: k_rec_prep + k_rec_main (second stream, beside the prehash) + k_rec_comb + k_rec_final + k_rec_addr (HIP-event brackets)",
