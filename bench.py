@@ -521,12 +521,15 @@ def e2e_leg_concurrent(eng, w, args, np, contexts: int = 3, threads: int = 4):
 
         def work(k):
             go.wait()
-            t = time.perf_counter()
-            for _ in range(args.steps):
-                res, vst, _, _ = engs[k].validate_proposals(b, d, w.now, want_votes=True)
-            times[k] = time.perf_counter() - t
-            if not ((vst == 0).all() and (res["status"] == 0).all()):
-                bad.append(k)
+            try:
+                t = time.perf_counter()
+                for _ in range(args.steps):
+                    res, vst, _, _ = engs[k].validate_proposals(b, d, w.now, want_votes=True)
+                times[k] = time.perf_counter() - t
+                if not ((vst == 0).all() and (res["status"] == 0).all()):
+                    bad.append(k)
+            except Exception as e:  # noqa: BLE001 -- re-raised on the calling thread below
+                bad.append(f"{k}: {type(e).__name__}: {e}")
 
         th = [threading.Thread(target=work, args=(k,)) for k in range(contexts)]
         for x in th:
@@ -534,7 +537,7 @@ def e2e_leg_concurrent(eng, w, args, np, contexts: int = 3, threads: int = 4):
         go.wait()
         for x in th:
             x.join()
-        assert not bad, f"contexts {bad}: results differ from the expected outcomes"
+        assert not bad, f"contexts {bad}: failed or results differ from the expected outcomes"
         el = max(times)
     finally:
         for e in engs[1:]:
