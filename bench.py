@@ -971,28 +971,38 @@ def main() -> int:
     if need_host:
         hb, hd, _ = db.to_host()
         w = synth.Workload(hb, hd, db.now, None, "config%d" % config)
+    def leg(name, fn):
+        """A secondary leg: its failure is reported in the line (with the error) instead of losing
+        the headline; only the headline's guard above ends the run."""
+        try:
+            out[name] = fn()
+        except Exception as e:  # noqa: BLE001
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+            print(f"bench: leg {name} failed: {out[name]['error']}", file=sys.stderr, flush=True)
+
     if w is not None and not args.no_wire:
-        out["wire"] = wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire,
-                               elapsed / args.steps)
+        leg("wire", lambda: wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire,
+                                     elapsed / args.steps))
     if w is not None and not args.no_e2e:
-        out["end_to_end"] = e2e_leg(eng, w, args, np)
-        out["end_to_end_pinned"] = e2e_leg(eng, w, args, np, pinned=True)
-        out["end_to_end_concurrent"] = e2e_leg_concurrent(eng, w, args, np)
+        leg("end_to_end", lambda: e2e_leg(eng, w, args, np))
+        leg("end_to_end_pinned", lambda: e2e_leg(eng, w, args, np, pinned=True))
+        leg("end_to_end_concurrent", lambda: e2e_leg_concurrent(eng, w, args, np))
     if dist is not None and not args.no_e2e:
         out["end_to_end"] = e2e_leg_sharded(eng, db, args, np, torch, dist, coll_dev, world)
     if w is not None and not args.no_stream:
-        out["stream"] = stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch)
+        leg("stream", lambda: stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, DeviceBatch))
     if world == 1 and not args.no_config3:
         eng.set_kernel_timing(True)
-        out["config3"] = config3_leg(eng, args, torch, synth, DeviceBatch, dev, ct)
+        leg("config3", lambda: config3_leg(eng, args, torch, synth, DeviceBatch, dev, ct))
         eng.set_kernel_timing(False)
     if world == 1 and not args.no_config5:
-        out["config5"] = config5_leg(eng, args, torch, synth, DeviceBatch, dev)
+        leg("config5", lambda: config5_leg(eng, args, torch, synth, DeviceBatch, dev))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(w.batch, w.desc, w.now, min(args.cpu_sample_proposals, P),
-                                           min(args.cpu_single_proposals, P))
-        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
-        out["gpu_over_cpu_whole_host_estimate"] = value / out["cpu_baseline"]["whole_host_estimate"]["value"]
+        leg("cpu_baseline", lambda: cpu_baseline(w.batch, w.desc, w.now, min(args.cpu_sample_proposals, P),
+                                                 min(args.cpu_single_proposals, P)))
+        if "value" in out["cpu_baseline"]:
+            out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+            out["gpu_over_cpu_whole_host_estimate"] = value / out["cpu_baseline"]["whole_host_estimate"]["value"]
     if probe:
         out["probe"] = "HLC_BENCH_PROBE=1: a timing-probe build, results not checked (not a valid measurement)"
     if rank == 0:

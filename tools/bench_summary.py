@@ -19,7 +19,8 @@ def main() -> None:
                     v = d[k].get("value")
                     parts.append(f"{k} {v / 1e6:.1f} M" if v is not None else f"{k} error: {d[k].get('error')}")
             if "cpu_baseline" in d:
-                parts.append(f"cpu {d['cpu_baseline']['value'] / 1e3:.1f} k")
+                c = d["cpu_baseline"]
+                parts.append(f"cpu {c['value'] / 1e3:.1f} k" if "value" in c else f"cpu error: {c.get('error')}")
             if "gathered_results" in d:
                 parts.append(f"gathered {d['gathered_results']}")
             if "counters_per_step" in d:
