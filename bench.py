@@ -389,6 +389,18 @@ def wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synt
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     step_s = el / args.steps
+    # the same bytes from host memory through hlc_validate_wire_proposals (upload, decode, validate,
+    # per-proposal results back): what an embedder holding gossip bytes in host buffers sees
+    host = None
+    if dist is None:
+        eng.validate_wire_proposals(wire, off, lens, scope, w.now)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            hres, _, _ = eng.validate_wire_proposals(wire, off, lens, scope, w.now)
+        hel = (time.perf_counter() - t0) / args.steps
+        assert np.array_equal(hres, res_s), "host wire-path outcomes differ from the SoA path"
+        host = {"value": db.n / hel, "unit": "votes/s", "ms_per_call": hel * 1e3,
+                "what": "hlc_validate_wire_proposals from host buffers (PCIe-inclusive)"}
     return {
         "metric": "verified votes/s from wire bytes (device protobuf decode + validation)",
         "value": db.n * world * args.steps / el,
@@ -399,6 +411,7 @@ def wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synt
         "decode_overhead_GBps": wire.size / max(step_s - soa_step_s, 1e-9) / 1e9,
         "outcomes_equal_soa_path": True,
         "host_encode_seconds": t_enc,
+        **({"from_host_buffers": host} if host is not None else {}),
     }
 
 
