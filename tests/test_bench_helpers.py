@@ -1,0 +1,46 @@
+"""bench.py's measurement helpers on CPU: the committed profile (roofline.json "profile") yields the
+traffic, VALU and chain-check / tally figures the bench line carries; the CPU-baseline scaling;
+and tools/bench_summary.py reads a line whose secondary legs failed."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_committed_profile_figures():
+    assert os.path.isdir(bench.PMC_PROFILE), bench.PMC_PROFILE
+    t = bench.pmc_traffic()
+    assert t["bytes"] > 0 and t["per_kernel"]["k_rec_main"]["write_bytes"] > 0
+    # per 640k-vote launch: the recovery kernels move a few GB, not MB and not tens of GB
+    assert 1e9 < t["bytes"] < 3e10
+    v = bench.valu_figures()
+    assert 0.2 < v["valu_lane_op_frac"] < 0.6
+    assert 2e5 < v["valu_instr_per_vote"]["k_rec_main"] < 4e5
+    for trace, fetch, write in (("trace_serial", "pmc_fetch", "pmc_write"), ("c3_trace", "c3_fetch", "c3_write")):
+        c = bench.chain_counters(trace, fetch, write)
+        assert c is not None and c["GBps"] > 100 and 0 < c["frac_of_hbm_achievable"] < 1.2
+        assert set(bench.CHAIN_KERNELS) <= set(c["per_kernel"])
+
+
+def test_whole_host_estimate():
+    e = bench.whole_host_estimate(8000.0, 7000.0)
+    assert e["physical_cores"] >= 1
+    assert e["value"] == 7000.0 * e["physical_cores"]  # the slower per-thread rate
+
+
+def test_bench_summary_reads_failed_legs(tmp_path):
+    line = {"metric": "m", "value": 1e8, "ms_per_step": 6.4, "n_gpus": 1,
+            "roofline": {"kernel_ms_avg": 6.3, "frac": 0.87},
+            "wire": {"value": 9.6e7}, "end_to_end": {"error": "RuntimeError: boom"},
+            "cpu_baseline": {"error": "OSError: x"}}
+    p = tmp_path / "b.json"
+    p.write_text("noise\n" + json.dumps(line) + "\n")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_summary.py"), str(p)],
+                         capture_output=True, text=True, check=True).stdout
+    assert "100.0 M votes/s" in out and "wire 96.0 M" in out
+    assert "end_to_end error: RuntimeError: boom" in out and "cpu error: OSError: x" in out
