@@ -18,7 +18,8 @@ rejected-by-code counters.
 
 cpu_baseline: the C restatement of validate_vote (recover + k256's re-verify, as upstream) on
 every host thread the process may use, one thread, and the two-pass (process_incoming_proposal)
-rate, rank 0 at N = 1 only, on a bounded sample of the same workload.
+rate, on rank 0, on a bounded sample of the same workload (at N > 1: of rank 0's shard, after the
+timed region, the other ranks waiting at a barrier), and gpu_over_cpu for all N GPUs.
 """
 from __future__ import annotations
 
@@ -279,6 +280,85 @@ def physical_cores() -> int:
         return os.cpu_count() or 1
 
 
+def _cpulist(text: str) -> set:
+    out = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def numa_facts(torch, dev, arrays) -> dict:
+    """Where a host-buffer leg's memory and threads sit relative to the GPU: the
+    GPU's NUMA node (sysfs, from its PCI address), the NUMA nodes of this process's CPUs, and the node
+    of every page of the given numpy arrays (move_pages(2) with no target = query), as {node: pages}."""
+    import ctypes
+    out = {}
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            out["gpu_numa_node"] = int(f.read())
+        out["gpu_pci"] = bdf
+    except Exception as e:  # noqa: BLE001
+        out["gpu_numa_node"] = f"unknown ({type(e).__name__})"
+    try:
+        aff = os.sched_getaffinity(0)
+        nodes = {}
+        base = "/sys/devices/system/node"
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                with open(f"{base}/{d}/cpulist") as f:
+                    k = len(_cpulist(f.read()) & aff)
+                if k:
+                    nodes[int(d[4:])] = k
+        out["process_cpus_by_node"] = nodes
+    except OSError:
+        pass
+    try:
+        import numpy as np
+        libc = ctypes.CDLL(None, use_errno=True)
+        pages = {}
+        for a in arrays:
+            lo = a.ctypes.data & ~4095
+            n = (a.ctypes.data + a.nbytes - lo + 4095) // 4096
+            step = max(1, n // 256)  # a sample of the array's pages
+            addrs = np.arange(lo, lo + n * 4096, 4096 * step, dtype=np.uint64)
+            st = np.zeros(addrs.size, np.int32)
+            if libc.syscall(279, 0, ctypes.c_ulong(addrs.size), ctypes.c_void_p(addrs.ctypes.data), None,
+                            ctypes.c_void_p(st.ctypes.data), 0) == 0:
+                for v in st.tolist():
+                    pages[v] = pages.get(v, 0) + 1
+        out["input_pages_by_node"] = {str(k): v for k, v in sorted(pages.items())}
+        out["pages_note"] = "sampled pages of the input arrays; negative = not resident (-errno)"
+    except Exception as e:  # noqa: BLE001
+        out["input_pages_by_node"] = f"unknown ({type(e).__name__})"
+    return out
+
+
+def traced_phases(eng, call, calls: int = 3) -> dict:
+    """The host-buffer call's phase times (HLC_HOST_TRACE=2, hlc_ctx_last_host_trace) over `calls`
+    extra untimed calls: per phase the median ms from the call's start, plus the trace's facts."""
+    import statistics
+    os.environ["HLC_HOST_TRACE"] = "2"
+    runs = []
+    try:
+        for _ in range(calls):
+            call()
+            runs.append(eng.last_host_trace())
+    finally:
+        os.environ.pop("HLC_HOST_TRACE", None)
+    runs = [r for r in runs if r]
+    if not runs:
+        return {}
+    med = lambda key: {k: statistics.median(r[key].get(k, float("nan")) for r in runs)  # noqa: E731
+                       for k in runs[0][key]}
+    return {"host_ms": med("host"), "device_ms": med("device"), "facts": runs[-1].get("facts", {}),
+            "calls": len(runs), "what": "median over traced untimed calls; ms from the call's start (device: from "
+                                        "an event recorded first on the upload stream)"}
+
+
 def whole_host_estimate(single: float, per_thread: float) -> dict:
     """The CPU baseline scaled to every physical core of the host (keep the whole-host
     comparison visible beside the quota-bound one): the measured per-thread rate (the slower of the
@@ -393,14 +473,32 @@ def wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synt
     # per-proposal results back): what an embedder holding gossip bytes in host buffers sees
     host = None
     if dist is None:
-        eng.validate_wire_proposals(wire, off, lens, scope, w.now)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            hres, _, _ = eng.validate_wire_proposals(wire, off, lens, scope, w.now)
-        hel = (time.perf_counter() - t0) / args.steps
-        assert np.array_equal(hres, res_s), "host wire-path outcomes differ from the SoA path"
+        def host_call():
+            return eng.validate_wire_proposals(wire, off, lens, scope, w.now)
+
+        def timed_host():
+            for _ in range(max(1, args.warmup)):
+                host_call()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                hres, _, _ = host_call()
+            assert np.array_equal(hres, res_s), "host wire-path outcomes differ from the SoA path"
+            return (time.perf_counter() - t0) / args.steps
+
+        hel = timed_host()
+        # the unpipelined arm of the same entry (HLC_WIRE_PIPELINE=0: the whole buffer uploaded, then
+        # decoded, then validated) beside it -- what the message-range pipeline gains
+        os.environ["HLC_WIRE_PIPELINE"] = "0"
+        try:
+            pel = timed_host()
+        finally:
+            os.environ.pop("HLC_WIRE_PIPELINE", None)
         host = {"value": db.n / hel, "unit": "votes/s", "ms_per_call": hel * 1e3,
-                "what": "hlc_validate_wire_proposals from host buffers (PCIe-inclusive)"}
+                "what": "hlc_validate_wire_proposals from host buffers (PCIe-inclusive; pageable bytes, decoded and "
+                        "recovered message range by message range as they land)",
+                "unpipelined": {"value": db.n / pel, "unit": "votes/s", "ms_per_call": pel * 1e3,
+                                "what": "the same entry with HLC_WIRE_PIPELINE=0 (upload all, decode, validate)"},
+                "phases": traced_phases(eng, host_call)}
     return {
         "metric": "verified votes/s from wire bytes (device protobuf decode + validation)",
         "value": db.n * world * args.steps / el,
@@ -483,7 +581,7 @@ def stream_leg(eng, w, dev, stream, handle, args, world, dist, np, torch, Device
     }
 
 
-def e2e_leg(eng, w, args, np, pinned=False):
+def e2e_leg(eng, w, args, np, torch, dev, pinned=False):
     """Secondary line: the same workload through the host-buffer entry hlc_validate_proposals
     (inputs copied host -> HBM over PCIe, results copied back, blocking): what a caller holding the
     votes in host memory sees.  Never the headline value (inputs are not HBM-resident).
@@ -495,7 +593,9 @@ def e2e_leg(eng, w, args, np, pinned=False):
                    + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
     if pinned:
         b = b.pinned()
-    eng.validate_proposals(b, d, w.now, want_votes=True)
+    # the same warm-up for both legs (round 4 gave the page-locked leg one call only)
+    for _ in range(max(1, args.warmup)):
+        eng.validate_proposals(b, d, w.now, want_votes=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res, vst, _, _ = eng.validate_proposals(b, d, w.now, want_votes=True)
@@ -508,6 +608,9 @@ def e2e_leg(eng, w, args, np, pinned=False):
         "unit": "votes/s",
         "ms_per_call": el / args.steps * 1e3,
         "bytes_in_per_call": bytes_in,
+        "warmup_calls": max(1, args.warmup),
+        "phases": traced_phases(eng, lambda: eng.validate_proposals(b, d, w.now, want_votes=True)),
+        "numa": numa_facts(torch, dev, (b.arena, b.field_off, b.field_len, b.timestamp)),
     }
 
 
@@ -997,8 +1100,8 @@ def main() -> int:
         leg("wire", lambda: wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synth, DeviceWire,
                                      elapsed / args.steps))
     if w is not None and not args.no_e2e:
-        leg("end_to_end", lambda: e2e_leg(eng, w, args, np))
-        leg("end_to_end_pinned", lambda: e2e_leg(eng, w, args, np, pinned=True))
+        leg("end_to_end", lambda: e2e_leg(eng, w, args, np, torch, dev))
+        leg("end_to_end_pinned", lambda: e2e_leg(eng, w, args, np, torch, dev, pinned=True))
         leg("end_to_end_concurrent", lambda: e2e_leg_concurrent(eng, w, args, np))
     if dist is not None and not args.no_e2e:
         out["end_to_end"] = e2e_leg_sharded(eng, db, args, np, torch, dist, coll_dev, world)
@@ -1013,9 +1116,25 @@ def main() -> int:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         leg("cpu_baseline", lambda: cpu_baseline(w.batch, w.desc, w.now, min(args.cpu_sample_proposals, P),
                                                  min(args.cpu_single_proposals, P)))
-        if "value" in out["cpu_baseline"]:
-            out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
-            out["gpu_over_cpu_whole_host_estimate"] = value / out["cpu_baseline"]["whole_host_estimate"]["value"]
+    elif dist is not None and not args.no_cpu_baseline:
+        # N > 1: after the timed region and every collective of the legs above,
+        # rank 0 times the same CPU baseline on a sample of its own shard (its first proposals, copied
+        # back once) while the other ranks wait at a barrier; the line then states the north star's
+        # ratio for all N GPUs
+        if rank == 0:
+            def cpu_leg():
+                sample = min(args.cpu_sample_proposals, P)
+                hb, hd = db.host_prefix(sample)
+                cb = cpu_baseline(hb, hd, db.now, sample, min(args.cpu_single_proposals, sample))
+                cb["timed_while"] = "the other ranks wait at a barrier (after the timed region)"
+                return cb
+            leg("cpu_baseline", cpu_leg)
+        dist.barrier()
+    if rank == 0 and "value" in out.get("cpu_baseline", {}):
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        out["gpu_over_cpu_whole_host_estimate"] = value / out["cpu_baseline"]["whole_host_estimate"]["value"]
+        out["gpu_over_cpu_basis"] = (f"value ({world} GPU(s), all ranks' votes) / cpu_baseline.value "
+                                     f"({out['cpu_baseline']['cores']} host threads)")
     if probe:
         out["probe"] = "HLC_BENCH_PROBE=1: a timing-probe build, results not checked (not a valid measurement)"
     if rank == 0:

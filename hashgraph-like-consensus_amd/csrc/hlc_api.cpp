@@ -19,6 +19,11 @@
 #include "../../include/hlc.h"
 #include "hlc_kernels.h"
 
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(__x86_64__)
+#include <immintrin.h>
+#define HLC_HAVE_NT_COPY 1
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -93,6 +98,51 @@ struct PBuf {
   }
   uint8_t* at(size_t off) const { return static_cast<uint8_t*>(p) + off; }
 };
+
+// The host-buffer entries' staging copies into page-locked memory (HLC_NT_COPY, default 1): 32-byte
+// non-temporal stores when the CPU has AVX2 -- the staging buffer is written once and next read by the
+// DMA engine, so the copy need not read its destination lines into the cache first (a plain memcpy of
+// the pool's 16-256 KB pieces stays below glibc's non-temporal threshold and does); sfence at the end,
+// before the pool reports the piece done and the DMA of it is enqueued.
+#ifdef HLC_HAVE_NT_COPY
+__attribute__((target("avx2"))) void copy_nt_avx2(uint8_t* dst, const uint8_t* src, size_t n) {
+  const size_t head = (32 - ((uintptr_t)dst & 31)) & 31;
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+    const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
+  }
+  std::memcpy(dst + i, src + i, n - i);
+  _mm_sfence();
+}
+#endif
+std::atomic<bool> g_nt_copy{false};  // refreshed from the environment by every host-buffer call (host_resources)
+void refresh_nt_copy() {
+#ifdef HLC_HAVE_NT_COPY
+  const char* e = std::getenv("HLC_NT_COPY");
+  g_nt_copy.store((!e || std::atoi(e) != 0) && __builtin_cpu_supports("avx2"), std::memory_order_relaxed);
+#endif
+}
+bool nt_copy_enabled() { return g_nt_copy.load(std::memory_order_relaxed); }
+void stage_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+#ifdef HLC_HAVE_NT_COPY
+  if (n >= 4096 && nt_copy_enabled()) {
+    copy_nt_avx2(dst, src, n);
+    return;
+  }
+#endif
+  std::memcpy(dst, src, n);
+}
 
 // A small host worker pool for the host-buffer entries' field checks and staging copies: run(fn) calls
 // fn(chunk, chunks()) once for every chunk, on the workers and the calling thread, and returns when all
@@ -177,11 +227,16 @@ struct hlc_ctx {
   // records) so that two k_rec_main grids over the two vote ranges of a call overlap; an upload stream;
   // the page-locked staging of the inputs and outputs and their device copies (allocated on first use)
   hipStream_t aux2 = nullptr, copy = nullptr;
+  hipStream_t dec = nullptr, wlk = nullptr;  // wire host entry: the ranges' decode and walks (greatest priority)
   DBuf rec_scratch2;
   std::vector<std::unique_ptr<DBuf>> rec_works;  // each recovery range's work list, prefix products, counters
   PBuf pin_in, pin_out;
   DBuf dev_in, dev_out;
   std::vector<hipEvent_t> ev_up, ev_main;  // per recovery range: inputs landed, main stage done
+  std::vector<hipEvent_t> ev_cnt, ev_dec;  // wire host entry, per message range: vote count read back, decoded
+  PBuf pin_cnt;                            // wire host entry: the ranges' vote counts (page-locked)
+  uint64_t wire_hint = 0;                  // wire host entry: the largest vote count a call decoded
+  std::string last_trace;                  // the last host-buffer call's HLC_HOST_TRACE JSON
   hipEvent_t ev_rest = nullptr, ev_done = nullptr;
   std::unique_ptr<HostPool> pool;  // staging workers (HLC_HOST_THREADS)
   // staged host inputs (host-buffer entry points)
@@ -211,6 +266,8 @@ struct hlc_ctx {
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : ev_up) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_main) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_cnt) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_dec) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_rest, ev_done})
       if (e) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -331,7 +388,7 @@ struct RecFront {
 // per range they cost 0.95 ms against 0.67 ms for one launch over 640k votes.)
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t np,
                uint64_t now, uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, uint8_t* chain_code,
-               hipStream_t s, const RecFront* fronts = nullptr, int nfronts = 0) {
+               hipStream_t s, const RecFront* fronts = nullptr, int nfronts = 0, uint64_t rec_stride = 0) {
   const uint64_t n = dv->n;
   CHK(c->pre.ensure(n));
   CHK(c->pre_reason.ensure(n));
@@ -381,7 +438,8 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     for (int k = 0; k < nfronts; ++k) HIPCHK(hipStreamWaitEvent(s, fronts[k].done, 0));
     hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
                                dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(),
-                               c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact);
+                               c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact,
+                               rec_stride);
     hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
                             c->verify.as<uint8_t>(), status, reason, red, s);
     HIPCHK(hipGetLastError());
@@ -445,7 +503,7 @@ int reserve_validate(hlc_ctx* c, uint64_t n, uint64_t np) {
 // Device-resident validate-many (every pointer is device memory).
 int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops, uint64_t np, uint64_t now,
                     hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s,
-                    const RecFront* fronts = nullptr, int nfronts = 0) {
+                    const RecFront* fronts = nullptr, int nfronts = 0, uint64_t rec_stride = 0) {
   const uint64_t n = dv->n;
   if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
   hipEvent_t call0 = nullptr, call1 = nullptr;
@@ -481,7 +539,7 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   // recovery's main stage: k_vote_status reports each proposal's first failing vote)
   if (n)
     CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, np, now, status, reason, drec, c->red.as<uint32_t>(),
-                   c->chain_code.as<uint8_t>(), s, fronts, nfronts));
+                   c->chain_code.as<uint8_t>(), s, fronts, nfronts, rec_stride));
   hipEvent_t ch0 = nullptr, ch1 = nullptr;
   if (c->timing) {  // chain check + duplicate detection + tally (+ k_chain_small's bracket in vote_stage)
     ch0 = c->take_event();
@@ -692,25 +750,42 @@ int stage_votes(hlc_ctx* c, const hlc_votes* v, hlc_votes* dv, hipStream_t s) {
 
 void destroy_ctx(hlc_ctx* ctx) {
   if (!ctx) return;
-  for (hipStream_t x : {ctx->stream, ctx->aux, ctx->aux2, ctx->copy})
+  for (hipStream_t x : {ctx->stream, ctx->aux, ctx->aux2, ctx->copy, ctx->dec, ctx->wlk})
     if (x) (void)hipStreamSynchronize(x);
-  hipStream_t s = ctx->stream, a = ctx->aux, a2 = ctx->aux2, cp = ctx->copy;
+  hipStream_t s = ctx->stream, a = ctx->aux, a2 = ctx->aux2, cp = ctx->copy, dc = ctx->dec, wk = ctx->wlk;
   delete ctx;
-  for (hipStream_t x : {s, a, a2, cp})
+  for (hipStream_t x : {s, a, a2, cp, dc, wk})
     if (x) (void)hipStreamDestroy(x);
 }
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Staging workers of the host-buffer entries (HLC_HOST_THREADS, default 16 -- the GPU box's CPU share
-// per GPU -- capped by the hardware threads; including the calling thread).  Measured on two boxes
-// with the chunked pool: 16 threads 86.9 / 88.3 M votes/s, 12: 86.0 / 88.0, 8: 85.2 / 87.1
-// (profiles/r04/host_pool_threads.txt).
+// The CPUs the cgroup (v2) quota grants the process, or 0 when there is none.
+double cgroup_cpu_quota() {
+  std::FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r");
+  if (!f) return 0;
+  char q[64] = {0};
+  double per = 0;
+  const int got = std::fscanf(f, "%63s %lf", q, &per);
+  std::fclose(f);
+  if (got != 2 || per <= 0 || std::strcmp(q, "max") == 0) return 0;
+  return std::atof(q) / per;
+}
+
+// Staging workers of the host-buffer entries (including the calling thread): HLC_HOST_THREADS, or by
+// default 16 -- the GPU box's CPU share per GPU -- capped by the hardware threads and by this
+// process's share of the CPUs: the cgroup quota (or the hardware threads) divided by the ranks on
+// the node (LOCAL_WORLD_SIZE, set by torch.distributed.run), so that 8 ranks do not run 8 x 16
+// staging threads on one node's quota.  Measured on two boxes with the chunked pool: 16 threads
+// 86.9 / 88.3 M votes/s, 12: 86.0 / 88.0, 8: 85.2 / 87.1 (profiles/r04/host_pool_threads.txt).
 int host_threads() {
-  const char* e = std::getenv("HLC_HOST_THREADS");
+  if (const char* e = std::getenv("HLC_HOST_THREADS")) return std::max(1, std::min(std::atoi(e), 64));
   const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-  const int t = e ? std::atoi(e) : std::min(16, hw);
-  return std::max(1, std::min(t, 64));
+  int ranks = 1;
+  if (const char* r = std::getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, std::atoi(r));
+  const double quota = cgroup_cpu_quota();
+  const double share = (quota > 0 ? std::min(quota, (double)hw) : (double)hw) / ranks;
+  return std::max(1, std::min({16, hw, (int)(share + 1e-9)}));
 }
 
 // The recovery ranges of a host-buffer call of n items (HLC_SPLIT_VOTES="a,b,...", default
@@ -743,21 +818,28 @@ std::vector<uint64_t> split_ranges(uint64_t n) {
 
 // Whether [p, p + len) lies in page-locked host memory the device can DMA from directly
 // (hlc_host_alloc, hipHostMalloc or hipHostRegister): then the host-buffer entries upload that array
-// from the caller's memory and skip its staging copy.
-bool is_pinned(const void* p, size_t len) {
-  if (!p || !len) return false;
+// from the caller's memory and skip its staging copy.  The first and the last byte must be page-locked
+// host memory of ONE allocation (the same buffer id): an allocation is contiguous, so the whole range
+// is then inside it.  Two page-locked blocks that happen to abut, or a buffer registered in two
+// separate parts with pageable memory between them, are staged.
+bool pinned_buffer(const void* q, unsigned long long& id) {
   hipPointerAttribute_t a;
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+  if (hipPointerGetAttributes(&a, q) != hipSuccess) {
     (void)hipGetLastError();  // pageable memory: clear the sticky error
     return false;
   }
   if (a.type != hipMemoryTypeHost) return false;
-  hipPointerAttribute_t b;  // the last byte in the same allocation
-  if (hipPointerGetAttributes(&b, static_cast<const uint8_t*>(p) + len - 1) != hipSuccess) {
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)q) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
-  return b.type == hipMemoryTypeHost;
+  return true;
+}
+bool is_pinned(const void* p, size_t len) {
+  if (!p || !len) return false;
+  unsigned long long a = 0, b = 0;
+  if (!pinned_buffer(p, a) || !pinned_buffer(static_cast<const uint8_t*>(p) + len - 1, b)) return false;
+  return a == b;
 }
 
 // The host-buffer entries' streams, events, staging pool and second recovery slot (on first use).
@@ -768,10 +850,13 @@ bool is_pinned(const void* p, size_t len) {
 // upload stream takes the greatest priority and the second recovery stream the least: each draws
 // its queue from a pool of its own, apart from the normal-priority launch / aux streams.
 int host_resources(hlc_ctx* c) {
+  refresh_nt_copy();
   int least = 0, greatest = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   if (!c->copy) HIPCHK(hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, greatest));
   if (!c->aux2) HIPCHK(hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, least));
+  if (!c->dec) HIPCHK(hipStreamCreateWithPriority(&c->dec, hipStreamNonBlocking, greatest));
+  if (!c->wlk) HIPCHK(hipStreamCreateWithPriority(&c->wlk, hipStreamNonBlocking, greatest));
   for (hipEvent_t* e : {&c->ev_rest, &c->ev_done})
     if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   if (!c->pool || c->pool->threads() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
@@ -780,16 +865,29 @@ int host_resources(hlc_ctx* c) {
   return 0;
 }
 
-// HLC_HOST_TRACE=1: one line per hlc_validate_proposals call on stderr -- host phase ends and device
-// event times, ms from the call's start (the device times from an event recorded first on the
-// upload stream)
+// HLC_HOST_TRACE=1: one line per host-buffer call (hlc_validate_proposals, hlc_validate_wire_proposals,
+// hlc_eth_verify_batch) on stderr -- host phase ends and device event times, ms from the call's start
+// (the device times from an event recorded first on the upload stream); HLC_HOST_TRACE=2: the same
+// JSON kept for hlc_ctx_last_host_trace only (bench.py's per-phase figures), nothing printed.
 struct HostTrace {
   using clk = std::chrono::steady_clock;
-  bool on = false;
+  bool on = false, print = false;
+  std::string* sink = nullptr;
   clk::time_point t0;
-  std::vector<std::pair<std::string, double>> host;
+  std::vector<std::pair<std::string, double>> host, facts;
   std::vector<std::pair<std::string, hipEvent_t>> dev;
   hipEvent_t e0 = nullptr;
+  // a value about the call (not a time): which inputs were DMA'd from the caller's page-locked memory
+  void fact(const std::string& what, double v) {
+    if (on) facts.emplace_back(what, v);
+  }
+  explicit HostTrace(std::string* keep) : sink(keep) {
+    if (const char* e = std::getenv("HLC_HOST_TRACE")) {
+      const int v = std::atoi(e);
+      on = v != 0;
+      print = v == 1;
+    }
+  }
   void start(hipStream_t s) {
     if (!on) return;
     t0 = clk::now();
@@ -810,17 +908,28 @@ struct HostTrace {
   ~HostTrace() {
     if (!on) return;
     (void)hipDeviceSynchronize();
-    std::fprintf(stderr, "HLC_HOST_TRACE {\"host\": {");
-    for (size_t k = 0; k < host.size(); ++k)
-      std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", host[k].first.c_str(), host[k].second);
-    std::fprintf(stderr, "}, \"device\": {");
+    std::string j = "{\"host\": {";
+    char b[96];
+    for (size_t k = 0; k < host.size(); ++k) {
+      std::snprintf(b, sizeof b, "%s\"%s\": %.3f", k ? ", " : "", host[k].first.c_str(), host[k].second);
+      j += b;
+    }
+    j += "}, \"device\": {";
     for (size_t k = 0; k < dev.size(); ++k) {
       float f = -1;
       (void)hipEventElapsedTime(&f, e0, dev[k].second);
-      std::fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", dev[k].first.c_str(), (double)f);
+      std::snprintf(b, sizeof b, "%s\"%s\": %.3f", k ? ", " : "", dev[k].first.c_str(), (double)f);
+      j += b;
       (void)hipEventDestroy(dev[k].second);
     }
-    std::fprintf(stderr, "}}\n");
+    j += "}, \"facts\": {";
+    for (size_t k = 0; k < facts.size(); ++k) {
+      std::snprintf(b, sizeof b, "%s\"%s\": %.17g", k ? ", " : "", facts[k].first.c_str(), facts[k].second);
+      j += b;
+    }
+    j += "}}";
+    if (print) std::fprintf(stderr, "HLC_HOST_TRACE %s\n", j.c_str());
+    if (sink) *sink = j;
     if (e0) (void)hipEventDestroy(e0);
   }
 };
@@ -840,7 +949,20 @@ struct Staging {
     return 0;
   }
   void drain() {
-    for (hipStream_t x : {c->copy, c->aux, c->aux2, c->stream}) (void)hipStreamSynchronize(x);
+    for (hipStream_t x : {c->copy, c->wlk, c->dec, c->aux, c->aux2, c->stream})
+      if (x) (void)hipStreamSynchronize(x);
+  }
+};
+
+// Drains a host-buffer call's streams when it returns early (HLC_EINVAL from a field check, or a HIP
+// failure) with work in flight: no upload may still read the page-locked staging buffer, and no range
+// kernel may still use the call's workspace or events, when the next call reuses them.
+// Disarmed once the call has waited for its outputs.
+struct DrainOnExit {
+  Staging& st;
+  bool armed = true;
+  ~DrainOnExit() {
+    if (armed) st.drain();
   }
 };
 
@@ -872,7 +994,7 @@ int first_batch() {
 // aux2, each with its own per-lane scratch), once its upload (ev_up[k]) has landed.
 int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, uint64_t m, const uint8_t* dbytes,
                  const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len, size_t len_stride,
-                 std::vector<RecFront>& fronts) {
+                 std::vector<RecFront>& fronts, hipEvent_t ready = nullptr) {
   if (!m) return 0;
   // the first range's prep is on the call's critical path with the device otherwise idle: one vote
   // per lane (no batched inversion), so its dependent chain is an eighth as long
@@ -880,7 +1002,7 @@ int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, u
   const bool odd = k % 2;
   hipStream_t a = odd ? c->aux2 : c->aux;
   uint32_t* scratch = (odd ? c->rec_scratch2 : c->rec_scratch).as<uint32_t>();
-  HIPCHK(hipStreamWaitEvent(a, c->ev_up[k], 0));
+  HIPCHK(hipStreamWaitEvent(a, ready ? ready : c->ev_up[k], 0));
   hlc::launch_recover_prep(n, dbytes, sig_off, off_stride, sig_len, len_stride, c->rec_work.as<uint32_t>(), a,
                            nullptr, &range);
   hlc::launch_recover_main(n, dbytes, sig_off, off_stride, scratch, c->rec_lanes, c->rec_work.as<uint32_t>(), a,
@@ -909,7 +1031,7 @@ int stage_rows(Staging& st, HostPool& pool, Arr* arr, int na, uint64_t a0, uint6
     const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
     for (int q = 0; q < na; ++q)
       if (!arr[q].pinned && b1 > b0)
-        std::memcpy(st.P + arr[q].dst + arr[q].elem * b0, arr[q].src + arr[q].elem * b0, arr[q].elem * (b1 - b0));
+        stage_copy(st.P + arr[q].dst + arr[q].elem * b0, arr[q].src + arr[q].elem * b0, arr[q].elem * (b1 - b0));
     if (also) also(t, b0, b1);
   });
   for (int q = 0; q < na; ++q) {
@@ -927,7 +1049,7 @@ int stage_span(Staging& st, HostPool& pool, const uint8_t* bytes, bool pinned, s
   if (pinned) return st.up_from(o_arena + lo, bytes + lo, hi - lo);
   pool.run([&](int t, int T) {
     const uint64_t d0 = lo + (hi - lo) * t / T, d1 = lo + (hi - lo) * (t + 1) / T;
-    if (d1 > d0) std::memcpy(st.P + o_arena + d0, bytes + d0, d1 - d0);
+    if (d1 > d0) stage_copy(st.P + o_arena + d0, bytes + d0, d1 - d0);
   });
   return st.up(o_arena + lo, hi - lo);
 }
@@ -1000,8 +1122,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   const uint64_t blen = v->bytes ? v->bytes_len : 0;
   CHK(host_resources(c));
   HostPool& pool = *c->pool;
-  HostTrace tr;
-  if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
+  HostTrace tr(&c->last_trace);
   tr.start(c->copy);
   // inputs, page-locked and on the device alike: dense signatures | signature lengths | vote_id |
   // proposal_id | timestamp | vote | field_off | field_len | proposals | arena
@@ -1032,6 +1153,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   std::vector<uint64_t> rb;
   CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  DrainOnExit guard{st};
   const uint8_t* D = st.D;
   const int parts = pool.chunks();
   std::vector<RecFront> fronts;
@@ -1039,10 +1161,8 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
     int rc = 0;
     if (!stage_sigs(st, pool, v->bytes, v->bytes_len, v->field_off + HLC_F_SIGNATURE, v->field_len + HLC_F_SIGNATURE,
-                    HLC_NFIELDS, o[0], o[1], a0, a1, &rc)) {
-      st.drain();
+                    HLC_NFIELDS, o[0], o[1], a0, a1, &rc))
       return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-    }
     CHK(rc);
     HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
     tr.mark("sigs_staged_" + std::to_string(k));
@@ -1061,6 +1181,12 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   Arr parr{reinterpret_cast<const uint8_t*>(props), o[8], sizeof(hlc_proposal), false};
   parr.pinned = is_pinned(props, np * sizeof(hlc_proposal));
   const bool arena_pinned = is_pinned(v->bytes, blen);
+  {  // bit q: arr[q] DMA'd straight from the caller (vote_id, proposal_id, timestamp, vote, field_off,
+     // field_len), bit 6: the proposals, bit 7: the arena
+    int mask = 0;
+    for (int q = 0; q < 6; ++q) mask |= arr[q].pinned ? 1 << q : 0;
+    tr.fact("pinned_mask", mask | (parr.pinned ? 64 : 0) | (arena_pinned ? 128 : 0));
+  }
   CHK(stage_rows(st, pool, &parr, 1, 0, np));
   std::vector<int> bad(parts, 0);
   const int K = rest_pieces();
@@ -1079,12 +1205,8 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   }
   // a field outside the arena: nothing that reads the fields is enqueued (the recovery ranges
   // already in flight read only the signatures, checked when they were gathered)
-  for (int x : bad) {
-    if (x) {
-      st.drain();
-      return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
-    }
-  }
+  for (int x : bad)
+    if (x) return set_err(HLC_EINVAL, "field (offset, length) outside the byte arena");
   tr.mark("rest_staged");
   HIPCHK(hipEventRecord(c->ev_rest, c->copy));
   tr.ev("rest_landed", c->copy);
@@ -1111,6 +1233,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
   HIPCHK(hipEventSynchronize(c->ev_done));
+  guard.armed = false;
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);
   pool.run([&](int t, int T) {
@@ -1139,8 +1262,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   const uint64_t blen = bytes ? bytes_len : 0;
   CHK(host_resources(c));
   HostPool& pool = *c->pool;
-  HostTrace tr;
-  if (const char* e = std::getenv("HLC_HOST_TRACE")) tr.on = std::atoi(e) != 0;
+  HostTrace tr(&c->last_trace);
   tr.start(c->copy);
   // inputs: dense signatures | signature lengths | identity / payload lengths | identity / payload
   // offsets | arena
@@ -1163,16 +1285,15 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   std::vector<uint64_t> rb;
   CHK(prepare_ranges(c, n, rb));
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  DrainOnExit guard{st};
   const uint8_t* D = st.D;
   const int parts = pool.chunks();
   std::vector<RecFront> fronts;
   for (size_t k = 0; k + 1 < rb.size(); ++k) {
     const uint64_t a0 = rb[k], a1 = rb[k + 1];
     int rc = 0;
-    if (!stage_sigs(st, pool, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], a0, a1, &rc)) {
-      st.drain();
+    if (!stage_sigs(st, pool, bytes, bytes_len, sig_off, sig_len, 1, o[0], o[1], a0, a1, &rc))
       return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
-    }
     CHK(rc);
     HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
     tr.mark("sigs_staged_" + std::to_string(k));
@@ -1203,12 +1324,8 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
     }));
     CHK(stage_span(st, pool, bytes, arena_pinned, o[6], blen * k / K, blen * (k + 1) / K));
   }
-  for (int x : bad) {  // nothing that reads identities / payloads is enqueued
-    if (x) {
-      st.drain();
-      return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
-    }
-  }
+  for (int x : bad)  // nothing that reads identities / payloads is enqueued
+    if (x) return set_err(HLC_EINVAL, "item (offset, length) outside the byte arena");
   tr.mark("rest_staged");
   HIPCHK(hipEventRecord(c->ev_rest, c->copy));
   tr.ev("rest_landed", c->copy);
@@ -1234,6 +1351,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   tr.ev("outputs_landed", s);
   tr.mark("enqueued");
   HIPCHK(hipEventSynchronize(c->ev_done));
+  guard.armed = false;
   tr.mark("device_done");
   const uint8_t* src = c->pin_out.at(0);
   pool.run([&](int t, int T) {
@@ -1243,6 +1361,374 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
       if (out_addr) std::memcpy(out_addr + 20 * a0, src + r1 + 20 * a0, 20 * (a1 - a0));
     }
   });
+  tr.mark("outputs_copied");
+  return 0;
+}
+
+// hlc_validate_wire_proposals without pipelining: the whole wire buffer uploaded, decoded, validated
+// (messages over wire_huge_threshold(), and the fallback of validate_wire_host).
+int wire_host_plain(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* moff, const uint32_t* mlen,
+                    uint64_t nm, const hlc_scope_config* scope, uint64_t n_scope, uint64_t now, hlc_result* out_res,
+                    hlc_wire_proposal* out_wire, uint64_t* out_n_votes) {
+  hipStream_t s = c->stream;
+  CHK(stage_wire(c, wire, wire_len, moff, mlen, nm, scope, n_scope, s));
+  CHK(c->w_res.ensure(nm * sizeof(hlc_result) + 16));
+  hlc_votes dv;
+  uint64_t nv = 0;
+  CHK(decode_device(c, c->w_wire.as<uint8_t>(), wire_len, c->w_moff.as<uint64_t>(), c->w_mlen.as<uint32_t>(), nm,
+                    c->w_scope.as<hlc_scope_config>(), n_scope, c->w_props.as<hlc_proposal>(),
+                    c->w_wout.as<hlc_wire_proposal>(), &dv, &nv, s));
+  CHK(validate_device(c, &dv, c->w_props.as<hlc_proposal>(), nm, now, c->w_res.as<hlc_result>(), nullptr, nullptr,
+                      nullptr, s));
+  hlc::launch_wire_results(nm, c->w_wout.as<hlc_wire_proposal>(), c->w_res.as<hlc_result>(), s);
+  HIPCHK(hipGetLastError());
+  if (nm) {
+    HIPCHK(hipMemcpyAsync(out_res, c->w_res.p, nm * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
+    if (out_wire)
+      HIPCHK(hipMemcpyAsync(out_wire, c->w_wout.p, nm * sizeof(hlc_wire_proposal), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  if (out_n_votes) *out_n_votes = nv;
+  c->wire_hint = std::max(c->wire_hint, nv);
+  return 0;
+}
+
+// The message ranges of a pipelined wire call: range k = messages [mb[k], mb[k+1]), which lie in the
+// byte prefix [0, ub[k+1]) of the wire buffer (ub[k] = the largest message end among earlier messages;
+// range k uploads [ub[k], ub[k+1])).  Byte sizes as split_ranges' vote counts: HLC_WIRE_SPLIT_BYTES
+// ("a,b,...", default 8, 16, 24, 32 MiB -- about 45k, 90k, 135k and 180k votes of config 2's 187 B per
+// vote), a range of each listed size while at least twice that many bytes remain, then doubling, at
+// most 16 ranges, then one range for the rest.  Swept on the box (tools/wire_pipe.py,
+// profiles/r05/wire_pipe_sweep.txt): 8,16,24,32 MiB beat 8,16 / 16,32 / 8,16,24 / 4,8,16,24 and a
+// shrinking tail (8,16,24,24,16,16,8) by 1-4%.  Messages that are out of order in the buffer only make a
+// range's prefix longer (an earlier range may then upload everything).
+void wire_ranges(const uint64_t* moff, const uint32_t* mlen, uint64_t nm, std::vector<uint64_t>& mb,
+                 std::vector<uint64_t>& ub) {
+  std::vector<uint64_t> sizes;
+  const char* e = std::getenv("HLC_WIRE_SPLIT_BYTES");
+  const char* p = e ? e : "8388608,16777216,25165824,33554432";
+  while (*p) {
+    char* end = nullptr;
+    const uint64_t x = std::strtoull(p, &end, 10);
+    if (end == p) break;
+    sizes.push_back(x);
+    p = *end == ',' ? end + 1 : end;
+  }
+  std::vector<uint64_t> pre(nm);  // prefix maximum of the message ends (empty messages read nothing)
+  uint64_t hi = 0;
+  for (uint64_t m = 0; m < nm; ++m) {
+    if (mlen[m]) hi = std::max(hi, moff[m] + mlen[m]);
+    pre[m] = hi;
+  }
+  mb.assign(1, 0);
+  ub.assign(1, 0);
+  uint64_t x = 0, m = 0;
+  for (size_t k = 0; k < 15 && nm; ++k) {
+    x = k < sizes.size() ? sizes[k] : 2 * x;
+    if (!x || hi - ub.back() < 2 * x) break;
+    while (m < nm && pre[m] < ub.back() + x) ++m;
+    if (m + 1 >= nm) break;
+    mb.push_back(m + 1);
+    ub.push_back(pre[m]);
+    ++m;
+  }
+  if (mb.back() < nm) {
+    mb.push_back(nm);
+    ub.push_back(hi);
+  }
+}
+
+// bytes per staging / upload piece of the wire host entry (HLC_WIRE_CHUNK, default 4 MiB; 8 MiB measured
+// 1-2% slower with non-temporal staging copies): piece j+1 is copied into page-locked memory while piece
+// j's DMA runs
+uint64_t wire_chunk() {
+  const char* e = std::getenv("HLC_WIRE_CHUNK");
+  const uint64_t x = e ? std::strtoull(e, nullptr, 10) : (4ull << 20);
+  return std::max<uint64_t>(x, 4096);
+}
+
+// hlc_validate_wire_proposals over host buffers, pipelined: gossip bytes go to
+// the device in message ranges (wire_ranges), and each range is decoded and its signatures recovered
+// as it lands, the way validate_host's signatures-first ranges start the recovery early:
+//   1. the message extents and scope configs go up first (12 B + 16 B per message); then the wire
+//      bytes, range by range, in wire_chunk() pieces: the host pool copies piece j+1 into page-locked
+//      memory while piece j's DMA runs (a page-locked wire buffer is DMA'd straight from the caller);
+//   2. behind range k's last piece, on the walk stream (greatest priority): the walker over its
+//      messages and one block scanning their vote counts (vote_begin relative to the range) that writes
+//      the range's vote total into mapped page-locked memory; the host polls for it between the next
+//      range's pieces, so the pieces keep flowing, and the walks of later ranges queue behind their
+//      bytes without waiting for the host;
+//   3. with the total known, on the decode stream (greatest priority, so its kernels are dispatched
+//      ahead of the recovery grids): the range's records placed, its Vote records decoded at vote base
+//      b_k (the sum of the earlier ranges' totals; per-message arrays at the range's first message,
+//      per-vote arrays at b_k, so the numbering equals a decode of the whole buffer), and its first-
+//      error pass; then its k_rec_prep + k_rec_main on the aux streams in turn, reading the signatures
+//      through the decoded (offset, length) pairs straight out of the device wire buffer;
+//   4. once every range is decoded: the validation over all votes on the launch stream (prehash, chain,
+//      duplicate, tally), one recovery finish after the last main stage, and one D2H of the results.
+// The per-vote arrays and the recovery records (row stride N) are sized once, after the first range's
+// total: N = the whole call's votes estimated from the first range's density (x 1.25, at least the
+// largest total an earlier call decoded, at most wire bytes / 2 -- a vote record takes at least a key
+// and a length byte).  A call that decodes more than N votes is drained and re-run unpipelined
+// (wire_host_plain), as is any call with a message over wire_huge_threshold() (the parallel huge-message
+// decoder needs its own host round trips).  Only stream / event dependencies order the device work.
+int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint64_t* moff, const uint32_t* mlen,
+                       uint64_t nm, const hlc_scope_config* scope, uint64_t n_scope, uint64_t now, hlc_result* out_res,
+                       hlc_wire_proposal* out_wire, uint64_t* out_n_votes) {
+  bool plain = nm == 0 || !wire;
+  for (uint64_t m = 0; m < nm && !plain; ++m) plain = mlen[m] > hlc::wire_huge_threshold();
+  if (plain) return wire_host_plain(c, wire, wire_len, moff, mlen, nm, scope, n_scope, now, out_res, out_wire,
+                                    out_n_votes);
+  CHK(host_resources(c));
+  HostPool& pool = *c->pool;
+  HostTrace tr(&c->last_trace);
+  tr.start(c->copy);
+  std::vector<uint64_t> mb, ub;
+  wire_ranges(moff, mlen, nm, mb, ub);
+  const size_t R = mb.size() - 1;
+  const uint64_t U = ub.back();
+  // page-locked staging and its device copy: message offsets | lengths | scope configs | wire bytes
+  // [0, U) (the bytes past the last message end are never read)
+  size_t o[5];
+  o[0] = 0;
+  o[1] = al256(nm * 8);
+  o[2] = o[1] + al256(nm * 4);
+  o[3] = o[2] + al256(n_scope * sizeof(hlc_scope_config));
+  o[4] = o[3] + al256(U + 16);
+  CHK(c->pin_in.ensure(o[4] + 16));
+  CHK(c->dev_in.ensure(o[4] + 16));
+  const size_t r1 = al256(nm * sizeof(hlc_result)), r2 = r1 + nm * sizeof(hlc_wire_proposal);  // results | wire info
+  CHK(c->pin_out.ensure(r2 + 16));
+  CHK(c->pin_cnt.ensure(R * 32 + 32));
+  // per-message device workspace (the per-vote arrays follow the first range's total)
+  const uint64_t slab = hlc::wire_slab();
+  CHK(c->w_vcount.ensure(nm * 8 + 8));
+  CHK(c->w_vbegin.ensure(nm * 8 + 8));
+  CHK(c->w_slab_off.ensure(nm * slab * 8 + 8));
+  CHK(c->w_slab_len.ensure(nm * slab * 4 + 4));
+  CHK(c->w_big.ensure(32));
+  CHK(c->w_huge.ensure(nm * 16 + 16));
+  CHK(c->w_first_bad.ensure(nm * 4 + 4));
+  CHK(c->w_props.ensure(nm * sizeof(hlc_proposal) + 16));
+  CHK(c->w_wout.ensure(nm * sizeof(hlc_wire_proposal) + 16));
+  CHK(c->w_res.ensure(nm * sizeof(hlc_result) + 16));
+  while (c->ev_cnt.size() < R) {
+    hipEvent_t a = nullptr, b = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    c->ev_cnt.push_back(a);
+    HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    c->ev_dec.push_back(b);
+  }
+  while (c->ev_up.size() < R) {
+    hipEvent_t a = nullptr, b = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    c->ev_up.push_back(a);
+    HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    c->ev_main.push_back(b);
+  }
+  while (c->rec_works.size() < R) c->rec_works.emplace_back(new DBuf());
+  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  DrainOnExit guard{st};
+  uint8_t* D = st.D;
+  const uint8_t* dwire = D + o[3];
+  const uint64_t* dmoff = reinterpret_cast<const uint64_t*>(D + o[0]);
+  const uint32_t* dmlen = reinterpret_cast<const uint32_t*>(D + o[1]);
+  const hlc_scope_config* dscope = reinterpret_cast<const hlc_scope_config*>(D + o[2]);
+  hipStream_t s = c->stream;
+  uint64_t* vcount = c->w_vcount.as<uint64_t>();
+  uint64_t* vbegin = c->w_vbegin.as<uint64_t>();
+  hlc_proposal* dprops = c->w_props.as<hlc_proposal>();
+  hlc_wire_proposal* dwout = c->w_wout.as<hlc_wire_proposal>();
+  uint64_t* cnt = reinterpret_cast<uint64_t*>(c->pin_cnt.p);
+  // 1. the message extents and scope configs
+  std::memcpy(st.P + o[0], moff, nm * 8);
+  std::memcpy(st.P + o[1], mlen, nm * 4);
+  std::memcpy(st.P + o[2], scope, n_scope * sizeof(hlc_scope_config));
+  CHK(st.up(0, o[3]));
+  const bool wire_pinned = is_pinned(wire, U);
+  const uint64_t chunk = wire_chunk();
+  tr.fact("ranges", (double)R);
+  tr.fact("wire_pinned", wire_pinned ? 1 : 0);
+  uint64_t N = 0, base = 0;  // per-vote capacity (fixed after range 0), votes decoded so far
+  size_t walked = 0, done = 0;
+  bool overflow = false;
+  std::vector<RecFront> fronts;
+  hlc_votes dv{};
+  // range k's walk + scan + vote total read-back, on the walk stream behind its bytes: two kernels (the
+  // walker; one block scanning the counts and writing the total into mapped page-locked memory)
+  uint64_t* cnt_dev = nullptr;
+  HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&cnt_dev), c->pin_cnt.p, 0));
+  hipStream_t ws = c->wlk;
+  auto walk = [&](size_t k) -> int {
+    const uint64_t m0 = mb[k], mk = mb[k + 1] - m0;
+    HIPCHK(hipStreamWaitEvent(ws, c->ev_up[k], 0));
+    hlc::launch_wire_walk(0, dwire, dmoff + m0, dmlen + m0, mk, vcount + m0, nullptr, dwout + m0, dprops + m0,
+                          n_scope == 1 ? dscope : dscope + m0, n_scope, c->w_slab_off.as<uint64_t>() + m0 * slab,
+                          c->w_slab_len.as<uint32_t>() + m0 * slab, c->w_big.as<uint32_t>(), nullptr, nullptr,
+                          nullptr, c->w_huge.as<uint64_t>(), ws, c->w_first_bad.as<uint32_t>() + m0);
+    hlc::launch_wire_range_scan(vcount + m0, vbegin + m0, mk, cnt_dev + 4 * k, ws);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_cnt[k], ws));
+    tr.ev("walked_" + std::to_string(k), ws);
+    return 0;
+  };
+  // the per-vote arrays at capacity n_cap (before any kernel writes them)
+  auto size_votes = [&](uint64_t n_cap) -> int {
+    CHK(c->w_vrec_off.ensure(n_cap * 8 + 8));
+    CHK(c->w_vrec_len.ensure(n_cap * 4 + 4));
+    CHK(c->w_vrec_msg.ensure(n_cap * 4 + 4));
+    CHK(c->w_vote_err.ensure(n_cap + 1));
+    CHK(c->w_vid.ensure(n_cap * 4 + 4));
+    CHK(c->w_pid.ensure(n_cap * 4 + 4));
+    CHK(c->w_ts.ensure(n_cap * 8 + 8));
+    CHK(c->w_vote.ensure(n_cap + 1));
+    CHK(c->w_foff.ensure(n_cap * 8 * HLC_NFIELDS + 8));
+    CHK(c->w_flen.ensure(n_cap * 4 * HLC_NFIELDS + 4));
+    CHK(reserve_validate(c, n_cap, nm));
+    CHK(c->rec_work.ensure(hlc::recover_work_words(n_cap) * sizeof(uint32_t)));
+    dv.vote_id = c->w_vid.as<uint32_t>();
+    dv.proposal_id = c->w_pid.as<uint32_t>();
+    dv.timestamp = c->w_ts.as<uint64_t>();
+    dv.vote = c->w_vote.as<uint8_t>();
+    dv.bytes = dwire;
+    dv.bytes_len = wire_len;
+    dv.field_off = c->w_foff.as<uint64_t>();
+    dv.field_len = c->w_flen.as<uint32_t>();
+    return 0;
+  };
+  // range k once its total is known: records placed, Vote records decoded at vote base `base`, the
+  // first-error pass, then its recovery front half
+  auto decode = [&](size_t k) -> int {
+    const uint64_t m0 = mb[k], mk = mb[k + 1] - m0;
+    const uint64_t nv = cnt[4 * k];
+    const bool big = cnt[4 * k + 1] != 0;
+    if (k == 0) {
+      const uint64_t est = (uint64_t)((double)nv * (double)U / (double)std::max<uint64_t>(ub[1], 1) * 1.25) + 4096;
+      N = std::min(U / 2 + 1, std::max(est, c->wire_hint));
+      N = std::max(N, nv);
+      CHK(size_votes(N));
+    }
+    if (base + nv > N) {
+      overflow = true;
+      return 0;
+    }
+    hipStream_t ds = c->dec;  // behind the walk's read-back on the launch stream (already complete)
+    HIPCHK(hipStreamWaitEvent(ds, c->ev_cnt[k], 0));
+    hlc_votes dk = dv;  // the range's votes
+    dk.n = nv;
+    dk.vote_id += base;
+    dk.proposal_id += base;
+    dk.timestamp += base;
+    dk.vote += base;
+    dk.field_off += base * HLC_NFIELDS;
+    dk.field_len += base * HLC_NFIELDS;
+    uint64_t* vro = c->w_vrec_off.as<uint64_t>() + base;
+    uint32_t* vrl = c->w_vrec_len.as<uint32_t>() + base;
+    uint32_t* vrm = c->w_vrec_msg.as<uint32_t>() + base;
+    // (first_bad of the range's messages was reset by the walker)
+    if (!big) {  // every record in the walker's slab: place + decode in one kernel
+      hlc::launch_wire_votes_slab(dwire, dmoff + m0, dmlen + m0, mk, vcount + m0, vbegin + m0,
+                                  c->w_slab_off.as<uint64_t>() + m0 * slab, c->w_slab_len.as<uint32_t>() + m0 * slab,
+                                  dprops + m0, base, &dk, c->w_vote_err.as<uint8_t>() + base,
+                                  c->w_first_bad.as<uint32_t>() + m0, ds);
+    } else {
+      hlc::launch_wire_place(mk, vcount + m0, vbegin + m0, c->w_slab_off.as<uint64_t>() + m0 * slab,
+                             c->w_slab_len.as<uint32_t>() + m0 * slab, dprops + m0, vro, vrl, vrm, ds, base);
+      hlc::launch_wire_walk(1, dwire, dmoff + m0, dmlen + m0, mk, vcount + m0, vbegin + m0, dwout + m0, dprops + m0,
+                            n_scope == 1 ? dscope : dscope + m0, n_scope, nullptr, nullptr, nullptr, vro, vrl, vrm,
+                            c->w_huge.as<uint64_t>(), ds);
+      hlc::launch_wire_votes(dwire, dmoff + m0, dmlen + m0, nv, vro, vrl, vrm, vbegin + m0, &dk,
+                             c->w_vote_err.as<uint8_t>() + base, c->w_first_bad.as<uint32_t>() + m0, ds);
+    }
+    HIPCHK(hipGetLastError());
+    // the range's recovery needs the decoded signature fields only: it starts here, and the first-error
+    // pass (which only marks failed messages) follows on the decode stream
+    HIPCHK(hipEventRecord(c->ev_dec[k], ds));
+    tr.ev("decoded_" + std::to_string(k), ds);
+    hlc::launch_wire_final(mk, vbegin + m0, c->w_vote_err.as<uint8_t>() + base, c->w_first_bad.as<uint32_t>() + m0,
+                           dwout + m0, dprops + m0, ds);
+    HIPCHK(hipGetLastError());
+    if (nv) {
+      CHK(c->rec_works[k]->ensure(hlc::recover_range_words(nv) * 4));
+      CHK(launch_front(c, tr, N, k, base, nv, dwire, dk.field_off + HLC_F_SIGNATURE, HLC_NFIELDS,
+                       dk.field_len + HLC_F_SIGNATURE, HLC_NFIELDS, fronts, c->ev_dec[k]));
+    }
+    base += nv;
+    return 0;
+  };
+  // decodes every walked range whose total has come back (all of them when `wait`)
+  auto drain_counts = [&](bool wait) -> int {
+    while (done < walked && !overflow) {
+      if (wait) {
+        HIPCHK(hipEventSynchronize(c->ev_cnt[done]));
+      } else {
+        const hipError_t q = hipEventQuery(c->ev_cnt[done]);
+        if (q == hipErrorNotReady) {
+          (void)hipGetLastError();  // not an error: the total is still on its way
+          return 0;
+        }
+        HIPCHK(q);
+      }
+      tr.mark("count_" + std::to_string(done));
+      CHK(decode(done));
+      ++done;
+    }
+    return 0;
+  };
+  // 2. the wire bytes, range by range, piece by piece
+  for (size_t k = 0; k < R; ++k) {
+    for (uint64_t lo = ub[k]; lo < ub[k + 1];) {
+      const uint64_t hi = std::min(ub[k + 1], lo + chunk);
+      if (wire_pinned) {
+        CHK(st.up_from(o[3] + lo, wire + lo, hi - lo));
+      } else {
+        pool.run([&](int t, int T) {
+          const uint64_t d0 = lo + (hi - lo) * t / T, d1 = lo + (hi - lo) * (t + 1) / T;
+          if (d1 > d0) stage_copy(st.P + o[3] + d0, wire + d0, d1 - d0);
+        });
+        CHK(st.up(o[3] + lo, hi - lo));
+      }
+      lo = hi;
+      CHK(drain_counts(false));
+    }
+    HIPCHK(hipEventRecord(c->ev_up[k], c->copy));
+    tr.mark("staged_" + std::to_string(k));
+    tr.ev("landed_" + std::to_string(k), c->copy);
+    if (overflow) break;
+    CHK(walk(k));
+    ++walked;
+    CHK(drain_counts(false));
+  }
+  CHK(drain_counts(true));
+  if (overflow) {  // more votes than the first range's density promised: unpipelined, from the start
+    tr.fact("overflow_capacity", (double)N);
+    st.drain();
+    guard.armed = false;
+    c->wire_hint = std::max(c->wire_hint, N + 1);
+    return wire_host_plain(c, wire, wire_len, moff, mlen, nm, scope, n_scope, now, out_res, out_wire, out_n_votes);
+  }
+  // 4. validation over every decoded vote, one finish after the ranges' main stages
+  HIPCHK(hipEventRecord(c->ev_rest, c->dec));  // every range decoded, first-error passes included
+  HIPCHK(hipStreamWaitEvent(s, c->ev_rest, 0));
+  dv.n = base;
+  CHK(validate_device(c, &dv, dprops, nm, now, c->w_res.as<hlc_result>(), nullptr, nullptr, nullptr, s, fronts.data(),
+                      (int)fronts.size(), N));
+  hlc::launch_wire_results(nm, dwout, c->w_res.as<hlc_result>(), s);
+  HIPCHK(hipGetLastError());
+  tr.ev("kernels_end", s);
+  HIPCHK(hipMemcpyAsync(c->pin_out.p, c->w_res.p, nm * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
+  if (out_wire) HIPCHK(hipMemcpyAsync(c->pin_out.at(r1), dwout, nm * sizeof(hlc_wire_proposal), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(c->ev_done, s));
+  tr.ev("outputs_landed", s);
+  tr.mark("enqueued");
+  HIPCHK(hipEventSynchronize(c->ev_done));
+  guard.armed = false;
+  tr.mark("device_done");
+  std::memcpy(out_res, c->pin_out.p, nm * sizeof(hlc_result));
+  if (out_wire) std::memcpy(out_wire, c->pin_out.at(r1), nm * sizeof(hlc_wire_proposal));
+  if (out_n_votes) *out_n_votes = base;
+  tr.fact("capacity", (double)N);
+  c->wire_hint = std::max(c->wire_hint, base);
   tr.mark("outputs_copied");
   return 0;
 }
@@ -1266,6 +1752,10 @@ void hlc_host_free(void* p) {
 }
 
 int hlc_abi_version(void) { return HLC_ABI_VERSION; }
+
+int hlc_host_threads(void) { return host_threads(); }
+
+const char* hlc_ctx_last_host_trace(hlc_ctx* ctx) { return ctx ? ctx->last_trace.c_str() : ""; }
 
 int hlc_ctx_create(int device, hlc_ctx** out) {
   if (!out) return set_err(HLC_EINVAL, "out is NULL");
@@ -1521,26 +2011,11 @@ int hlc_validate_wire_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire
   CHK(check_wire_host(wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope));
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
-  hipStream_t s = ctx->stream;
-  CHK(stage_wire(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, s));
-  CHK(ctx->w_res.ensure(n_msgs * sizeof(hlc_result) + 16));
-  hlc_votes dv;
-  uint64_t nv = 0;
-  CHK(decode_device(ctx, ctx->w_wire.as<uint8_t>(), wire_len, ctx->w_moff.as<uint64_t>(), ctx->w_mlen.as<uint32_t>(),
-                    n_msgs, ctx->w_scope.as<hlc_scope_config>(), n_scope, ctx->w_props.as<hlc_proposal>(),
-                    ctx->w_wout.as<hlc_wire_proposal>(), &dv, &nv, s));
-  CHK(validate_device(ctx, &dv, ctx->w_props.as<hlc_proposal>(), n_msgs, now, ctx->w_res.as<hlc_result>(), nullptr,
-                      nullptr, nullptr, s));
-  hlc::launch_wire_results(n_msgs, ctx->w_wout.as<hlc_wire_proposal>(), ctx->w_res.as<hlc_result>(), s);
-  HIPCHK(hipGetLastError());
-  if (n_msgs) {
-    HIPCHK(hipMemcpyAsync(out_results, ctx->w_res.p, n_msgs * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
-    if (out_wire)
-      HIPCHK(hipMemcpyAsync(out_wire, ctx->w_wout.p, n_msgs * sizeof(hlc_wire_proposal), hipMemcpyDeviceToHost, s));
-  }
-  HIPCHK(hipStreamSynchronize(s));
-  if (out_n_votes) *out_n_votes = nv;
-  return 0;
+  if (const char* e = std::getenv("HLC_WIRE_PIPELINE"); e && std::atoi(e) == 0)  // A/B arm: unpipelined
+    return wire_host_plain(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, now, out_results, out_wire,
+                           out_n_votes);
+  return validate_wire_host(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, now, out_results, out_wire,
+                            out_n_votes);
 }
 
 }  // extern "C"

@@ -94,7 +94,8 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
                          const RecRange* range = nullptr);
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gtab, uint32_t* work,
-                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0);
+                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0,
+                           uint64_t stride = 0);  // stride: the records' row stride (0 = n; the fronts' n)
 uint64_t recover_grid_lanes();
 uint64_t recover_scratch_words();  // per-lane workspace words of k_rec_main
 uint64_t recover_work_words(uint64_t n);
@@ -140,7 +141,7 @@ void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, co
                       uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout, hlc_proposal* pout,
                       const hlc_scope_config* scope, uint64_t n_scope, uint64_t* slab_off, uint32_t* slab_len,
                       uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, uint64_t* huge,
-                      hipStream_t s);
+                      hipStream_t s, uint32_t* first_bad = nullptr);  // mode 0: first_bad[m] = ~0 when given
 // Messages longer than wire_huge_threshold() are skipped by the walker (mode 0 appends (m, len) to
 // huge[1..], count in huge[0]) and decoded by launch_huge_decode: parallel field-boundary discovery
 // (next[] per byte offset + pointer jumping), records into hoff/hlen in stream order, then
@@ -156,16 +157,28 @@ int launch_huge_decode(const uint8_t* wire, uint64_t m, uint64_t base, uint32_t 
 void launch_huge_place(uint64_t m, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* hoff,
                        const uint32_t* hlen, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg,
                        hipStream_t s);
+// (vb_base: added to vote_begin in pout[m].vote_begin -- a message range decoded on its own, with
+// vote_begin relative to its first vote; first_bad != nullptr: first_bad[m] reset to ~0 for k_wire_votes)
 void launch_wire_place(uint64_t nm, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* slab_off,
                        const uint32_t* slab_len, hlc_proposal* pout, uint64_t* vrec_off, uint32_t* vrec_len,
-                       uint32_t* vrec_msg, hipStream_t s);
+                       uint32_t* vrec_msg, hipStream_t s, uint64_t vb_base = 0, uint32_t* first_bad = nullptr);
 uint64_t wire_slab();
+// one block: vote_begin = exclusive scan of vote_count[0, nm); out_mapped (page-locked host memory, its
+// device pointer): [0] = the total, [1] = 1 if some count exceeds wire_slab()
+void launch_wire_range_scan(const uint64_t* vote_count, uint64_t* vote_begin, uint64_t nm, uint64_t* out_mapped,
+                            hipStream_t s);
 void launch_wire_touch(const uint8_t* wire, uint64_t len, uint32_t* sink, hipStream_t s);
 // decodes vote records into `out` (device SoA); first_bad[m] (pre-set to ~0) = first failing record
 void launch_wire_votes(const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nv,
                        const uint64_t* vrec_off, const uint32_t* vrec_len, const uint32_t* vrec_msg,
                        const uint64_t* vote_begin, const hlc_votes* out, uint8_t* vote_err, uint32_t* first_bad,
                        hipStream_t s);
+// k_wire_place + k_wire_votes in one kernel for messages of at most wire_slab() records (records read from
+// the walker's slab; first_bad reset by the walker); `out` at the range's first vote
+void launch_wire_votes_slab(const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
+                            const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* slab_off,
+                            const uint32_t* slab_len, hlc_proposal* pout, uint64_t vb_base, const hlc_votes* out,
+                            uint8_t* vote_err, uint32_t* first_bad, hipStream_t s);
 void launch_wire_final(uint64_t nm, const uint64_t* vote_begin, const uint8_t* vote_err, const uint32_t* first_bad,
                        hlc_wire_proposal* wout, hlc_proposal* pout, hipStream_t s);
 void launch_wire_results(uint64_t nm, const hlc_wire_proposal* wout, hlc_result* res, hipStream_t s);

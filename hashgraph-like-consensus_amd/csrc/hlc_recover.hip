@@ -212,9 +212,10 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
 // ---- comb: after the prehash, one lane per vote at full occupancy: u1 = -z / r, u1 G by the comb
 // (12 mixed additions from the HBM table), Q = u2 R + u1 G.  Votes the pre-checks rejected keep
 // their state untouched, as before the split. ----
-__global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_comb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest,
-                                                  const uint32_t* gcomb, uint8_t* state, const uint32_t* rec,
-                                                  uint32_t* q, const uint8_t* mst, int force_exact) {
+__global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_comb(uint64_t n, uint64_t st, const uint8_t* pre,
+                                                  const uint32_t* z_digest, const uint32_t* gcomb, uint8_t* state,
+                                                  const uint32_t* rec, uint32_t* q, const uint8_t* mst,
+                                                  int force_exact) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || (pre && pre[i] != PRE_PENDING)) return;
   const uint8_t m = mst[i];
@@ -226,13 +227,13 @@ __global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_comb(uint64_t n
   fe z, u1, qx, qy, qz;
   bool neg_g;
   fe_from_digest(z, z_digest + 8 * i);
-  rec_u1(z, rec + i, n, u1, neg_g);
-  const int code = rec_comb29(u1, neg_g, m == MST_INF, q + i, n, qx, qy, qz, gcomb, force_exact != 0);
+  rec_u1(z, rec + i, st, u1, neg_g);
+  const int code = rec_comb29(u1, neg_g, m == MST_INF, q + i, st, qx, qy, qz, gcomb, force_exact != 0);
   state[i] = code != SCHEME_NONE ? (uint8_t)(1 + code) : REC_PENDING;
   if (code != SCHEME_NONE) return;
-  store_fe_ws(qx, q + i, n);
-  store_fe_ws(qy, q + (size_t)8 * n + i, n);
-  store_fe_ws(qz, q + (size_t)16 * n + i, n);
+  store_fe_ws(qx, q + i, st);
+  store_fe_ws(qy, q + (size_t)8 * st + i, st);
+  store_fe_ws(qz, q + (size_t)16 * st + i, st);
 }
 
 #ifndef HLC_FIN_BATCH
@@ -243,8 +244,8 @@ constexpr int FIN_BATCH = HLC_FIN_BATCH;  // votes per lane (one inversion) in k
 // lane per vote at full occupancy) keccak of X || Y and the owner compare.  Split in two because
 // the eight keccak-f of a lane's batch made k_rec_final one long dependent chain per lane at ~1.2
 // waves/SIMD (latency-bound); the address stage runs 8x as many waves. ----
-__global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, const uint8_t* pre, uint8_t* state,
-                                                        uint32_t* q, uint32_t* pfx) {
+__global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t st, uint64_t L, const uint8_t* pre,
+                                                        uint8_t* state, uint32_t* q, uint32_t* pfx) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= L) return;
   fe acc;
@@ -255,7 +256,7 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, 
     if (i >= n) break;
     if ((pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
     fe z;
-    load_fe_ws(z, q + (size_t)16 * n + i, n);
+    load_fe_ws(z, q + (size_t)16 * st + i, st);
     store_fe_ws(acc, pfx + (size_t)k * 8 * L + t, L);
     fe_mul(acc, acc, z);
   }
@@ -266,9 +267,9 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, 
     const uint64_t i = t + (uint64_t)k * L;
     if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) continue;
     fe x, y, z, prev, zi, zi2, zi3;
-    load_fe_ws(x, q + i, n);
-    load_fe_ws(y, q + (size_t)8 * n + i, n);
-    load_fe_ws(z, q + (size_t)16 * n + i, n);
+    load_fe_ws(x, q + i, st);
+    load_fe_ws(y, q + (size_t)8 * st + i, st);
+    load_fe_ws(z, q + (size_t)16 * st + i, st);
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
     fe_mul(zi, prev, cur);  // Z_k^-1
     fe_mul(cur, cur, z);
@@ -278,19 +279,19 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t L, 
     fe_mul(y, y, zi3);
     fe_normalize(x, x);
     fe_normalize(y, y);
-    store_fe_ws(x, q + i, n);  // affine X, Y over the Jacobian ones (k_rec_addr reads them)
-    store_fe_ws(y, q + (size_t)8 * n + i, n);
+    store_fe_ws(x, q + i, st);  // affine X, Y over the Jacobian ones (k_rec_addr reads them)
+    store_fe_ws(y, q + (size_t)8 * st + i, st);
   }
 }
 
-__global__ void __launch_bounds__(256) k_rec_addr(uint64_t n, const uint8_t* pre, const uint8_t* bytes,
+__global__ void __launch_bounds__(256) k_rec_addr(uint64_t n, uint64_t st, const uint8_t* pre, const uint8_t* bytes,
                                                   const uint64_t* id_off, size_t off_stride, uint8_t* state,
                                                   const uint32_t* q, uint8_t* addr_out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) return;
   fe x, y;
-  load_fe_ws(x, q + i, n);
-  load_fe_ws(y, q + (size_t)8 * n + i, n);
+  load_fe_ws(x, q + i, st);
+  load_fe_ws(y, q + (size_t)8 * st + i, st);
   uint32_t addr[5];
   pubkey_address(x, y, addr);
   const uint8_t* id = bytes + id_off[i * off_stride];
@@ -499,16 +500,17 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
 
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb, uint32_t* work,
-                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact) {
+                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact, uint64_t stride) {
   if (!n) return;
-  const RecBufs b = rec_bufs(n, work);
+  const uint64_t st = stride ? stride : n;  // the records' row stride (>= n)
+  const RecBufs b = rec_bufs(st, work);
   const uint64_t Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
   const unsigned fb = (unsigned)((Lf + PREP_TPB - 1) / PREP_TPB);
   const unsigned vb = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(k_rec_comb, dim3(vb), dim3(256), 0, s, n, pre, z_digest, gcomb, verify_out, b.rec, b.q, b.mst,
-                     force_exact);
-  hipLaunchKernelGGL(k_rec_final, dim3(fb), dim3(PREP_TPB), 0, s, n, Lf, pre, verify_out, b.q, b.pfx);
-  hipLaunchKernelGGL(k_rec_addr, dim3(vb), dim3(256), 0, s, n, pre, bytes, id_off, off_stride, verify_out, b.q,
+  hipLaunchKernelGGL(k_rec_comb, dim3(vb), dim3(256), 0, s, n, st, pre, z_digest, gcomb, verify_out, b.rec, b.q,
+                     b.mst, force_exact);
+  hipLaunchKernelGGL(k_rec_final, dim3(fb), dim3(PREP_TPB), 0, s, n, st, Lf, pre, verify_out, b.q, b.pfx);
+  hipLaunchKernelGGL(k_rec_addr, dim3(vb), dim3(256), 0, s, n, st, pre, bytes, id_off, off_stride, verify_out, b.q,
                      addr_out);
 }
 

@@ -17,7 +17,13 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <utility>
+
+#ifndef WIRE_WALK_LDS_DEFAULT
+#define WIRE_WALK_LDS_DEFAULT 0  // the lane walker: 7.0 vs 7.35 ms for the device-resident config-2 wire step
+#endif
 
 #include "hlc_kernels.h"
 
@@ -27,6 +33,21 @@ namespace {
 
 constexpr int TPB = 256;
 constexpr int RECURSION_LIMIT = 100;  // prost DecodeContext default
+
+// Issue priority of the decode kernels' waves (s_setprio).  The wire host entry (hlc_api.cpp
+// validate_wire_host) decodes range k+1 while range k's k_rec_main grid holds the SIMDs: at the default
+// priority the walker's dependent reads got a third of the issue slots or less, and one range's walk took
+// up to 1.5 ms instead of ~0.1 ms, holding back that range's recovery.  The decode is a small amount of
+// work that gates everything after it, so its waves go first.  (Alone on the device -- the
+// device-resident wire entry -- the priority changes nothing.)
+#ifndef HLC_WIRE_PRIO
+#define HLC_WIRE_PRIO 3
+#endif
+__device__ __forceinline__ void wire_prio() {
+#if HLC_WIRE_PRIO
+  __builtin_amdgcn_s_setprio(HLC_WIRE_PRIO);
+#endif
+}
 constexpr int GROUP_STACK = RECURSION_LIMIT + 1;
 
 enum : int { WT_VARINT = 0, WT_I64 = 1, WT_LEN = 2, WT_SGROUP = 3, WT_EGROUP = 4, WT_I32 = 5 };
@@ -325,9 +346,12 @@ __global__ void __launch_bounds__(WALK_TPB) k_wire_walk(int mode, const uint8_t*
                                                    uint64_t n_scope, uint64_t* __restrict__ slab_off,
                                                    uint32_t* __restrict__ slab_len, uint32_t* __restrict__ big,
                                                    uint64_t* __restrict__ vrec_off, uint32_t* __restrict__ vrec_len,
-                                                   uint32_t* __restrict__ vrec_msg, uint64_t* __restrict__ huge) {
+                                                   uint32_t* __restrict__ vrec_msg, uint64_t* __restrict__ huge,
+                                                   uint32_t* __restrict__ first_bad) {
+  wire_prio();
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nm) return;
+  if (mode == 0 && first_bad) first_bad[m] = 0xFFFFFFFFu;  // (k_wire_votes*' atomicMin target)
   if (is_huge(msg_len[m])) {  // decoded by the parallel boundary-discovery path instead
     if (mode == 0) {
       vote_count[m] = 0;  // until launch_huge_decode
@@ -369,6 +393,70 @@ __global__ void __launch_bounds__(WALK_TPB) k_wire_walk(int mode, const uint8_t*
     for (uint32_t k = 0; k < nv; ++k) vrec_msg[vote_begin[m] + k] = (uint32_t)m;
     return;
   }
+  if (nv > SLAB) atomicOr(big, 1u);
+  emit_message(m, o, nv, err, vote_count, wout, pout, scope, n_scope);
+}
+
+// Mode-0 walk with the messages staged in LDS first: one wave per LW_MPW messages.  The wave's 64 lanes
+// copy each message's first LW_WIN bytes into LDS with 16-byte loads (coalesced, all misses in flight at
+// once), then lane j parses message j out of LDS (WinSrc: bytes past the window from global memory,
+// e.g. the tail of a message longer than the window; the name's UTF-8 check and unknown fields read
+// global memory as in k_wire_walk).  The lane-per-message walker above pays one dependent miss per
+// field (~70 per config-2 message); here a field costs a few LDS reads.  That matters most when the
+// walk shares the device with k_rec_main (the wire host entry decodes range k+1 while range k
+// recovers): there the lane walker's misses wait behind the recovery's table traffic.  Same outputs
+// as k_wire_walk mode 0, message for message.
+constexpr int LW_MPW = 4;           // messages per wave
+constexpr uint32_t LW_WIN = 12288;  // LDS bytes per message (a config-2 message is ~11.9 KB)
+
+__global__ void __launch_bounds__(64) k_wire_walk_lds(const uint8_t* __restrict__ wire, int aligned,
+                                                      const uint64_t* __restrict__ msg_off,
+                                                      const uint32_t* __restrict__ msg_len, uint64_t nm,
+                                                      uint64_t* __restrict__ vote_count,
+                                                      hlc_wire_proposal* __restrict__ wout,
+                                                      hlc_proposal* __restrict__ pout, const hlc_scope_config* scope,
+                                                      uint64_t n_scope, uint64_t* __restrict__ slab_off,
+                                                      uint32_t* __restrict__ slab_len, uint32_t* __restrict__ big,
+                                                      uint64_t* __restrict__ huge, uint32_t* __restrict__ first_bad) {
+  wire_prio();
+  __shared__ __attribute__((aligned(16))) uint8_t win[LW_MPW * LW_WIN];
+  const uint64_t m0 = (uint64_t)blockIdx.x * LW_MPW;
+  uint64_t my_lo = 0, my_len = 0;
+#pragma unroll 1
+  for (int j = 0; j < LW_MPW; ++j) {
+    const uint64_t m = m0 + j;
+    if (m >= nm) break;
+    const uint32_t len = msg_len[m];
+    if (!len || is_huge(len)) continue;
+    const uint64_t lo = msg_off[m] & ~15ull;
+    const uint64_t hi = std::min<uint64_t>(msg_off[m] + len, lo + LW_WIN);
+    load_window(win + (size_t)j * LW_WIN, wire, lo, hi, aligned != 0);
+    if ((int)threadIdx.x == j) {
+      my_lo = lo;
+      my_len = hi - lo;
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x >= LW_MPW) return;
+  const uint64_t m = m0 + threadIdx.x;
+  if (m >= nm) return;
+  if (first_bad) first_bad[m] = 0xFFFFFFFFu;
+  if (is_huge(msg_len[m])) {  // decoded by the parallel boundary-discovery path instead
+    vote_count[m] = 0;
+    const uint64_t i = atomicAdd((unsigned long long*)huge, 1ull);
+    huge[1 + 2 * i] = m;
+    huge[2 + 2 * i] = msg_len[m];
+    return;
+  }
+  const uint64_t base = msg_off[m];
+  const uint64_t end = base + msg_len[m];
+  WalkOut o = {};
+  uint32_t nv = 0;
+  int err = HLC_WIRE_OK;
+  uint64_t pos = base;
+  const WinSrc src{wire, win + (size_t)threadIdx.x * LW_WIN, my_lo, my_len};
+  while (pos < end)
+    if ((err = walk_field(src, wire, pos, base, end, o, nv, slab_off + m * SLAB, slab_len + m * SLAB, SLAB))) break;
   if (nv > SLAB) atomicOr(big, 1u);
   emit_message(m, o, nv, err, vote_count, wout, pout, scope, n_scope);
 }
@@ -590,6 +678,7 @@ __global__ void __launch_bounds__(TPB) k_huge_place(uint64_t m, const uint64_t* 
 // one cache miss per field -- hit the Infinity Cache instead of HBM.
 __global__ void __launch_bounds__(TPB) k_wire_touch(const uint8_t* __restrict__ wire, uint64_t len,
                                                     uint32_t* __restrict__ sink) {
+  wire_prio();
   uint32_t acc = 0;
   const uint64_t n16 = len / 16;
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n16; c += (uint64_t)gridDim.x * blockDim.x) {
@@ -599,18 +688,23 @@ __global__ void __launch_bounds__(TPB) k_wire_touch(const uint8_t* __restrict__ 
   if (acc == 0x9E3779B9u && len == 1) *sink = acc;  // never true: keeps the loads
 }
 
-// Slab records -> their final place (one lane per (message, record < SLAB)); vote_begin into pout.
+// Slab records -> their final place (one lane per (message, record < SLAB)); vb_base + vote_begin into pout.
 __global__ void __launch_bounds__(TPB) k_wire_place(uint64_t nm, const uint64_t* __restrict__ vote_count,
                                                     const uint64_t* __restrict__ vote_begin,
                                                     const uint64_t* __restrict__ slab_off,
                                                     const uint32_t* __restrict__ slab_len,
                                                     hlc_proposal* __restrict__ pout, uint64_t* __restrict__ vrec_off,
-                                                    uint32_t* __restrict__ vrec_len, uint32_t* __restrict__ vrec_msg) {
+                                                    uint32_t* __restrict__ vrec_len, uint32_t* __restrict__ vrec_msg,
+                                                    uint64_t vb_base, uint32_t* __restrict__ first_bad) {
+  wire_prio();
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t m = t / SLAB, k = t % SLAB;
   if (m >= nm) return;
   const uint64_t vb = vote_begin[m];
-  if (k == 0) pout[m].vote_begin = vb;
+  if (k == 0) {
+    pout[m].vote_begin = vb_base + vb;
+    if (first_bad) first_bad[m] = 0xFFFFFFFFu;  // (k_wire_votes' atomicMin target, reset here)
+  }
   const uint64_t nv = vote_count[m];
   if (nv > SLAB || k >= nv) return;  // > SLAB: k_wire_walk mode 1 writes them all
   vrec_off[vb + k] = slab_off[t];
@@ -620,45 +714,36 @@ __global__ void __launch_bounds__(TPB) k_wire_place(uint64_t nm, const uint64_t*
 
 constexpr int VOTE_WIN = 48 * 1024;  // LDS staging of a block's vote records
 
-// One Vote record per lane (prost message::merge -> merge_loop, consensus.proto:19-29): fields are
-// read from the enclosing message (bounded by its end) and the loop must stop exactly at the
-// record's end ("delimited length exceeded").  The block's records -- contiguous in the wire
-// for the usual layout -- are staged in LDS first; reads outside the staged span go to global.
-__global__ void __launch_bounds__(TPB) k_wire_votes(const uint8_t* __restrict__ wire, int aligned,
-                                                    const uint64_t* __restrict__ msg_off,
-                                                    const uint32_t* __restrict__ msg_len, uint64_t nv,
-                                                    const uint64_t* __restrict__ vrec_off,
-                                                    const uint32_t* __restrict__ vrec_len,
-                                                    const uint32_t* __restrict__ vrec_msg,
-                                                    const uint64_t* __restrict__ vote_begin, uint32_t* vote_id,
-                                                    uint32_t* proposal_id, uint64_t* timestamp, uint8_t* vote,
-                                                    uint64_t* field_off, uint32_t* field_len,
-                                                    uint8_t* __restrict__ vote_err, uint32_t* __restrict__ first_bad) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[VOTE_WIN];
-  __shared__ unsigned long long s_lo, s_hi;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// The block's record span [s_lo, s_hi) staged into LDS (a contiguous span of at most VOTE_WIN bytes;
+// scattered records are read from global memory).  Every thread calls it (it has barriers).
+__device__ __forceinline__ WinSrc stage_records(uint8_t* win, unsigned long long& s_lo, unsigned long long& s_hi,
+                                                const uint8_t* __restrict__ wire, int aligned, bool have,
+                                                uint64_t pos, uint64_t vend) {
   if (threadIdx.x == 0) {
     s_lo = ~0ull;
     s_hi = 0;
   }
   __syncthreads();
-  uint64_t pos = 0, vend = 0;
-  if (i < nv) {
-    pos = vrec_off[i];
-    vend = pos + vrec_len[i];
+  if (have) {
     atomicMin(&s_lo, (unsigned long long)pos);
     atomicMax(&s_hi, (unsigned long long)vend);
   }
   __syncthreads();
   const uint64_t wlo = s_lo & ~15ull;
   uint64_t wlen = s_hi > wlo ? s_hi - wlo : 0;
-  if (wlen > VOTE_WIN) wlen = 0;  // scattered records: read them from global memory
+  if (wlen > VOTE_WIN) wlen = 0;
   if (wlen) load_window(win, wire, wlo, wlo + wlen, aligned != 0);
   __syncthreads();
-  if (i >= nv) return;
-  const WinSrc src{wire, win, wlo, wlen};
-  const uint32_t m = vrec_msg[i];
-  const uint64_t end = msg_off[m] + msg_len[m];
+  return WinSrc{wire, win, wlo, wlen};
+}
+
+// One Vote record (prost message::merge -> merge_loop, consensus.proto:19-29): fields are read from the
+// enclosing message (bounded by its end `end`) and the loop must stop exactly at the record's end `vend`
+// ("delimited length exceeded").  Vote i of the SoA gets the decoded fields; returns the prost error.
+__device__ __forceinline__ int decode_vote(const WinSrc& src, const uint8_t* __restrict__ wire, uint64_t pos,
+                                           uint64_t vend, uint64_t end, uint64_t i, uint32_t* vote_id,
+                                           uint32_t* proposal_id, uint64_t* timestamp, uint8_t* vote,
+                                           uint64_t* field_off, uint32_t* field_len) {
   uint32_t vid = 0, pid = 0;
   uint64_t ts = 0;
   uint8_t vt = 0;
@@ -700,8 +785,69 @@ __global__ void __launch_bounds__(TPB) k_wire_votes(const uint8_t* __restrict__ 
     field_off[i * HLC_NFIELDS + f] = foff[f];
     field_len[i * HLC_NFIELDS + f] = flen[f];
   }
+  return err;
+}
+
+// One Vote record per lane, records in place (vrec_*).  The block's records -- contiguous in the wire
+// for the usual layout -- are staged in LDS first; reads outside the staged span go to global.
+__global__ void __launch_bounds__(TPB) k_wire_votes(const uint8_t* __restrict__ wire, int aligned,
+                                                    const uint64_t* __restrict__ msg_off,
+                                                    const uint32_t* __restrict__ msg_len, uint64_t nv,
+                                                    const uint64_t* __restrict__ vrec_off,
+                                                    const uint32_t* __restrict__ vrec_len,
+                                                    const uint32_t* __restrict__ vrec_msg,
+                                                    const uint64_t* __restrict__ vote_begin, uint32_t* vote_id,
+                                                    uint32_t* proposal_id, uint64_t* timestamp, uint8_t* vote,
+                                                    uint64_t* field_off, uint32_t* field_len,
+                                                    uint8_t* __restrict__ vote_err, uint32_t* __restrict__ first_bad) {
+  wire_prio();
+  __shared__ __attribute__((aligned(16))) uint8_t win[VOTE_WIN];
+  __shared__ unsigned long long s_lo, s_hi;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool have = i < nv;
+  const uint64_t pos = have ? vrec_off[i] : 0, vend = have ? pos + vrec_len[i] : 0;
+  const WinSrc src = stage_records(win, s_lo, s_hi, wire, aligned, have, pos, vend);
+  if (!have) return;
+  const uint32_t m = vrec_msg[i];
+  const int err = decode_vote(src, wire, pos, vend, msg_off[m] + msg_len[m], i, vote_id, proposal_id, timestamp, vote,
+                              field_off, field_len);
   vote_err[i] = (uint8_t)err;
   if (err) atomicMin(first_bad + m, (uint32_t)(i - vote_begin[m]));
+}
+
+// k_wire_place and k_wire_votes in one kernel, for a message range whose messages all have at most SLAB
+// vote records (the walker kept every record in its slab): one lane per (message, slab slot), records
+// read straight from the slab, vote i = vote_begin[m] + slot.  The wire host entry's per-range decode,
+// where every kernel on the chain to the range's recovery waits its turn behind the running grids.
+// first_bad[m] was reset by the walker.
+__global__ void __launch_bounds__(TPB) k_wire_votes_slab(const uint8_t* __restrict__ wire, int aligned,
+                                                         const uint64_t* __restrict__ msg_off,
+                                                         const uint32_t* __restrict__ msg_len, uint64_t nm,
+                                                         const uint64_t* __restrict__ vote_count,
+                                                         const uint64_t* __restrict__ vote_begin,
+                                                         const uint64_t* __restrict__ slab_off,
+                                                         const uint32_t* __restrict__ slab_len,
+                                                         hlc_proposal* __restrict__ pout, uint64_t vb_base,
+                                                         uint32_t* vote_id, uint32_t* proposal_id, uint64_t* timestamp,
+                                                         uint8_t* vote, uint64_t* field_off, uint32_t* field_len,
+                                                         uint8_t* __restrict__ vote_err,
+                                                         uint32_t* __restrict__ first_bad) {
+  wire_prio();
+  __shared__ __attribute__((aligned(16))) uint8_t win[VOTE_WIN];
+  __shared__ unsigned long long s_lo, s_hi;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t m = t / SLAB, k = t % SLAB;
+  const bool inm = m < nm;
+  const bool have = inm && k < vote_count[m];
+  if (inm && k == 0) pout[m].vote_begin = vb_base + vote_begin[m];
+  const uint64_t pos = have ? slab_off[t] : 0, vend = have ? pos + slab_len[t] : 0;
+  const WinSrc src = stage_records(win, s_lo, s_hi, wire, aligned, have, pos, vend);
+  if (!have) return;
+  const uint64_t i = vote_begin[m] + k;
+  const int err = decode_vote(src, wire, pos, vend, msg_off[m] + msg_len[m], i, vote_id, proposal_id, timestamp, vote,
+                              field_off, field_len);
+  vote_err[i] = (uint8_t)err;
+  if (err) atomicMin(first_bad + m, (uint32_t)k);
 }
 
 // First error in stream order: a failing vote record precedes every later top-level error.
@@ -711,6 +857,7 @@ __global__ void __launch_bounds__(TPB) k_wire_final(uint64_t nm, const uint64_t*
                                                     const uint32_t* __restrict__ first_bad,
                                                     hlc_wire_proposal* __restrict__ wout,
                                                     hlc_proposal* __restrict__ pout) {
+  wire_prio();
   const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nm) return;
   const uint32_t fb = first_bad[m];
@@ -741,22 +888,77 @@ __global__ void __launch_bounds__(TPB) k_wire_results(uint64_t nm, const hlc_wir
   res[m] = r;
 }
 
+// The wire host entry's per-range scan + read-back, one block: vote_begin = the exclusive scan of the
+// range's vote counts; out[0] = the range's vote total, out[1] = 1 when a message has more records than
+// the walker's slab (its second walk is needed).  `out` is page-locked host memory mapped for the
+// device, written with system-scope stores: the host reads it once the event behind this kernel has
+// fired -- one kernel instead of a flag memset, a two-kernel library scan and a device-to-host copy,
+// each of which waits its turn behind the recovery grids when the device is busy.
+constexpr int RS_TPB = 1024;
+__global__ void __launch_bounds__(RS_TPB) k_wire_range_scan(const uint64_t* __restrict__ vote_count,
+                                                            uint64_t* __restrict__ vote_begin, uint64_t nm,
+                                                            uint64_t* out) {
+  wire_prio();
+  __shared__ uint64_t part[RS_TPB];
+  __shared__ uint64_t carry_s;
+  __shared__ uint32_t big_s;
+  if (threadIdx.x == 0) {
+    carry_s = 0;
+    big_s = 0;
+  }
+  __syncthreads();
+  for (uint64_t b0 = 0; b0 < nm; b0 += RS_TPB) {
+    const uint64_t m = b0 + threadIdx.x;
+    const uint64_t v = m < nm ? vote_count[m] : 0;
+    if (v > SLAB) big_s = 1;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < RS_TPB; d <<= 1) {  // inclusive Hillis-Steele scan of the block's counts
+      const uint64_t x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+      __syncthreads();
+      part[threadIdx.x] += x;
+      __syncthreads();
+    }
+    const uint64_t c = carry_s;
+    if (m < nm) vote_begin[m] = c + part[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == RS_TPB - 1) carry_s = c + part[RS_TPB - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(out, carry_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out + 1, (uint64_t)big_s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB); }
 
 }  // namespace
 
 static int is_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// the mode-0 walker (HLC_WIRE_WALK: "lds" = k_wire_walk_lds, "lane" = k_wire_walk; default below)
+static bool walk_lds() {
+  const char* e = std::getenv("HLC_WIRE_WALK");
+  return e ? std::strcmp(e, "lane") != 0 : WIRE_WALK_LDS_DEFAULT;
+}
+
 void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
                       uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout, hlc_proposal* pout,
                       const hlc_scope_config* scope, uint64_t n_scope, uint64_t* slab_off, uint32_t* slab_len,
                       uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, uint64_t* huge,
-                      hipStream_t s) {
+                      hipStream_t s, uint32_t* first_bad) {
   if (!nm) return;
+  if (mode == 0 && walk_lds()) {
+    hipLaunchKernelGGL(k_wire_walk_lds, dim3((unsigned)((nm + LW_MPW - 1) / LW_MPW)), dim3(64), 0, s, wire,
+                       is_aligned16(wire), msg_off, msg_len, nm, vote_count, wout, pout, scope, n_scope, slab_off,
+                       slab_len, big, huge, first_bad);
+    return;
+  }
   hipLaunchKernelGGL(k_wire_walk, dim3((unsigned)((nm + WALK_TPB - 1) / WALK_TPB)), dim3(WALK_TPB), 0, s, mode, wire, is_aligned16(wire), msg_off,
                      msg_len, nm,
                      vote_count, vote_begin, wout, pout, scope, n_scope, slab_off, slab_len, big, vrec_off,
-                     vrec_len, vrec_msg, huge);
+                     vrec_len, vrec_msg, huge, first_bad);
 }
 
 uint64_t wire_huge_threshold() { return HUGE_MSG; }
@@ -827,13 +1029,18 @@ void launch_huge_place(uint64_t m, const uint64_t* vote_count, const uint64_t* v
 
 void launch_wire_place(uint64_t nm, const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* slab_off,
                        const uint32_t* slab_len, hlc_proposal* pout, uint64_t* vrec_off, uint32_t* vrec_len,
-                       uint32_t* vrec_msg, hipStream_t s) {
+                       uint32_t* vrec_msg, hipStream_t s, uint64_t vb_base, uint32_t* first_bad) {
   if (!nm) return;
   hipLaunchKernelGGL(k_wire_place, dim3(blocks_for(nm * SLAB)), dim3(TPB), 0, s, nm, vote_count, vote_begin, slab_off,
-                     slab_len, pout, vrec_off, vrec_len, vrec_msg);
+                     slab_len, pout, vrec_off, vrec_len, vrec_msg, vb_base, first_bad);
 }
 
 uint64_t wire_slab() { return SLAB; }
+
+void launch_wire_range_scan(const uint64_t* vote_count, uint64_t* vote_begin, uint64_t nm, uint64_t* out_mapped,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_wire_range_scan, dim3(1), dim3(RS_TPB), 0, s, vote_count, vote_begin, nm, out_mapped);
+}
 
 void launch_wire_touch(const uint8_t* wire, uint64_t len, uint32_t* sink, hipStream_t s) {
   if (len < 16 || !is_aligned16(wire)) return;
@@ -850,6 +1057,18 @@ void launch_wire_votes(const uint8_t* wire, const uint64_t* msg_off, const uint3
                      const_cast<uint32_t*>(out->proposal_id), const_cast<uint64_t*>(out->timestamp),
                      const_cast<uint8_t*>(out->vote), const_cast<uint64_t*>(out->field_off),
                      const_cast<uint32_t*>(out->field_len), vote_err, first_bad);
+}
+
+void launch_wire_votes_slab(const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
+                            const uint64_t* vote_count, const uint64_t* vote_begin, const uint64_t* slab_off,
+                            const uint32_t* slab_len, hlc_proposal* pout, uint64_t vb_base, const hlc_votes* out,
+                            uint8_t* vote_err, uint32_t* first_bad, hipStream_t s) {
+  if (!nm) return;
+  hipLaunchKernelGGL(k_wire_votes_slab, dim3(blocks_for(nm * SLAB)), dim3(TPB), 0, s, wire, is_aligned16(wire), msg_off,
+                     msg_len, nm, vote_count, vote_begin, slab_off, slab_len, pout, vb_base,
+                     const_cast<uint32_t*>(out->vote_id), const_cast<uint32_t*>(out->proposal_id),
+                     const_cast<uint64_t*>(out->timestamp), const_cast<uint8_t*>(out->vote),
+                     const_cast<uint64_t*>(out->field_off), const_cast<uint32_t*>(out->field_len), vote_err, first_bad);
 }
 
 void launch_wire_final(uint64_t nm, const uint64_t* vote_begin, const uint8_t* vote_err, const uint32_t* first_bad,

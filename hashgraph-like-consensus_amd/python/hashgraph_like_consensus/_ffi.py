@@ -6,8 +6,10 @@ loudly (`HlcUnavailable`).
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 from ctypes import POINTER, c_char_p, c_double, c_int, c_uint8, c_uint32, c_uint64, c_void_p
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -134,6 +136,7 @@ EXPORTED_SYMBOLS = (
     "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
     "hlc_process_votes", "hlc_process_votes_device", "hlc_synth_arena_bytes", "hlc_synth_votes_device",
     "hlc_synth_byzantine_device", "hlc_outcome_counts_device", "hlc_host_alloc", "hlc_host_free",
+    "hlc_host_threads", "hlc_ctx_last_host_trace",
 )
 
 _lib = None
@@ -167,6 +170,10 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_host_alloc.restype = c_int
     lib.hlc_host_free.argtypes = [c_void_p]
     lib.hlc_host_free.restype = None
+    lib.hlc_host_threads.argtypes = []
+    lib.hlc_host_threads.restype = c_int
+    lib.hlc_ctx_last_host_trace.argtypes = [vp]
+    lib.hlc_ctx_last_host_trace.restype = c_char_p
     lib.hlc_compute_vote_hashes.argtypes = [vp, POINTER(hlc_votes), u8p]
     lib.hlc_compute_vote_hashes.restype = c_int
     lib.hlc_eth_verify_batch.argtypes = [vp, c_uint64, u8p, c_uint64, u64p, u32p, u64p, u32p,
@@ -219,6 +226,28 @@ def load_library(path: str = LIB_PATH):
     return lib
 
 
+# Every live context owner (engine.Engine): destroyed by an atexit hook, so that no libhlc context --
+# its streams, events, device / page-locked buffers and the parked threads of its host staging pool --
+# is left for the process's library finalizers (__cxa_finalize of libhlc and the HIP runtime) to
+# tear down in an unspecified order (a SIGSEGV inside __cxa_finalize after the
+# outputs were written, under rocprofv3).  Python's atexit hooks run before those finalizers.
+_live = weakref.WeakSet()
+
+
+def register_owner(obj) -> None:
+    """Adds an object with a close() method to the set destroyed at interpreter exit."""
+    _live.add(obj)
+
+
+@atexit.register
+def _close_live_owners() -> None:
+    for obj in list(_live):
+        try:
+            obj.close()
+        except Exception:  # noqa: BLE001 -- best effort at exit
+            pass
+
+
 def check(rc: int) -> None:
     if rc != 0:
         msg = _lib.hlc_last_error().decode(errors="replace") if _lib is not None else ""
@@ -235,7 +264,8 @@ def ptr(arr, ctype):
 class PinnedArena:
     """Page-locked host memory from hlc_host_alloc, handed out as numpy arrays (`take`): input
     arrays built here reach the device without the host-buffer entries' staging copy.  Freed with
-    the object (keep it alive while its arrays are in use)."""
+    the object, which every array taken from it keeps alive; an explicit close() frees it at once
+    (only when none of its arrays is used again)."""
 
     def __init__(self, nbytes: int):
         import numpy as np
@@ -244,6 +274,9 @@ class PinnedArena:
         check(self._lib.hlc_host_alloc(max(int(nbytes), 1), ctypes.byref(self._p)))
         self.nbytes = int(nbytes)
         buf = (ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self._p.value)
+        # every array carved out of the arena has this buffer at the root of its base chain: the
+        # arena stays alive (and its memory allocated) while any of them does
+        buf._owner = self
         self._u8 = np.frombuffer(buf, dtype=np.uint8)
         self._used = 0
 

@@ -149,6 +149,25 @@ class DeviceBatch:
             priv = self.priv[: n * 32].cpu().numpy().reshape(-1, 32)
         return batch, self.desc_numpy().copy(), priv
 
+    def host_prefix(self, p: int):
+        """The first `p` proposals with every vote up to their last one and the arena up to the last
+        byte those votes reference, copied back to the host: (VoteBatch, desc).  No re-basing -- the
+        cheap host sample of a large device-generated shard (bench.py's CPU baseline at N > 1)."""
+        self.torch.cuda.synchronize(self.device)
+        t = self._t
+        desc = self.desc_numpy()[:p].copy()
+        nv = int((desc["vote_begin"] + desc["vote_count"]).max()) if p else 0
+
+        def arr(name, dtype, width=1):
+            a = t[name][: nv * np.dtype(dtype).itemsize * width].cpu().numpy().view(dtype)
+            return a.reshape(-1, width) if width > 1 else a
+
+        foff, flen = arr("field_off", np.uint64, 5), arr("field_len", np.uint32, 5)
+        end = int((foff + flen).max()) if nv else 0
+        batch = VoteBatch(arr("vote_id", np.uint32), arr("proposal_id", np.uint32), arr("timestamp", np.uint64),
+                          arr("vote", np.uint8), t["bytes"][:max(end, 1)].cpu().numpy()[:end], foff, flen)
+        return batch, desc
+
     def host_proposals(self, idx) -> tuple:
         """Proposals `idx` (indices into this batch) with their votes copied back to the host as a
         self-contained (VoteBatch, desc, global vote index) triple -- the CPU cross-check of a

@@ -38,6 +38,7 @@ class Engine:
         _ffi.check(self.lib.hlc_ctx_create(device, ctypes.byref(h)))
         self.ctx = h
         self.device = device
+        _ffi.register_owner(self)  # destroyed at interpreter exit if the caller never closes it
 
     @classmethod
     def default(cls) -> "Engine":
@@ -49,9 +50,9 @@ class Engine:
             return cls._default
 
     def close(self) -> None:
-        if self.ctx:
-            self.lib.hlc_ctx_destroy(self.ctx)
-            self.ctx = None
+        ctx, self.ctx = getattr(self, "ctx", None), None
+        if ctx:
+            self.lib.hlc_ctx_destroy(ctx)
 
     def __del__(self):  # pragma: no cover
         try:
@@ -109,7 +110,18 @@ class Engine:
         """hlc_eth_verify_batch over pre-packed arrays (one byte arena, per-item u64 offsets and u32
         lengths, contiguous): no per-item Python work.  -> (status[n], recovered[n,20] or None); `out`
         reuses caller-owned output arrays."""
+        # the C ABI reads raw u8 / u64 / u32 arrays: convert (a copy only when needed) and check the
+        # per-item arrays agree in length before any pointer crosses (ADVICE r04)
+        arena = np.ascontiguousarray(arena, dtype=np.uint8).reshape(-1)
+        id_off, pay_off, sig_off = (np.ascontiguousarray(a, dtype=np.uint64).reshape(-1) for a in (id_off, pay_off, sig_off))
+        id_len, pay_len, sig_len = (np.ascontiguousarray(a, dtype=np.uint32).reshape(-1) for a in (id_len, pay_len, sig_len))
         n = int(id_off.shape[0])
+        if any(a.shape[0] != n for a in (id_len, pay_off, pay_len, sig_off, sig_len)):
+            raise ValueError("eth_verify_arrays: per-item arrays differ in length")
+        if out is not None and (out[0].dtype != np.uint8 or out[0].size < n or not out[0].flags.c_contiguous or
+                                (want_addr and (out[1] is None or out[1].dtype != np.uint8 or out[1].size < 20 * n
+                                                or not out[1].flags.c_contiguous))):
+            raise ValueError("eth_verify_arrays: `out` must be contiguous u8 arrays of n and n x 20")
         if out is None:
             st = np.zeros(max(n, 1), np.uint8)
             addr = np.zeros((max(n, 1), 20), np.uint8) if want_addr else None
@@ -281,6 +293,12 @@ class Engine:
             self.ctx, dwire.wire_ptr, dwire.wire_len, dwire.off_ptr, dwire.len_ptr, dwire.n_msgs, dwire.scope_ptr,
             dwire.n_scope, dwire.now, dwire.results_ptr, dwire.winfo_ptr,
             c_void_p(stream_handle) if stream_handle else None))
+
+    def last_host_trace(self) -> Optional[dict]:
+        """The last host-buffer call's phase times (HLC_HOST_TRACE=1 or 2 in the environment), or None."""
+        import json
+        raw = self.lib.hlc_ctx_last_host_trace(self.ctx)
+        return json.loads(raw.decode()) if raw else None
 
     def set_kernel_timing(self, enable: bool) -> None:
         _ffi.check(self.lib.hlc_ctx_set_kernel_timing(self.ctx, 1 if enable else 0))

@@ -227,6 +227,17 @@ int hlc_abi_version(void);
 int hlc_host_alloc(uint64_t bytes, void** out);
 void hlc_host_free(void* p);
 
+/* Host threads (including the caller's) the host-buffer entries (hlc_validate_proposals,
+ * hlc_validate_wire_proposals, hlc_eth_verify_batch) stage their copies with: HLC_HOST_THREADS when
+ * set, else min(16, hardware threads, the process's CPU share = the cgroup CPU quota (or the hardware
+ * threads) / LOCAL_WORLD_SIZE, the ranks on the node).  Read when a context first stages. */
+int hlc_host_threads(void);
+
+/* With HLC_HOST_TRACE=1 (also printed on stderr) or 2 in the environment: the last host-buffer call's
+ * phase times on this context as JSON -- {"host": {phase: ms}, "device": {event: ms}}, ms from the
+ * call's start; "" otherwise.  Valid until the next call on the context. */
+const char* hlc_ctx_last_host_trace(hlc_ctx* ctx);
+
 /* ---- Measurement hooks (bench.py roofline): HIP events on the launch stream ------ */
 /* enable != 0: every validate-many call records hipEvents around the signature-recovery
  * kernels (k_rec_prep and k_rec_main on the context's second stream; k_rec_comb, k_rec_final and

@@ -160,3 +160,42 @@ def test_wire_struct_layout_and_codes(tmp_path):
                  "RECURSION_LIMIT"):
         assert d["HLC_WIRE_" + name] == getattr(wo, name), name
     assert d["HLC_PROPOSAL_DECODE_ERROR"] == 17 and d["HLC_ERANGE"] == -5
+
+
+def _threads_in_child(env_extra):
+    """hlc_host_threads() in a fresh process with `env_extra` set (no GPU call is made)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from hashgraph_like_consensus import _ffi; "
+            "print(_ffi.load_library().hlc_host_threads())" % os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
+    env = {k: v for k, v in os.environ.items() if k not in ("HLC_HOST_THREADS", "LOCAL_WORLD_SIZE")}
+    env.update(env_extra)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    return int(out.stdout.strip())
+
+
+def _cpu_share():
+    """The CPUs this process may use by the library's rule: the cgroup v2 quota, else the hardware threads."""
+    hw = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            return min(float(q) / float(per), hw), hw
+    except (OSError, ValueError):
+        pass
+    return float(hw), hw
+
+
+def test_host_threads_default_is_rank_aware():
+    """the host-buffer entries' staging threads default to min(16, hardware
+    threads, the CPU quota / the ranks on the node), so 8 ranks on one node do not run 8 x 16 staging
+    threads on one quota; HLC_HOST_THREADS overrides (clamped to 1..64)."""
+    share, hw = _cpu_share()
+    for ranks in (1, 2, 8, 64):
+        want = max(1, min(16, hw, int(share / ranks + 1e-9)))
+        assert _threads_in_child({"LOCAL_WORLD_SIZE": str(ranks)}) == want, ranks
+    assert _threads_in_child({}) == max(1, min(16, hw, int(share + 1e-9)))
+    assert _threads_in_child({"HLC_HOST_THREADS": "5", "LOCAL_WORLD_SIZE": "8"}) == 5
+    assert _threads_in_child({"HLC_HOST_THREADS": "500"}) == 64

@@ -220,3 +220,57 @@ def test_gpu_host_entry_no_votes(engine):
     cres, _, _, _ = coracle.validate_proposals(b, d, 1_760_001_800, threads=1)
     assert np.array_equal(res, cres)
     assert (res["status"] == 0).all() and (res["transition"] == 0).all()
+
+
+def _hip_register():
+    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+def test_gpu_host_entry_split_registration_is_staged(engine, byz):
+    """VERDICT r04 item 5 / ADVICE r04: an input array whose first and last bytes are page-locked but
+    in two different registrations (two adjacent hipHostRegister blocks, or a first and a last page with
+    pageable memory between) is staged, not DMA'd straight from the caller as one block; one
+    registration covering the whole array is DMA'd directly.  Outcomes equal the oracle every time
+    (the HLC_HOST_TRACE pinned_mask fact shows which arrays went direct: bit 4 = field_off)."""
+    b, d, now = byz
+    hip = _hip_register()
+    page = 4096
+    fo = np.ascontiguousarray(b.field_off)
+    nb = fo.nbytes
+    raw = np.zeros(nb + 3 * page, np.uint8)
+    start = (-raw.ctypes.data) % page
+    buf = raw[start:start + nb + page]
+    view = buf[:nb].view(np.uint64).reshape(fo.shape)
+    view[...] = fo
+    assert nb > 3 * page
+    base = buf.ctypes.data
+    mid = (nb // 2) // page * page
+    cb = type(b)(b.vote_id, b.proposal_id, b.timestamp, b.vote, b.arena, view, b.field_len)
+    cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
+
+    def run():
+        os.environ["HLC_HOST_TRACE"] = "2"
+        try:
+            got = engine.validate_proposals(cb, d, now, want_votes=True, want_recovered=True)
+            mask = int(engine.last_host_trace()["facts"]["pinned_mask"])
+        finally:
+            os.environ.pop("HLC_HOST_TRACE", None)
+        assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
+        assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec)
+        return (mask >> 4) & 1
+
+    assert run() == 0  # pageable
+    layouts = [[(0, mid), (mid, nb + page - mid)],               # two adjacent registrations
+               [(0, page), (nb - nb % page - page, 2 * page)],   # first and last pages, pageable between
+               [(0, nb + page)]]                                 # one registration: direct DMA
+    for k, regs in enumerate(layouts):
+        for o, ln in regs:
+            assert hip.hipHostRegister(ctypes.c_void_p(base + o), ln, 0) == 0, (k, o, ln)
+        try:
+            assert run() == (1 if k == 2 else 0), f"layout {k}"
+        finally:
+            for o, _ in regs:
+                assert hip.hipHostUnregister(ctypes.c_void_p(base + o)) == 0

@@ -11,6 +11,8 @@
 #   n2         N = 2 dry run of the sharded bench (gloo, both ranks on GPU 0): config-4 shards
 #   rccl1      the N > 1 bench path at one rank over RCCL (HLC_BENCH_DIST=1): config-4 shard, exchange on GPU
 #   pipe       tools/host_pipe.py sweep, arguments from $PIPE_ARGS
+#   wirepipe   tools/wire_pipe.py sweep (the wire entry from host buffers), arguments from $WIRE_ARGS
+#   fetchcalib tools/fetch_calib under rocprofv3 FETCH_SIZE / WRITE_SIZE passes: counter bytes per access shape
 #   pipetrace  rocprofv3 kernel + memory-copy trace of one host-buffer setting ($PIPE_ARGS)
 #   verify     tools/verify_latency.py (hlc_eth_verify_batch at the C ABI)
 #   profile    tools/profile.sh TAG (kernel trace + PMC passes of the headline leg)
@@ -60,6 +62,18 @@ for step in "$@"; do
   pipe)
     timeout -k 10 500 python tools/host_pipe.py $PIPE_ARGS > $O/pipe_$TAG.txt 2> $O/pipe_$TAG.err || fail pipe $O/pipe_$TAG.err
     cat $O/pipe_$TAG.txt ;;
+  wirepipe)
+    timeout -k 10 500 python tools/wire_pipe.py $WIRE_ARGS > $O/wirepipe_$TAG.txt 2> $O/wirepipe_$TAG.err || fail wirepipe $O/wirepipe_$TAG.err
+    cat $O/wirepipe_$TAG.txt ;;
+  fetchcalib)
+    OUT=$PWD/$O/fetchcalib_$TAG
+    mkdir -p $OUT
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 $OLDPWD/tools/fetch_calib > $OUT/plain.txt 2>&1 && \
+      timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $OLDPWD/tools/fetch_calib \
+        > $OUT/fetch.txt 2>&1 && \
+      timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $OLDPWD/tools/fetch_calib \
+        > $OUT/write.txt 2>&1) || fail fetchcalib $OUT/fetch.txt
+    python tools/fetch_calib.py $OUT/fetch $OUT/write $OUT/plain.txt | tee $OUT/summary.json ;;
   pipetrace)
     OUT=$PWD/$O/pipetrace_$TAG
     mkdir -p $OUT
