@@ -184,3 +184,30 @@ def test_gpu_verify_batch_rejects_out_of_arena_outputs_untouched(engine):
     st, addr = engine.eth_verify_arrays(arena, offs[:n], lens[:n], offs[n:2 * n], lens[n:2 * n], offs[2 * n:],
                                         lens[2 * n:])
     assert [int(x) for x in st] == _oracle_verify(ids, pays, sigs)[0]
+
+
+def test_gpu_verify_large_payloads(engine):
+    """hlc_eth_verify_batch hashes each payload in one lane (k_verify_prehash: the EIP-191
+    keccak sponge is sequential per message, so one item's latency grows with its length -- about one
+    keccak-f per 136 bytes).  Payloads across the block and digit-count boundaries and up to 1 MiB, mixed
+    with short ones in one batch, equal the C oracle (its keccak, its recovery) item for item; a flipped
+    byte deep inside the 1 MiB payload is a well-formed mismatch (status 1), not an error."""
+    rnd = random.Random(77)
+    lens = [0, 9, 99, 100, 135, 136, 137, 271, 272, 999, 1000, 4096, 65535, 65536, 1 << 20]
+    ids, pays, sigs = [], [], []
+    for k, ln in enumerate(lens + [20] * 16):
+        d = rnd.randrange(1, po.N)
+        msg = rnd.randbytes(ln)
+        ids.append(coracle_addr(d))
+        pays.append(msg)
+        sigs.append(coracle_sign(d, msg))
+    big = bytearray(pays[len(lens) - 1])
+    big[700_001] ^= 0x40
+    ids.append(ids[len(lens) - 1])
+    pays.append(bytes(big))
+    sigs.append(sigs[len(lens) - 1])
+    exp_st, exp_addr = _oracle_verify(ids, pays, sigs)
+    st, addr = engine.eth_verify_batch(ids, pays, sigs)
+    assert [int(x) for x in st] == exp_st
+    assert [a.tobytes() for a in addr] == exp_addr
+    assert exp_st[:len(lens)] == [0] * len(lens) and exp_st[-1] == 1

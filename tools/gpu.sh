@@ -13,6 +13,8 @@
 #   pipe       tools/host_pipe.py sweep, arguments from $PIPE_ARGS
 #   wirepipe   tools/wire_pipe.py sweep (the wire entry from host buffers), arguments from $WIRE_ARGS
 #   fetchcalib tools/fetch_calib under rocprofv3 FETCH_SIZE / WRITE_SIZE passes: counter bytes per access shape
+#   counters   rocprofv3 -L on the box; tools/fetch_calib under the L2 request-size counters when present
+#   teardownprof  tools/host_pipe.py under rocprofv3 --kernel-trace --stats: exit status must be 0
 #   pipetrace  rocprofv3 kernel + memory-copy trace of one host-buffer setting ($PIPE_ARGS)
 #   verify     tools/verify_latency.py (hlc_eth_verify_batch at the C ABI)
 #   profile    tools/profile.sh TAG (kernel trace + PMC passes of the headline leg)
@@ -74,6 +76,27 @@ for step in "$@"; do
       timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $OLDPWD/tools/fetch_calib \
         > $OUT/write.txt 2>&1) || fail fetchcalib $OUT/fetch.txt
     python tools/fetch_calib.py $OUT/fetch $OUT/write $OUT/plain.txt | tee $OUT/summary.json ;;
+  counters)
+    # the counters this rocprofv3 offers on the box, then (when it has them) tools/fetch_calib under the L2's
+    # request-size counters: which shapes issue 128-B requests that FETCH_SIZE tallies at 64 B
+    OUT=$PWD/$O/counters_$TAG
+    mkdir -p $OUT
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 -L > $OUT/list.txt 2>&1) || true
+    grep -o "TCC_[A-Z0-9_]*" $OUT/list.txt | sort -u > $OUT/tcc.txt || true
+    if grep -qx "TCC_BUBBLE" $OUT/tcc.txt && grep -qx "TCC_EA0_RDREQ" $OUT/tcc.txt; then
+      EXTRA=""
+      grep -qx "TCC_EA0_RDREQ_32B" $OUT/tcc.txt && EXTRA="TCC_EA0_RDREQ_32B"
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ TCC_BUBBLE $EXTRA --output-format csv \
+        -d $OUT/req -o run -- $OLDPWD/tools/fetch_calib > $OUT/req.txt 2>&1) || echo "request-size pass failed"
+    fi
+    wc -l $OUT/tcc.txt ;;
+  teardownprof)
+    # the host pipeline tool under rocprofv3 must exit 0 (no SIGSEGV in the finalizers)
+    OUT=$PWD/$O/teardown_$TAG
+    mkdir -p $OUT
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT \
+      -o run -- python3 $OLDPWD/tools/host_pipe.py --steps 3 > $OUT/out.txt 2> $OUT/err.txt; echo "exit $?" > $OUT/rc.txt)
+    cat $OUT/rc.txt; grep -q "exit 0" $OUT/rc.txt || fail teardownprof $OUT/err.txt ;;
   pipetrace)
     OUT=$PWD/$O/pipetrace_$TAG
     mkdir -p $OUT
