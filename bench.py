@@ -76,22 +76,67 @@ def pmc_duration_ms(name: str, kernel: str):
     return sum(durs) / len(durs) if durs else None
 
 
+# Memory-side read bytes from the L2's request counters.  gfx950's FETCH_SIZE is
+# (TCC_BUBBLE*128 + (TCC_EA0_RDREQ - TCC_BUBBLE - TCC_EA0_RDREQ_32B)*64 + TCC_EA0_RDREQ_32B*32) / 1024 KiB,
+# and TCC_BUBBLE reads 0 on this box, so every request is tallied at 64 B.  Calibrated with
+# tools/fetch_calib.hip (profiles/r05/fetch_calibration.json, fetch_calib_requests.csv): coalesced streams
+# of 16-, 4- and 1-byte loads per lane issue 128-B requests (FETCH_SIZE = exactly 1/2 of their bytes);
+# a lane's own 64-B entry (4 x 16-B loads) is one 64-B request (FETCH_SIZE = its bytes); 32-B and 16-B
+# pieces at scattered addresses cost a whole 64-B request each (FETCH_SIZE = 2x / 4x the useful bytes --
+# real traffic, the granule the fabric moves).  So the memory-side read bytes of a kernel are
+#   128 x TCC_EA0_RDREQ_128B + 64 x (TCC_EA0_RDREQ - _128B - _32B) + 32 x _32B
+# when the committed profile has that pass (pmc_req); otherwise FETCH_SIZE x the factor of the kernel's
+# dominant load shape below, with FETCH_SIZE itself (`fetch_raw_bytes`) beside it.
+FETCH_SHAPE = {
+    "k_rec_prep": (2.0, "coalesced: the signatures (65-B records of consecutive votes), the skip-list fields"),
+    "k_rec_main": (1.0, "per-lane gathers of 64-B R-table entries dominate (52 per vote, 3.3 KB)"),
+    "k_rec_comb": (1.0, "per-lane gathers of 64-B comb entries dominate (12 per vote, 768 B; records and Q are "
+                        "~270 B/vote of coalesced loads, under-counted by half)"),
+    "k_rec_final": (2.0, "coalesced word-major Q / prefix products"),
+    "k_rec_addr": (2.0, "coalesced word-major Q (64 B/vote); the 20-B owner reads are scattered"),
+    "k_chain_small": (1.0, "per-lane reads of owner / hash fields at scattered arena offsets"),
+    "k_clear_if": (2.0, "streaming"),
+    "k_tables": (1.0, "scattered key reads and table probes"),
+    "k_chain_check": (1.0, "scattered key reads and table probes"),
+    "k_vote_status": (2.0, "coalesced per-vote bytes"),
+    "k_finalize": (2.0, "coalesced per-proposal records"),
+}
+REQ_COUNTERS = ("TCC_EA0_RDREQ", "TCC_EA0_RDREQ_128B", "TCC_EA0_RDREQ_32B")
+
+
+def read_bytes(kernel: str, fetch_kib, req_pass: str = "pmc_req"):
+    """(memory-side read bytes per launch, basis) for `kernel`: from the request-size pass when the
+    committed profile has it, else FETCH_SIZE x the kernel's shape factor (FETCH_SHAPE)."""
+    req = {c: pmc_per_launch(req_pass, c, kernel) for c in REQ_COUNTERS}
+    if all(v is not None for v in req.values()):
+        rd, r128, r32 = (req[c] for c in REQ_COUNTERS)
+        return 128.0 * r128 + 64.0 * (rd - r128 - r32) + 32.0 * r32, "request counters (pmc_req)"
+    f, why = FETCH_SHAPE.get(kernel, (1.0, "unclassified: FETCH_SIZE as counted"))
+    return f * fetch_kib * 1024.0, f"FETCH_SIZE x {f:g} ({why})"
+
+
 def pmc_traffic():
-    """Per-launch memory-side bytes of the recovery kernels from the committed FETCH_SIZE /
-    WRITE_SIZE passes (KiB), FETCH doubled per the gfx950 note of MI355X_MICROARCH.md (exact for
-    16-B-per-lane streams; the per-lane table gathers are uncalibrated, so `fetch_raw_bytes` is
-    given beside it), or None."""
+    """Per-launch memory-side bytes of the recovery kernels from the committed profile: reads by
+    read_bytes() (request counters, or FETCH_SIZE by the kernel's load shape), writes from WRITE_SIZE
+    (exact for every shape calibrated, profiles/r05/fetch_calibration.json).  `fetch_raw_bytes` is
+    FETCH_SIZE as counted; `fetch_x2_bytes` the round-4 blanket doubling, for comparison."""
     out = {}
     for k in REC_KERNELS:
         f = pmc_per_launch("pmc_fetch", "FETCH_SIZE", k)
         w = pmc_per_launch("pmc_write", "WRITE_SIZE", k)
         if f is None or w is None:
             return None
-        out[k] = {"fetch_raw_bytes": f * 1024.0, "fetch_bytes": 2.0 * f * 1024.0, "write_bytes": w * 1024.0}
-    tot = {key: sum(v[key] for v in out.values()) for key in ("fetch_raw_bytes", "fetch_bytes", "write_bytes")}
-    tot["bytes"] = tot["fetch_bytes"] + tot["write_bytes"]
+        rb, basis = read_bytes(k, f)
+        out[k] = {"fetch_raw_bytes": f * 1024.0, "fetch_x2_bytes": 2.0 * f * 1024.0, "read_bytes": rb,
+                  "read_basis": basis, "write_bytes": w * 1024.0}
+    tot = {key: sum(v[key] for v in out.values()) for key in ("fetch_raw_bytes", "fetch_x2_bytes", "read_bytes",
+                                                               "write_bytes")}
+    tot["bytes"] = tot["read_bytes"] + tot["write_bytes"]
+    tot["bytes_blanket_x2"] = tot["fetch_x2_bytes"] + tot["write_bytes"]
     tot["per_kernel"] = out
     tot["source"] = os.path.relpath(PMC_PROFILE, ROOT)
+    tot["rule"] = ("reads: 128 B per 128-B L2 request, 64 B per other request (FETCH_SIZE tallies every request at "
+                   "64 B on gfx950; calibrated per access shape by tools/fetch_calib.hip); writes: WRITE_SIZE")
     return tot
 
 
@@ -186,8 +231,8 @@ def chain_counters(trace_dir: str, fetch_dir: str, write_dir: str):
     """Chain check + duplicate detection + tally kernels (validate_vote_chain utils.rs:175-215,
     initialize_with_votes session.rs:253-298, the tally utils.rs:227-286; k_vote_status's per-proposal
     first failing vote with them) per validate-many call, from the committed profile: each kernel's
-    memory-side bytes (FETCH_SIZE doubled per the gfx950 note of MI355X_MICROARCH.md, the raw figure
-    beside it; WRITE_SIZE) over its own duration in a kernel trace where it runs alone (HLC_SERIAL_STAGES
+    memory-side bytes (reads by read_bytes(): request counters, or FETCH_SIZE by the kernel's load shape,
+    the raw FETCH_SIZE beside it; WRITE_SIZE) over its own duration in a kernel trace where it runs alone (HLC_SERIAL_STAGES
     =1 for config 2, where k_chain_small otherwise shares the SIMDs with k_rec_main), and the achieved
     GB/s against the guide's measured 6.29 TB/s.  Per call = sum over the kernel's launches / the calls
     (k_finalize launches)."""
@@ -223,12 +268,14 @@ def chain_counters(trace_dir: str, fetch_dir: str, write_dir: str):
             out.setdefault(k, {})[ctr] = v / max(pc, 1)
     per = {}
     tot_b = tot_raw = tot_ms = 0.0
+    req_pass = fetch_dir.replace("fetch", "req")
     for k in CHAIN_KERNELS:
         f = out.get(k, {}).get("FETCH_SIZE", 0.0)
         w = out.get(k, {}).get("WRITE_SIZE", 0.0)
         ms = dur[k] / calls
-        b = 2.0 * f + w
-        per[k] = {"fetch_raw_bytes": f, "fetch_bytes": 2.0 * f, "write_bytes": w, "ms": ms,
+        rb, basis = read_bytes(k, f / 1024.0, req_pass)
+        b = rb + w
+        per[k] = {"fetch_raw_bytes": f, "read_bytes": rb, "read_basis": basis, "write_bytes": w, "ms": ms,
                   "GBps": b / max(ms * 1e-3, 1e-12) / 1e9 if ms > 0 else None}
         tot_b += b
         tot_raw += f + w

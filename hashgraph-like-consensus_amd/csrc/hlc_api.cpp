@@ -2,8 +2,12 @@
 // and the orchestration of the kernels in hlc_prehash.hip / hlc_recover.hip.
 #include <hip/hip_runtime.h>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -151,8 +155,18 @@ void stage_copy(uint8_t* dst, const uint8_t* src, size_t n) {
 // the job.
 class HostPool {
  public:
-  explicit HostPool(int workers) {
-    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+  // cpus non-empty: every worker is bound to that CPU set (the GPU's NUMA node, host_pool_cpus)
+  explicit HostPool(int workers, const std::vector<int>& cpus = {}) {
+    for (int i = 0; i < workers; ++i)
+      th_.emplace_back([this, cpus] {
+        if (!cpus.empty()) {
+          cpu_set_t set;
+          CPU_ZERO(&set);
+          for (int c : cpus) CPU_SET(c, &set);
+          (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+        }
+        loop();
+      });
   }
   ~HostPool() {
     {
@@ -239,6 +253,8 @@ struct hlc_ctx {
   std::string last_trace;                  // the last host-buffer call's HLC_HOST_TRACE JSON
   hipEvent_t ev_rest = nullptr, ev_done = nullptr;
   std::unique_ptr<HostPool> pool;  // staging workers (HLC_HOST_THREADS)
+  std::vector<int> pool_cpus;      // the CPU set its workers are bound to (host_pool_cpus)
+  int pool_bind = -1;              // the HLC_POOL_BIND setting the pool was made with
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
   DBuf in_off2, in_len2, in_off3, in_len3, in_priv, byz_key;
@@ -788,6 +804,51 @@ int host_threads() {
   return std::max(1, std::min({16, hw, (int)(share + 1e-9)}));
 }
 
+// The CPUs of the device's NUMA node that this process may run on (sysfs: the device's PCI address ->
+// numa_node -> that node's cpulist, intersected with the affinity mask), or {} when unknown or when
+// HLC_POOL_BIND=0.  The host pool's workers are bound to them: their staging copies then write the
+// page-locked buffer from the socket the GPU hangs off (the DMA reads it from there).
+std::vector<int> host_pool_cpus(int device) {
+  std::vector<int> out;
+  const char* e = std::getenv("HLC_POOL_BIND");
+  if (e && std::atoi(e) == 0) return out;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return out;
+  }
+  for (char* q = bus; *q; ++q) *q = (char)std::tolower((unsigned char)*q);
+  int node = -1;
+  {
+    std::FILE* f = std::fopen((std::string("/sys/bus/pci/devices/") + bus + "/numa_node").c_str(), "r");
+    if (!f) return out;
+    if (std::fscanf(f, "%d", &node) != 1) node = -1;
+    std::fclose(f);
+  }
+  if (node < 0) return out;
+  std::FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+  if (!f) return out;
+  char buf[4096] = {0};
+  const size_t got = std::fread(buf, 1, sizeof buf - 1, f);
+  std::fclose(f);
+  buf[got] = 0;
+  cpu_set_t aff;
+  CPU_ZERO(&aff);
+  if (sched_getaffinity(0, sizeof aff, &aff) != 0) return out;
+  for (char* q = buf; *q;) {  // "0-63,128-191"
+    char* end = nullptr;
+    const long a = std::strtol(q, &end, 10);
+    if (end == q) break;
+    long b = a;
+    q = end;
+    if (*q == '-') b = std::strtol(q + 1, &q, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET((int)c, &aff)) out.push_back((int)c);
+    while (*q == ',' || *q == '\n' || *q == ' ') ++q;
+  }
+  return out;
+}
+
 // The recovery ranges of a host-buffer call of n items (HLC_SPLIT_VOTES="a,b,...", default
 // "98304,196608"; "0" = one range): a range of each listed size while at least twice that many
 // items remain, then ranges of twice the previous size on the same rule (a large batch keeps the
@@ -859,7 +920,15 @@ int host_resources(hlc_ctx* c) {
   if (!c->wlk) HIPCHK(hipStreamCreateWithPriority(&c->wlk, hipStreamNonBlocking, greatest));
   for (hipEvent_t* e : {&c->ev_rest, &c->ev_done})
     if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  if (!c->pool || c->pool->threads() != host_threads()) c->pool.reset(new HostPool(host_threads() - 1));
+  {
+    const char* e = std::getenv("HLC_POOL_BIND");
+    const int bind = e ? (std::atoi(e) != 0) : 1;
+    if (!c->pool || c->pool->threads() != host_threads() || c->pool_bind != bind) {
+      c->pool_cpus = host_pool_cpus(c->device);  // sysfs reads: once per pool
+      c->pool.reset(new HostPool(host_threads() - 1, c->pool_cpus));
+      c->pool_bind = bind;
+    }
+  }
   CHK(ensure_recover_scratch(c));
   CHK(c->rec_scratch2.ensure(c->rec_lanes * hlc::recover_scratch_words() * sizeof(uint32_t)));
   return 0;
@@ -1186,6 +1255,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
     int mask = 0;
     for (int q = 0; q < 6; ++q) mask |= arr[q].pinned ? 1 << q : 0;
     tr.fact("pinned_mask", mask | (parr.pinned ? 64 : 0) | (arena_pinned ? 128 : 0));
+    tr.fact("pool_cpus", (double)c->pool_cpus.size());
   }
   CHK(stage_rows(st, pool, &parr, 1, 0, np));
   std::vector<int> bad(parts, 0);
@@ -1549,6 +1619,7 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
   const uint64_t chunk = wire_chunk();
   tr.fact("ranges", (double)R);
   tr.fact("wire_pinned", wire_pinned ? 1 : 0);
+  tr.fact("pool_cpus", (double)c->pool_cpus.size());
   uint64_t N = 0, base = 0;  // per-vote capacity (fixed after range 0), votes decoded so far
   size_t walked = 0, done = 0;
   bool overflow = false;

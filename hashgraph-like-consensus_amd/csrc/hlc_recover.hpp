@@ -49,10 +49,18 @@ namespace hlc {
 // the same bit positions, so a wave executes exactly one addition per window and half-scalar.
 // (A sparse wNAF is useless in SIMT: a wave runs an addition whenever ANY of its 64 lanes has a
 // non-zero digit, i.e. at nearly every position -- measured 3.0M VALU instructions per vote.)
-constexpr int W_R = 5;                          // window for R / lambda R (u2 halves)
-constexpr int M_R = 26;                         // windows: 26 * 5 = 130 >= 129 bits
+#ifndef HLC_W_R
+#define HLC_W_R 5  // A/B knob (make variant DEFS=-DHLC_W_R=6): the table doubles per extra bit
+#endif
+constexpr int W_R = HLC_W_R;                    // window for R / lambda R (u2 halves)
+constexpr int M_R = (129 + W_R - 1) / W_R;      // windows: 26 * 5 = 130 >= 129 bits
 constexpr int TOP_BIT = W_R * (M_R - 1);        // first (most significant) chain position: 125
 constexpr int RTAB_N = 1 << (W_R - 1);          // 16 odd multiples 1..31 (per lane)
+#ifndef HLC_REG_ENTRIES
+#define HLC_REG_ENTRIES 6  // the R table's last entries kept in registers through the build (A/B: profiles/r05/ab_reg_entries_window.txt)
+#endif
+constexpr int REG_E = HLC_REG_ENTRIES;
+static_assert(REG_E >= 0 && REG_E < RTAB_N, "HLC_REG_ENTRIES out of range");
 constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
 // Per-lane workspace of the main stage (persistent grid):
 //  * lane-interleaved (word w of lane t at w * lanes + t: every lane touches the same word, so
@@ -542,6 +550,7 @@ HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx,
     fe29_mul(a.y, R.y, c3);
     tab.store(0, a.x, a.y);
     uint32_t* zrws = ws + (size_t)ZR_OFF * ws_stride;
+#if HLC_REG_ENTRIES == 0
     for (int i = 1; i < RTAB_N; ++i) {
       fe29 zr;
       gej29_zaddu(a, dp, zr);
@@ -562,6 +571,56 @@ HLC_DEV int rec_u2r29(const fe& r32, const uint32_t* rec, size_t stride, fe& qx,
       fe29_mul(e.y, e.y, s3);
       tab.store(i, e.x, e.y);
     }
+#else
+    // The last REG_E entries and their z-ratios stay in registers through the build: they are written
+    // once, already in the common frame, instead of written, read back and rewritten by the rescale.
+    // (Entry i's scale is the product of the z-ratios of steps i+1 .. RTAB_N-1.)
+    constexpr int FIRST_REG = RTAB_N - REG_E;
+#pragma unroll 1
+    for (int i = 1; i < FIRST_REG; ++i) {
+      fe29 zr;
+      gej29_zaddu(a, dp, zr);
+      tab.store(i, a.x, a.y);
+      store_fe29_ws(zr, zrws + (size_t)(9 * (i - 1)) * ws_stride, ws_stride);
+    }
+    ge29 E[REG_E];
+    fe29 ZR[REG_E];
+#pragma unroll
+    for (int j = 0; j < REG_E; ++j) {
+      gej29_zaddu(a, dp, ZR[j]);
+      E[j] = a;
+    }
+    fe29 sc;
+    fe29_set(sc, 1);
+#pragma unroll
+    for (int j = REG_E - 1; j >= 0; --j) {
+      if (j != REG_E - 1) {
+        fe29 s2, s3;
+        fe29_sqr(s2, sc);
+        fe29_mul(s3, s2, sc);
+        fe29_mul(E[j].x, E[j].x, s2);
+        fe29_mul(E[j].y, E[j].y, s3);
+      }
+      tab.store(FIRST_REG + j, E[j].x, E[j].y);
+      fe29_mul(sc, sc, ZR[j]);
+    }
+#pragma unroll 1
+    for (int i = FIRST_REG - 1; i >= 0; --i) {
+      fe29 s2, s3;
+      fe29_sqr(s2, sc);
+      fe29_mul(s3, s2, sc);
+      ge29 e;
+      tab.load(e, i);
+      fe29_mul(e.x, e.x, s2);
+      fe29_mul(e.y, e.y, s3);
+      tab.store(i, e.x, e.y);
+      if (i > 0) {
+        fe29 zr;
+        load_fe29_ws(zr, zrws + (size_t)(9 * (i - 1)) * ws_stride, ws_stride);
+        fe29_mul(sc, sc, zr);
+      }
+    }
+#endif
     fe29_mul(zg, sc, d.z);
   }
   gej29 acc;

@@ -83,11 +83,10 @@ for step in "$@"; do
     mkdir -p $OUT
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 -L > $OUT/list.txt 2>&1) || true
     grep -o "TCC_[A-Z0-9_]*" $OUT/list.txt | sort -u > $OUT/tcc.txt || true
-    if grep -qx "TCC_BUBBLE" $OUT/tcc.txt && grep -qx "TCC_EA0_RDREQ" $OUT/tcc.txt; then
-      EXTRA=""
-      grep -qx "TCC_EA0_RDREQ_32B" $OUT/tcc.txt && EXTRA="TCC_EA0_RDREQ_32B"
-      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ TCC_BUBBLE $EXTRA --output-format csv \
-        -d $OUT/req -o run -- $OLDPWD/tools/fetch_calib > $OUT/req.txt 2>&1) || echo "request-size pass failed"
+    if grep -qx "TCC_EA0_RDREQ_128B" $OUT/tcc.txt && grep -qx "TCC_EA0_RDREQ" $OUT/tcc.txt; then
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc TCC_EA0_RDREQ TCC_EA0_RDREQ_128B \
+        TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_32B --output-format csv -d $OUT/req -o run -- $OLDPWD/tools/fetch_calib \
+        > $OUT/req.txt 2>&1) || echo "request-size pass failed"
     fi
     wc -l $OUT/tcc.txt ;;
   teardownprof)

@@ -39,6 +39,8 @@ def main() -> int:
                     "before the last, e.g. 131072,196608/0; 0 = one recovery range)")
     ap.add_argument("--threads", default="16", help="HLC_HOST_THREADS settings")
     ap.add_argument("--nt", default="1", help="','-separated HLC_NT_COPY settings (non-temporal staging copies)")
+    ap.add_argument("--bind", default="1", help="','-separated HLC_POOL_BIND settings (staging workers on the GPU's "
+                    "NUMA node)")
     ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
     ap.add_argument("--proposals", type=int, default=10_000)
     ap.add_argument("--pinned", action="store_true", help="the host batch in page-locked memory (hlc_host_alloc)")
@@ -66,10 +68,11 @@ def main() -> int:
     bytes_in = int(b.arena.nbytes + b.vote_id.nbytes + b.proposal_id.nbytes + b.timestamp.nbytes + b.vote.nbytes
                    + b.field_off.nbytes + b.field_len.nbytes + d.nbytes)
     ref = None
-    settings = [(sp, th, nt) for sp in a.split.split("/") for th in a.threads.split(",")
-                for nt in a.nt.split(",")] * max(1, a.rounds)
-    for sp, th, nt in settings:
+    settings = [(sp, th, nt, bd) for sp in a.split.split("/") for th in a.threads.split(",")
+                for nt in a.nt.split(",") for bd in a.bind.split(",")] * max(1, a.rounds)
+    for sp, th, nt, bd in settings:
         os.environ["HLC_NT_COPY"] = nt
+        os.environ["HLC_POOL_BIND"] = bd
         os.environ["HLC_SPLIT_VOTES"] = sp
         os.environ["HLC_HOST_THREADS"] = th
         r = eng.validate_proposals(b, d, db.now, want_votes=True)
@@ -81,7 +84,8 @@ def main() -> int:
         for _ in range(a.steps):
             eng.validate_proposals(b, d, db.now, want_votes=True)
         el = (time.perf_counter() - t) / a.steps
-        row = {"split": sp, "threads": int(th), "nt_copy": int(nt), "pinned": a.pinned, "ms_per_call": el * 1e3,
+        row = {"split": sp, "threads": int(th), "nt_copy": int(nt), "pool_bind": int(bd), "pinned": a.pinned,
+               "ms_per_call": el * 1e3,
                "votes_per_s": b.n / el, "bytes_in_per_call": bytes_in, "outputs_equal_first_setting": True}
         print(json.dumps(row), flush=True)
     if a.contexts > 1:

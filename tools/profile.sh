@@ -5,8 +5,9 @@
 #                  leg only, so the averages are config-2 launches; bench.json = that run's own line
 #  trace_serial/   the same with HLC_SERIAL_STAGES=1 (every kernel alone on one stream): isolated
 #                  durations of the chain / tally kernels
-#  pmc_*/          one counter pass per run (counter-block limits: 8 SQ, 4 TCC (FETCH_SIZE uses 3), 2 GRBM)
-#  c3_trace/, c3_fetch/, c3_write/   config 3 (tools/config3_time.py: 1 proposal, 1M chained votes)
+#  pmc_*/          one counter pass per run (counter-block limits: 8 SQ, 4 TCC (FETCH_SIZE uses 3), 2 GRBM);
+#                  pmc_req: the L2 read requests by size (TCC_EA0_RDREQ, _128B, _32B) for exact read bytes
+#  c3_trace/, c3_fetch/, c3_write/, c3_req/   config 3 (tools/config3_time.py: 1 proposal, 1M chained votes)
 set -o pipefail
 TAG=${1:-r04}
 OUT=$PWD/gpurun_out/prof_$TAG
@@ -25,9 +26,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 HLC_SERIAL_STAGES=1 run trace_serial 300 --kernel-trace --stats --output-format csv -d $OUT/trace_serial -o run -- python3 $PBENCH
 run pmc_fetch 300 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $PBENCH
 run pmc_write 300 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $PBENCH
+# the L2's read requests by size (bench.py read_bytes: FETCH_SIZE tallies 128-B requests at 64 B on gfx950)
+run pmc_req 300 --kernel-trace --pmc TCC_EA0_RDREQ TCC_EA0_RDREQ_128B TCC_EA0_RDREQ_32B --output-format csv -d $OUT/pmc_req -o run -- python3 $PBENCH
 run pmc_valu 300 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/pmc_valu -o run -- python3 $PBENCH
 run pmc_stall 300 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM SQ_INSTS_VMEM --output-format csv -d $OUT/pmc_stall -o run -- python3 $PBENCH
 run c3_trace 300 --kernel-trace --stats --output-format csv -d $OUT/c3_trace -o run -- python3 $C3
 run c3_fetch 300 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/c3_fetch -o run -- python3 $C3
 run c3_write 300 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/c3_write -o run -- python3 $C3
+run c3_req 300 --kernel-trace --pmc TCC_EA0_RDREQ TCC_EA0_RDREQ_128B TCC_EA0_RDREQ_32B --output-format csv -d $OUT/c3_req -o run -- python3 $C3
 find $OUT -name "*.csv" | head -60

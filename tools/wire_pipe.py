@@ -28,6 +28,8 @@ def main() -> int:
     ap.add_argument("--chunk", default="8388608", help="','-separated HLC_WIRE_CHUNK settings")
     ap.add_argument("--threads", default="16", help="','-separated HLC_HOST_THREADS settings")
     ap.add_argument("--nt", default="1", help="','-separated HLC_NT_COPY settings (non-temporal staging copies)")
+    ap.add_argument("--bind", default="1", help="','-separated HLC_POOL_BIND settings (staging workers on the GPU's "
+                    "NUMA node)")
     ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
     ap.add_argument("--proposals", type=int, default=10_000)
     ap.add_argument("--pinned", action="store_true", help="the wire bytes in page-locked memory (hlc_host_alloc)")
@@ -55,10 +57,11 @@ def main() -> int:
         pw = arena.take(wire.shape, np.uint8)
         pw[:] = wire
         wire = pw
-    settings = [(sp, ch, th, nt) for sp in a.split.split("/") for ch in a.chunk.split(",")
-                for th in a.threads.split(",") for nt in a.nt.split(",")] * max(1, a.rounds)
-    for sp, ch, th, nt in settings:
+    settings = [(sp, ch, th, nt, bd) for sp in a.split.split("/") for ch in a.chunk.split(",")
+                for th in a.threads.split(",") for nt in a.nt.split(",") for bd in a.bind.split(",")] * max(1, a.rounds)
+    for sp, ch, th, nt, bd in settings:
         os.environ["HLC_NT_COPY"] = nt
+        os.environ["HLC_POOL_BIND"] = bd
         os.environ["HLC_WIRE_PIPELINE"] = "0" if sp == "plain" else "1"
         if sp != "plain":
             os.environ["HLC_WIRE_SPLIT_BYTES"] = sp
@@ -70,7 +73,8 @@ def main() -> int:
         for _ in range(a.steps):
             eng.validate_wire_proposals(wire, off, lens, scope, db.now)
         el = (time.perf_counter() - t) / a.steps
-        row = {"split": sp, "chunk": int(ch), "threads": int(th), "nt_copy": int(nt), "pinned": a.pinned,
+        row = {"split": sp, "chunk": int(ch), "threads": int(th), "nt_copy": int(nt), "pool_bind": int(bd),
+               "pinned": a.pinned,
                "ms_per_call": el * 1e3,
                "votes_per_s": db.n / el, "wire_bytes": int(wire.size), "outputs_equal_device_soa_path": True}
         if a.trace and sp != "plain":
