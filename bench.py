@@ -76,50 +76,37 @@ def pmc_duration_ms(name: str, kernel: str):
     return sum(durs) / len(durs) if durs else None
 
 
-# Memory-side read bytes from the L2's request counters.  gfx950's FETCH_SIZE is
-# (TCC_BUBBLE*128 + (TCC_EA0_RDREQ - TCC_BUBBLE - TCC_EA0_RDREQ_32B)*64 + TCC_EA0_RDREQ_32B*32) / 1024 KiB,
-# and TCC_BUBBLE reads 0 on this box, so every request is tallied at 64 B.  Calibrated with
-# tools/fetch_calib.hip (profiles/r05/fetch_calibration.json, fetch_calib_requests.csv): coalesced streams
-# of 16-, 4- and 1-byte loads per lane issue 128-B requests (FETCH_SIZE = exactly 1/2 of their bytes);
-# a lane's own 64-B entry (4 x 16-B loads) is one 64-B request (FETCH_SIZE = its bytes); 32-B and 16-B
-# pieces at scattered addresses cost a whole 64-B request each (FETCH_SIZE = 2x / 4x the useful bytes --
-# real traffic, the granule the fabric moves).  So the memory-side read bytes of a kernel are
-#   128 x TCC_EA0_RDREQ_128B + 64 x (TCC_EA0_RDREQ - _128B - _32B) + 32 x _32B
-# when the committed profile has that pass (pmc_req); otherwise FETCH_SIZE x the factor of the kernel's
-# dominant load shape below, with FETCH_SIZE itself (`fetch_raw_bytes`) beside it.
-FETCH_SHAPE = {
-    "k_rec_prep": (2.0, "coalesced: the signatures (65-B records of consecutive votes), the skip-list fields"),
-    "k_rec_main": (1.0, "per-lane gathers of 64-B R-table entries dominate (52 per vote, 3.3 KB)"),
-    "k_rec_comb": (1.0, "per-lane gathers of 64-B comb entries dominate (12 per vote, 768 B; records and Q are "
-                        "~270 B/vote of coalesced loads, under-counted by half)"),
-    "k_rec_final": (2.0, "coalesced word-major Q / prefix products"),
-    "k_rec_addr": (2.0, "coalesced word-major Q (64 B/vote); the 20-B owner reads are scattered"),
-    "k_chain_small": (1.0, "per-lane reads of owner / hash fields at scattered arena offsets"),
-    "k_clear_if": (2.0, "streaming"),
-    "k_tables": (1.0, "scattered key reads and table probes"),
-    "k_chain_check": (1.0, "scattered key reads and table probes"),
-    "k_vote_status": (2.0, "coalesced per-vote bytes"),
-    "k_finalize": (2.0, "coalesced per-proposal records"),
-}
+# Memory-side read bytes from the L2's request counters (round 4 doubled FETCH_SIZE for
+# every kernel on the strength of the guide's note about 16-B-per-lane streams).  gfx950's FETCH_SIZE is
+# (TCC_BUBBLE*128 + (TCC_EA0_RDREQ - TCC_BUBBLE - TCC_EA0_RDREQ_32B)*64 + TCC_EA0_RDREQ_32B*32) / 1024 KiB, and
+# TCC_BUBBLE reads 0 on this box, so every request is tallied at 64 B.  Calibrated with tools/fetch_calib.hip
+# (profiles/r05/fetch_calibration.json, fetch_calib_requests_by_size.csv: 2 GiB touched once per shape):
+# every read request of every shape measured -- coalesced streams of 16-, 4- and 1-byte loads per lane, a
+# lane's own 64-B entry at a scattered address (4 x 16-B loads), 32-B and 16-B pieces at scattered addresses --
+# is a 128-B request (TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ; _64B and _32B ~0).  So the memory moves 128 B per
+# request and FETCH_SIZE is exactly half of the memory-side read bytes for all of them; what differs by shape
+# is the useful fraction: 1 for streams, 1/2 for 64-B gathers (the other half of the 128-B line comes along),
+# 1/4 and 1/8 for 32- and 16-B pieces.  Read bytes per launch:
+#   128 x TCC_EA0_RDREQ_128B + 64 x TCC_EA0_RDREQ_64B + 32 x TCC_EA0_RDREQ_32B   (pmc_req, when committed),
+#   else 2 x FETCH_SIZE (the same for every shape calibrated), with FETCH_SIZE itself beside it.
 REQ_COUNTERS = ("TCC_EA0_RDREQ", "TCC_EA0_RDREQ_128B", "TCC_EA0_RDREQ_32B")
 
 
 def read_bytes(kernel: str, fetch_kib, req_pass: str = "pmc_req"):
     """(memory-side read bytes per launch, basis) for `kernel`: from the request-size pass when the
-    committed profile has it, else FETCH_SIZE x the kernel's shape factor (FETCH_SHAPE)."""
+    committed profile has it, else 2 x FETCH_SIZE (see the calibration note above)."""
     req = {c: pmc_per_launch(req_pass, c, kernel) for c in REQ_COUNTERS}
     if all(v is not None for v in req.values()):
         rd, r128, r32 = (req[c] for c in REQ_COUNTERS)
         return 128.0 * r128 + 64.0 * (rd - r128 - r32) + 32.0 * r32, "request counters (pmc_req)"
-    f, why = FETCH_SHAPE.get(kernel, (1.0, "unclassified: FETCH_SIZE as counted"))
-    return f * fetch_kib * 1024.0, f"FETCH_SIZE x {f:g} ({why})"
+    return 2.0 * fetch_kib * 1024.0, "2 x FETCH_SIZE (every calibrated read request is 128 B, tallied at 64 B)"
 
 
 def pmc_traffic():
     """Per-launch memory-side bytes of the recovery kernels from the committed profile: reads by
-    read_bytes() (request counters, or FETCH_SIZE by the kernel's load shape), writes from WRITE_SIZE
-    (exact for every shape calibrated, profiles/r05/fetch_calibration.json).  `fetch_raw_bytes` is
-    FETCH_SIZE as counted; `fetch_x2_bytes` the round-4 blanket doubling, for comparison."""
+    read_bytes() (the L2's read requests by size, or 2 x FETCH_SIZE), writes from WRITE_SIZE (exact for
+    every shape calibrated, profiles/r05/fetch_calibration.json).  `fetch_raw_bytes` is FETCH_SIZE as
+    counted; `fetch_x2_bytes` the round-4 blanket doubling, for comparison."""
     out = {}
     for k in REC_KERNELS:
         f = pmc_per_launch("pmc_fetch", "FETCH_SIZE", k)
@@ -135,8 +122,9 @@ def pmc_traffic():
     tot["bytes_blanket_x2"] = tot["fetch_x2_bytes"] + tot["write_bytes"]
     tot["per_kernel"] = out
     tot["source"] = os.path.relpath(PMC_PROFILE, ROOT)
-    tot["rule"] = ("reads: 128 B per 128-B L2 request, 64 B per other request (FETCH_SIZE tallies every request at "
-                   "64 B on gfx950; calibrated per access shape by tools/fetch_calib.hip); writes: WRITE_SIZE")
+    tot["rule"] = ("reads: the L2's memory read requests by size (128 / 64 / 32 B; on gfx950 FETCH_SIZE tallies every "
+                   "request at 64 B while every calibrated shape issues 128-B requests, tools/fetch_calib.hip); "
+                   "writes: WRITE_SIZE")
     return tot
 
 
@@ -231,8 +219,8 @@ def chain_counters(trace_dir: str, fetch_dir: str, write_dir: str):
     """Chain check + duplicate detection + tally kernels (validate_vote_chain utils.rs:175-215,
     initialize_with_votes session.rs:253-298, the tally utils.rs:227-286; k_vote_status's per-proposal
     first failing vote with them) per validate-many call, from the committed profile: each kernel's
-    memory-side bytes (reads by read_bytes(): request counters, or FETCH_SIZE by the kernel's load shape,
-    the raw FETCH_SIZE beside it; WRITE_SIZE) over its own duration in a kernel trace where it runs alone (HLC_SERIAL_STAGES
+    memory-side bytes (reads by read_bytes(): the L2's read requests by size, or 2 x FETCH_SIZE, the raw
+    FETCH_SIZE beside it; WRITE_SIZE) over its own duration in a kernel trace where it runs alone (HLC_SERIAL_STAGES
     =1 for config 2, where k_chain_small otherwise shares the SIMDs with k_rec_main), and the achieved
     GB/s against the guide's measured 6.29 TB/s.  Per call = sum over the kernel's launches / the calls
     (k_finalize launches)."""
