@@ -18,6 +18,11 @@ def test_committed_profile_figures():
     assert t["bytes"] > 0 and t["per_kernel"]["k_rec_main"]["write_bytes"] > 0
     # per 640k-vote launch: the recovery kernels move a few GB, not MB and not tens of GB
     assert 1e9 < t["bytes"] < 3e10
+    # reads from the L2's request counters by size (the committed profile has the pass): every request of
+    # the recovery kernels is a 128-B one, twice what FETCH_SIZE tallies (profiles/r05/FETCH_CALIBRATION.md)
+    for k, v in t["per_kernel"].items():
+        assert v["read_basis"] == "request counters (pmc_req)", k
+        assert 1.9 < v["read_bytes"] / v["fetch_raw_bytes"] < 2.1, k
     v = bench.valu_figures()
     assert 0.2 < v["valu_lane_op_frac"] < 0.6
     assert 2e5 < v["valu_instr_per_vote"]["k_rec_main"] < 4e5
