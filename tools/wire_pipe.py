@@ -25,7 +25,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--split", default="16777216,33554432/plain",
                     help="'/'-separated HLC_WIRE_SPLIT_BYTES settings ('plain' = the unpipelined arm)")
-    ap.add_argument("--chunk", default="8388608", help="','-separated HLC_WIRE_CHUNK settings")
+    ap.add_argument("--chunk", default="4194304", help="','-separated HLC_WIRE_CHUNK settings (the library default: 4 MiB)")
     ap.add_argument("--threads", default="16", help="','-separated HLC_HOST_THREADS settings")
     ap.add_argument("--nt", default="1", help="','-separated HLC_NT_COPY settings (non-temporal staging copies)")
     ap.add_argument("--bind", default="1", help="','-separated HLC_POOL_BIND settings (staging workers on the GPU's "
