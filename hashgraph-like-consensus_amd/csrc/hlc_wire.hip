@@ -238,18 +238,37 @@ constexpr int HUGE_RESUME_PASSES = 4;     // parallel re-marking passes past lon
 constexpr uint64_t HUGE_GROUP_SCAN = 256;
 __host__ __device__ __forceinline__ bool is_huge(uint32_t len) { return len > HUGE_MSG && len < HUGE_MAX; }
 
-// Loads wire[wlo, whi) (wlo 16-byte aligned) into LDS with the calling block's threads.
+// Loads wire[wlo, whi) (wlo 16-byte aligned) into LDS with the calling block's threads.  Each thread
+// issues LW_BATCH 16-byte loads before its first LDS write, so a window costs one or two memory round
+// trips instead of one per granule (a load followed by its LDS write in one loop iteration waits for
+// the load every time: 12 serial misses for a 12 KB message window on a 64-lane block).
+#ifndef HLC_WIN_BATCH
+#define HLC_WIN_BATCH 12  // A/B knob: 1 = one granule per round trip (the round-5 loader's behaviour)
+#endif
+constexpr int LW_BATCH = HLC_WIN_BATCH;
 __device__ __forceinline__ void load_window(uint8_t* lds, const uint8_t* __restrict__ wire, uint64_t wlo,
                                             uint64_t whi, bool aligned) {
   const uint64_t n = whi - wlo;
-  for (uint64_t c = threadIdx.x; c * 16 < n; c += blockDim.x) {
-    const uint64_t a = wlo + c * 16;
-    if (aligned && a + 16 <= whi) {
-      *reinterpret_cast<uint4*>(lds + c * 16) = *reinterpret_cast<const uint4*>(wire + a);
-    } else {
-      for (uint64_t k = a; k < whi && k < a + 16; ++k) lds[k - wlo] = wire[k];
+  const uint64_t full = aligned ? n / 16 : 0;  // granules loaded whole
+  const uint64_t step = blockDim.x;
+  const uint8_t* src = wire + wlo;  // uniform base, 32-bit per-lane offsets (windows are < 4 GB)
+  for (uint64_t c0 = threadIdx.x; c0 < full; c0 += step * LW_BATCH) {
+    uint4 r[LW_BATCH];
+    // unpredicated loads (a granule past the window reloads the window's last one)
+#pragma unroll
+    for (int j = 0; j < LW_BATCH; ++j) {
+      const uint32_t c = (uint32_t)std::min<uint64_t>(c0 + j * step, full - 1);
+      r[j] = *reinterpret_cast<const uint4*>(src + c * 16u);
+    }
+    // (unpredicated stores too: a clamped granule is written again with the same bytes.  A store under
+    // a branch lets the compiler sink its load into the branch, one wait per load again.)
+#pragma unroll
+    for (int j = 0; j < LW_BATCH; ++j) {
+      const uint64_t c = std::min<uint64_t>(c0 + j * step, full - 1);
+      *reinterpret_cast<uint4*>(lds + c * 16) = r[j];
     }
   }
+  for (uint64_t k = full * 16 + threadIdx.x; k < n; k += step) lds[k] = wire[wlo + k];  // the ragged tail
 }
 
 // One field of the Proposal at `pos` (prost Proposal::merge_field, consensus.proto:5-16).

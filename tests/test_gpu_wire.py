@@ -95,6 +95,28 @@ def test_gpu_decode_fuzzed_messages(engine):
             wo.DELIMITED_EXCEEDED, wo.RECURSION_LIMIT} <= codes
 
 
+@pytest.mark.parametrize("walker", ["lane", "lds"])
+def test_gpu_decode_fuzzed_messages_both_walkers(engine, monkeypatch, walker):
+    """Both top-level walkers (HLC_WIRE_WALK: k_wire_walk, one lane per message; k_wire_walk_lds, message
+    windows staged in LDS) against the prost restatement: fuzzed messages, messages longer than the LDS
+    window (12 KB: the walker reads past it from global memory) and messages at odd byte offsets."""
+    from wire_fuzz import random_vote
+    from hashgraph_like_consensus.protos import Proposal
+    monkeypatch.setenv("HLC_WIRE_WALK", walker)
+    rnd = random.Random(24)
+    msgs = []
+    for t in range(600):
+        msg = encode_proposal(random_proposal(rnd, max_votes=5))
+        msgs.append(msg if t % 3 == 0 else mutate(rnd, msg))
+    for t in range(6):  # 70-110 vote records: past the 12 KB window, some mutated near their end
+        big = encode_proposal(Proposal(name="w", proposal_id=70 + t, expected_voters_count=200,
+                                       votes=[random_vote(rnd) for _ in range(70 + 8 * t)]))
+        msgs.append(big if t % 2 == 0 else big[:-3] + bytes([rnd.randrange(256)]) + big[-2:])
+    msgs.insert(7, b"\x01")  # every later message starts at an odd offset
+    codes = _check_decode(engine, msgs, _scope(1))
+    assert {wo.OK, wo.INVALID_VARINT, wo.BUFFER_UNDERFLOW, wo.WIRE_TYPE_MISMATCH} <= codes
+
+
 def test_gpu_decode_per_message_scope_and_overlap(engine):
     rnd = random.Random(22)
     msgs = [encode_proposal(random_proposal(rnd, max_votes=3)) for _ in range(40)]

@@ -9,6 +9,7 @@
 #   legs                bench.py headline + config-5 legs, 20 steps
 #   host                tools/host_pipe.py (host-buffer entry, default schedule, 8 host threads), 20 calls
 #   wire                tools/wire_pipe.py (the wire entry from host buffers, default schedule), 20 calls
+#                       (AB_WIRE_ARGS="--device-walk lane" adds the device-resident wire entry)
 #                       (host_pipe.py sets HLC_SPLIT_VOTES / HLC_HOST_THREADS itself: vary those with its flags)
 set -o pipefail
 mkdir -p gpurun_out
@@ -32,8 +33,11 @@ for round in 1 2 3; do
       env $ENVS timeout -k 10 200 python tools/host_pipe.py --threads 8 --steps 20 > $O.txt 2> $O.err || { tail $O.err; exit 1; }
       python -c "import json;d=json.loads(open('$O.txt').read().splitlines()[-1]);print('$round $v host', round(d['votes_per_s']), 'votes/s', round(d['ms_per_call'],3), 'ms')" ;;
     wire)
-      env $ENVS timeout -k 10 200 python tools/wire_pipe.py --split 8388608,16777216,25165824,33554432 --steps 20 > $O.txt 2> $O.err || { tail $O.err; exit 1; }
-      python -c "import json;d=json.loads(open('$O.txt').read().splitlines()[-1]);print('$round $v wire', round(d['votes_per_s']), 'votes/s', round(d['ms_per_call'],3), 'ms')" ;;
+      env $ENVS timeout -k 10 200 python tools/wire_pipe.py --steps 20 $AB_WIRE_ARGS > $O.txt 2> $O.err || { tail $O.err; exit 1; }
+      python -c "
+import json
+for l in open('$O.txt'):
+    d=json.loads(l); print('$round $v wire', d.get('device_resident_walk', 'from-host'), round(d['votes_per_s']), 'votes/s', round(d['ms_per_call'],3), 'ms')" ;;
     *)
       echo "unknown AB_MODE $MODE"; exit 2 ;;
     esac

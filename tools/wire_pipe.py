@@ -5,7 +5,7 @@ For each setting of the pipelined schedule (hlc_api.cpp validate_wire_host: HLC_
 HLC_WIRE_CHUNK, HLC_HOST_THREADS, read on every call; "plain" = HLC_WIRE_PIPELINE=0, the unpipelined
 arm): outputs equal the device-resident SoA path's bit for bit, then --steps calls are timed.
 
-    python tools/wire_pipe.py --steps 10 --split 16777216,33554432/8388608,16777216/plain --chunk 8388608
+    python tools/wire_pipe.py --steps 10 --split default/16777216,33554432/plain --chunk 4194304,8388608
     (HLC_HOST_TRACE=1 adds each call's timeline on stderr; --trace prints one traced call per setting)
 """
 from __future__ import annotations
@@ -23,13 +23,16 @@ sys.path.insert(0, os.path.join(ROOT, "hashgraph-like-consensus_amd", "python"))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--split", default="16777216,33554432/plain",
-                    help="'/'-separated HLC_WIRE_SPLIT_BYTES settings ('plain' = the unpipelined arm)")
+    ap.add_argument("--split", default="default",
+                    help="'/'-separated HLC_WIRE_SPLIT_BYTES settings ('plain' = the unpipelined arm, 'default' = "
+                    "the library's schedule)")
     ap.add_argument("--chunk", default="4194304", help="','-separated HLC_WIRE_CHUNK settings (the library default: 4 MiB)")
     ap.add_argument("--threads", default="16", help="','-separated HLC_HOST_THREADS settings")
     ap.add_argument("--nt", default="1", help="','-separated HLC_NT_COPY settings (non-temporal staging copies)")
     ap.add_argument("--bind", default="1", help="','-separated HLC_POOL_BIND settings (staging workers on the GPU's "
                     "NUMA node)")
+    ap.add_argument("--walk", default="", help="','-separated HLC_WIRE_WALK settings for the pipelined entry "
+                    "(lane / lds; empty = the library default)")
     ap.add_argument("--rounds", type=int, default=1, help="alternate the whole sweep this many times (box drift)")
     ap.add_argument("--proposals", type=int, default=10_000)
     ap.add_argument("--pinned", action="store_true", help="the wire bytes in page-locked memory (hlc_host_alloc)")
@@ -57,13 +60,20 @@ def main() -> int:
         pw = arena.take(wire.shape, np.uint8)
         pw[:] = wire
         wire = pw
-    settings = [(sp, ch, th, nt, bd) for sp in a.split.split("/") for ch in a.chunk.split(",")
-                for th in a.threads.split(",") for nt in a.nt.split(",") for bd in a.bind.split(",")] * max(1, a.rounds)
-    for sp, ch, th, nt, bd in settings:
+    settings = [(sp, ch, th, nt, bd, wk) for sp in a.split.split("/") for ch in a.chunk.split(",")
+                for th in a.threads.split(",") for nt in a.nt.split(",") for bd in a.bind.split(",")
+                for wk in a.walk.split(",")] * max(1, a.rounds)
+    for sp, ch, th, nt, bd, wk in settings:
+        if wk:
+            os.environ["HLC_WIRE_WALK"] = wk
+        else:
+            os.environ.pop("HLC_WIRE_WALK", None)
         os.environ["HLC_NT_COPY"] = nt
         os.environ["HLC_POOL_BIND"] = bd
         os.environ["HLC_WIRE_PIPELINE"] = "0" if sp == "plain" else "1"
-        if sp != "plain":
+        if sp == "default":
+            os.environ.pop("HLC_WIRE_SPLIT_BYTES", None)
+        elif sp != "plain":
             os.environ["HLC_WIRE_SPLIT_BYTES"] = sp
         os.environ["HLC_WIRE_CHUNK"] = ch
         os.environ["HLC_HOST_THREADS"] = th
@@ -74,7 +84,7 @@ def main() -> int:
             eng.validate_wire_proposals(wire, off, lens, scope, db.now)
         el = (time.perf_counter() - t) / a.steps
         row = {"split": sp, "chunk": int(ch), "threads": int(th), "nt_copy": int(nt), "pool_bind": int(bd),
-               "pinned": a.pinned,
+               "walk": wk or "default", "pinned": a.pinned,
                "ms_per_call": el * 1e3,
                "votes_per_s": db.n / el, "wire_bytes": int(wire.size), "outputs_equal_device_soa_path": True}
         if a.trace and sp != "plain":
