@@ -131,6 +131,35 @@ def pmc_traffic():
 VALU_PEAK_LANE_OPS = ROOFLINE["peak"]["valu_lane_ops_T_per_s"]
 
 
+def measure_live_clock(eng, step, torch):
+    """The shader clock k_rec_main ran at on THIS box, right after the timed steps (the chip still in the
+    state they left it in): three more steps with the library's per-wave clock stamps on
+    (hlc_ctx_set_clock_probe; the timed steps ran without them), each call's median over its waves.
+    Box-to-box differences in the headline follow this clock (MI355X_MICROARCH.md, DVFS give-back item 5);
+    single calls can read well apart (2.26 then 1.94 GHz on one box), so all three are kept."""
+    try:
+        eng.set_clock_probe(True)
+        calls = []
+        for _ in range(3):
+            step()
+            torch.cuda.synchronize()
+            calls.append(eng.clock_probe())
+        meds = sorted(c["median_GHz"] for c in calls)
+        return {"median_GHz": meds[1], "per_call_median_GHz": [c["median_GHz"] for c in calls],
+                "min_GHz": min(c["min_GHz"] for c in calls), "max_GHz": max(c["max_GHz"] for c in calls),
+                "waves_per_call": calls[-1]["waves"],
+                "basis": "per-wave s_memtime / s_memrealtime over each k_rec_main wave's life; per call the "
+                         "median over its waves; median_GHz = the middle of three calls right after the "
+                         "timed steps"}
+    except Exception as e:  # noqa: BLE001 -- a diagnostic, never the headline
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        try:
+            eng.set_clock_probe(False)
+        except Exception:  # noqa: BLE001
+            pass
+
+
 def valu_figures():
     """Hardware VALU figures of the recovery from the committed profile of this bench command
     (one build, one box): per kernel SQ_INSTS_VALU (PMC pass) x 64 lanes / its kernel-trace
@@ -984,6 +1013,7 @@ def main() -> int:
     rec_ms, rec_n, call_ms, calls = eng.take_kernel_time()
     chain_ms, chain_n = eng.take_chain_time()
     eng.set_kernel_timing(False)
+    live_clock = measure_live_clock(eng, step, torch)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1097,6 +1127,7 @@ def main() -> int:
             "pmc_pass_sclk_GHz": valu["pmc_pass_sclk_GHz"] if valu else None,
             "in_kernel_sclk_GHz": valu["in_kernel_sclk_GHz"] if valu else None,
             "clock_ceiling_GHz": valu["clock_ceiling_GHz"] if valu else None,
+            "live_k_rec_main_clock": live_clock,
             "clock_source": valu["clock_source"] if valu else None,
             "kernel_ms_avg": rec_avg_s * 1e3,
             "kernel_launches": rec_n,

@@ -263,6 +263,9 @@ struct hlc_ctx {
   // internal workspace
   // measurement hooks
   bool timing = false;
+  bool clock_probe = false;  // hlc_ctx_set_clock_probe: k_rec_main's per-wave clock stamps into clk_buf
+  DBuf clk_buf;
+  uint64_t clk_waves = 0;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> rec_ev, rec_prep_ev, call_ev, chain_ev, chain_aux_ev;
   hipEvent_t take_event() {
@@ -478,8 +481,15 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     c->rec_prep_ev.emplace_back(p0, p1);
   }
   if (c->timing) HIPCHK(hipEventRecord(r0, aux));
+  unsigned long long* clk = nullptr;
+  if (c->clock_probe) {
+    CHK(c->clk_buf.ensure((c->rec_lanes / 64) * 32 + 32));
+    HIPCHK(hipMemsetAsync(c->clk_buf.p, 0, (c->rec_lanes / 64) * 32, aux));
+    clk = c->clk_buf.as<unsigned long long>();
+  }
   hlc::launch_recover_main(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, c->rec_scratch.as<uint32_t>(),
-                           c->rec_lanes, c->rec_work.as<uint32_t>(), aux, c->rec_force_exact);
+                           c->rec_lanes, c->rec_work.as<uint32_t>(), aux, c->rec_force_exact, nullptr, clk,
+                           clk ? &c->clk_waves : nullptr);
   if (!c->serial_stages) {
     HIPCHK(hipEventRecord(c->ev_join, aux));
     CHK(prehash_and_chain());
@@ -1898,6 +1908,37 @@ int hlc_ctx_set_kernel_timing(hlc_ctx* ctx, int enable) {
   if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->timing = enable != 0;
+  return 0;
+}
+
+int hlc_ctx_set_clock_probe(hlc_ctx* ctx, int enable) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->clock_probe = enable != 0;
+  ctx->clk_waves = 0;
+  return 0;
+}
+
+int hlc_ctx_clock_probe(hlc_ctx* ctx, double* median_ghz, double* min_ghz, double* max_ghz, uint64_t* waves) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  std::vector<double> ghz;
+  if (ctx->clk_waves && ctx->clk_buf.p) {
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(4 * ctx->clk_waves);
+    HIPCHK(hipMemcpy(h.data(), ctx->clk_buf.p, h.size() * 8, hipMemcpyDeviceToHost));
+    for (uint64_t w = 0; w < ctx->clk_waves; ++w) {  // (start core, start ref, end core, end ref) per wave
+      const unsigned long long* t = &h[4 * w];
+      if (t[2] > t[0] && t[3] > t[1]) ghz.push_back(0.1 * (double)(t[2] - t[0]) / (double)(t[3] - t[1]));
+    }
+  }
+  if (ghz.empty()) return set_err(HLC_EINVAL, "no k_rec_main launch stamped since hlc_ctx_set_clock_probe(ctx, 1)");
+  std::sort(ghz.begin(), ghz.end());
+  if (median_ghz) *median_ghz = ghz[ghz.size() / 2];
+  if (min_ghz) *min_ghz = ghz.front();
+  if (max_ghz) *max_ghz = ghz.back();
+  if (waves) *waves = ghz.size();
   return 0;
 }
 

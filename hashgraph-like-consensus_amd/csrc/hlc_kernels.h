@@ -91,7 +91,8 @@ void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
                          const RecSkip* skip = nullptr, const RecRange* range = nullptr);
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact = 0,
-                         const RecRange* range = nullptr);
+                         const RecRange* range = nullptr, unsigned long long* clk = nullptr,
+                         uint64_t* clk_waves = nullptr);
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gtab, uint32_t* work,
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0,

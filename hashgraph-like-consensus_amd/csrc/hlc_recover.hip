@@ -151,26 +151,29 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t st, 
 // Work is handed out dynamically, 64 listed votes per wave per grab (one atomic by lane 0).
 // The SIMD's arbiter favours its oldest wave, so with a static vote-per-lane stride the oldest of
 // the 3 resident waves finishes its share long before the youngest, which then runs alone at
-// lone-wave efficiency (measured with HLC_CLOCK_PROBE: 4-vote blocks done at 3.5 ms, the last
+// lone-wave efficiency (measured with per-wave clock stamps: 4-vote blocks done at 3.5 ms, the last
 // 3-vote blocks at 7.0 ms of one launch); grabbing keeps every wave busy until the work runs out.
+// clk != nullptr (hlc_ctx_set_clock_probe; never on a timed call): each wave stamps its core-clock ticks
+// (s_memtime) and constant 100 MHz ticks (s_memrealtime) at its start and end into clk[4w .. 4w + 3] --
+// the shader clock the chain ran at (MI355X_MICROARCH.md, DVFS give-back item 6).  The start stamps go
+// to memory at once, so nothing but the pointer stays live across the loop.
 __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_t st, const uint8_t* bytes,
                                                                      const uint64_t* sig_off, size_t off_stride,
                                                                      uint32_t* scratch, uint64_t lanes,
                                                                      const uint32_t* rec, uint32_t* q, uint8_t* mst,
                                                                      int force_exact, unsigned long long* ctr,
                                                                      const uint32_t* list,
-                                                                     const unsigned long long* list_len) {
+                                                                     const unsigned long long* list_len,
+                                                                     unsigned long long* clk) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t* ws = scratch + tid;
   rtab29 tab;
   tab.g = scratch + (size_t)IL_WORDS * lanes + (size_t)tid * RTAB_WORDS;
-#ifdef HLC_CLOCK_PROBE
-  // A/B probe (make variant NAME=clk DEFS=-DHLC_CLOCK_PROBE): the shader clock a wave sees under
-  // the real kernel = core-clock ticks (clock64) over constant 100 MHz ticks (wall_clock64)
-  const uint64_t clk0 = clock64(), wall0 = wall_clock64();
-  uint32_t done = 0;
-#endif
   const unsigned lane = threadIdx.x & 63u;
+  if (clk && lane == 0) {  // (vector stores from one lane)
+    clk[4 * (tid >> 6)] = __builtin_amdgcn_s_memtime();
+    clk[4 * (tid >> 6) + 1] = __builtin_amdgcn_s_memrealtime();
+  }
   const unsigned long long nl = *list_len;  // votes k_rec_prep listed
   for (;;) {
     unsigned long long base = 0;
@@ -179,9 +182,6 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
     if (base >= nl) break;
     if (base + lane >= nl) continue;  // the next grab is past the list's end: the wave leaves together
     const uint64_t i = list[base + lane];
-#ifdef HLC_CLOCK_PROBE
-    ++done;
-#endif
     fe r, qx, qy, qz;
     bool inf = false;
     fe_load_be(r, sig_at(bytes, sig_off, off_stride, i));
@@ -195,13 +195,10 @@ __global__ void __launch_bounds__(REC_TPB, HLC_REC_MIN_WAVES) k_rec_main(uint64_
     store_fe_ws(qy, q + (size_t)8 * st + i, st);
     store_fe_ws(qz, q + (size_t)16 * st + i, st);
   }
-#ifdef HLC_CLOCK_PROBE
-  if (threadIdx.x == 0 && blockIdx.x % 61 == 0) {
-    const uint64_t dc = clock64() - clk0, dw = wall_clock64() - wall0;
-    printf("HLC_CLOCK block %u votes %u clk %llu wall %llu GHz %.3f\n", blockIdx.x, done, (unsigned long long)dc,
-           (unsigned long long)dw, dw ? (double)dc / ((double)dw * 10.0) : 0.0);
+  if (clk && lane == 0) {
+    clk[4 * (tid >> 6) + 2] = __builtin_amdgcn_s_memtime();
+    clk[4 * (tid >> 6) + 3] = __builtin_amdgcn_s_memrealtime();
   }
-#endif
 }
 
 #ifndef HLC_COMB_MIN_WAVES
@@ -486,16 +483,17 @@ void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
 
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact,
-                         const RecRange* range) {
+                         const RecRange* range, unsigned long long* clk, uint64_t* clk_waves) {
   const uint64_t m = range ? range->m : n;
   if (!m) return;
   const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr, range);
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (m + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
+  if (clk_waves) *clk_waves = blocks * (REC_TPB / 64);
   hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, f.st, bytes, sig_off, off_stride,
                      scratch, (uint64_t)blocks * REC_TPB, f.b.rec, f.b.q, f.b.mst, force_exact, f.b.ctr, f.b.list,
-                     f.b.ctr + 1);
+                     f.b.ctr + 1, clk);
 }
 
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,

@@ -136,7 +136,7 @@ EXPORTED_SYMBOLS = (
     "hlc_decode_proposals", "hlc_validate_wire_proposals", "hlc_validate_wire_proposals_device",
     "hlc_process_votes", "hlc_process_votes_device", "hlc_synth_arena_bytes", "hlc_synth_votes_device",
     "hlc_synth_byzantine_device", "hlc_outcome_counts_device", "hlc_host_alloc", "hlc_host_free",
-    "hlc_host_threads", "hlc_ctx_last_host_trace",
+    "hlc_host_threads", "hlc_ctx_last_host_trace", "hlc_ctx_set_clock_probe", "hlc_ctx_clock_probe",
 )
 
 _lib = None
@@ -222,6 +222,12 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_ctx_take_kernel_time.restype = c_int
     lib.hlc_ctx_take_chain_time.argtypes = [vp, POINTER(ctypes.c_double), u64p]
     lib.hlc_ctx_take_chain_time.restype = c_int
+    if hasattr(lib, "hlc_ctx_set_clock_probe"):  # (diagnostics: absent from older builds loaded for A/B runs)
+        lib.hlc_ctx_set_clock_probe.argtypes = [vp, c_int]
+        lib.hlc_ctx_set_clock_probe.restype = c_int
+        lib.hlc_ctx_clock_probe.argtypes = [vp, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
+                                            POINTER(ctypes.c_double), u64p]
+        lib.hlc_ctx_clock_probe.restype = c_int
     _lib = lib
     return lib
 

@@ -311,6 +311,18 @@ class Engine:
                                                      ctypes.byref(cms), ctypes.byref(cl)))
         return rms.value, rl.value, cms.value, cl.value
 
+    def set_clock_probe(self, enable: bool) -> None:
+        """k_rec_main of later validate_proposals_device calls stamps each wave's clock ticks (diagnostic)."""
+        _ffi.check(self.lib.hlc_ctx_set_clock_probe(self.ctx, 1 if enable else 0))
+
+    def clock_probe(self) -> dict:
+        """The shader clock the last stamped k_rec_main launch's waves ran at (hlc_ctx_clock_probe)."""
+        med, lo, hi = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        w = c_uint64()
+        _ffi.check(self.lib.hlc_ctx_clock_probe(self.ctx, ctypes.byref(med), ctypes.byref(lo), ctypes.byref(hi),
+                                                ctypes.byref(w)))
+        return {"median_GHz": med.value, "min_GHz": lo.value, "max_GHz": hi.value, "waves": w.value}
+
     def take_chain_time(self):
         """-> (chain_ms, launches): chain-check + duplicate + tally kernels since the previous take."""
         ms, n = ctypes.c_double(), c_uint64()

@@ -251,6 +251,13 @@ int hlc_ctx_take_kernel_time(hlc_ctx* ctx, double* recover_ms, uint64_t* recover
 /* The same for the chain-check + duplicate + tally kernels of each validate-many call
  * (validate_vote_chain, initialize_with_votes and the tally: utils.rs:175-286, session.rs:253-298). */
 int hlc_ctx_take_chain_time(hlc_ctx* ctx, double* chain_ms, uint64_t* launches);
+/* enable != 0: k_rec_main of every later validate-many call on device buffers (hlc_validate_proposals_device)
+ * stamps each wave's core-clock and 100 MHz reference ticks over its life (s_memtime / s_memrealtime; one
+ * store per wave at its end).  Diagnostic: bench.py turns it on for calls after its timed steps only. */
+int hlc_ctx_set_clock_probe(hlc_ctx* ctx, int enable);
+/* The shader clock (GHz) the stamped waves of the last such launch ran at: median, minimum and maximum over
+ * the waves, and how many waves stamped.  HLC_EINVAL when no launch was stamped. */
+int hlc_ctx_clock_probe(hlc_ctx* ctx, double* median_ghz, double* min_ghz, double* max_ghz, uint64_t* waves);
 
 /* ---- Hot-path entry points (host buffers, blocking) ----------------------------- */
 

@@ -1,13 +1,13 @@
 """Shader clock under k_rec_main, measured per MI355X_MICROARCH.md 'DVFS give-back' item 6 (GPU box).
 
-Run with a probe build (make variant NAME=clk DEFS=-DHLC_CLOCK_PROBE; HLC_LIB points at it): the
-config-2 batch (640k votes, generated on the device) goes through hlc_validate_proposals_device
-back to back for --seconds; then --last stamped launches are separated by marker lines.  Every
-launch's k_rec_main blocks print `HLC_CLOCK block b votes v clk c wall w GHz g` (s_memtime ticks
-over s_memrealtime ticks); `summarize` reads the log and reports, per variant, the median clock
-of the last launch's blocks and the back-to-back votes/s.
+The config-2 batch (640k votes, generated on the device) goes through hlc_validate_proposals_device
+back to back for --seconds; then --last calls run with the library's clock stamps on
+(hlc_ctx_set_clock_probe: every k_rec_main wave stamps s_memtime / s_memrealtime at its start and end)
+and each prints `HLC_CLOCK call k median m min a max b waves w`.  `summarize` reads the logs and
+reports, per log, the last stamped call's clock and the back-to-back votes/s.  (HLC_LIB selects another
+build of the library for an A/B.)
 
-    HLC_LIB=.../libhlc_clk.so python tools/clock_probe.py run --tag clk > gpurun_out/clk.log
+    python tools/clock_probe.py run --tag shipped > gpurun_out/clk.log
     python tools/clock_probe.py summarize gpurun_out/clk*.log
 """
 from __future__ import annotations
@@ -15,7 +15,6 @@ from __future__ import annotations
 import argparse
 import os
 import re
-import statistics
 import sys
 import time
 
@@ -44,34 +43,32 @@ def run(args) -> None:
         torch.cuda.synchronize()
     el = time.perf_counter() - t0
     print(f"HLC_RATE tag={args.tag} calls={calls} seconds={el:.3f} votes_per_s={db.n * calls / el:.6g}", flush=True)
+    eng.set_clock_probe(True)
     for k in range(args.last):
-        print(f"HLC_MARK {k}", flush=True)
         eng.validate_proposals_device(db, s.cuda_stream)
         torch.cuda.synchronize()
-    print("HLC_END", flush=True)
+        c = eng.clock_probe()
+        print(f"HLC_CLOCK call {k} median {c['median_GHz']:.4f} min {c['min_GHz']:.4f} max {c['max_GHz']:.4f} "
+              f"waves {c['waves']}", flush=True)
+    eng.set_clock_probe(False)
     eng.close()
 
 
 def summarize(paths) -> None:
-    pat = re.compile(r"HLC_CLOCK block (\d+) votes (\d+) clk (\d+) wall (\d+) GHz ([\d.]+)")
+    pat = re.compile(r"HLC_CLOCK call (\d+) median ([\d.]+) min ([\d.]+) max ([\d.]+) waves (\d+)")
     for p in paths:
-        rate, cur, last = None, None, []
+        rate, last = None, None
         for line in open(p, errors="replace"):
             if line.startswith("HLC_RATE"):
                 rate = line.strip()
-            elif line.startswith("HLC_MARK"):
-                cur = []
-            elif line.startswith("HLC_END"):
-                last = cur or []
-            else:
-                m = pat.search(line)
-                if m and cur is not None:
-                    cur.append(float(m.group(5)))
-        med = statistics.median(last) if last else float("nan")
-        lo = min(last) if last else float("nan")
-        hi = max(last) if last else float("nan")
-        print(f"{os.path.basename(p)}: last stamped launch: {len(last)} blocks, median {med:.3f} GHz "
-              f"(min {lo:.3f}, max {hi:.3f}); {rate}")
+            m = pat.search(line)
+            if m:
+                last = m
+        if last is None:
+            print(f"{os.path.basename(p)}: no stamped call; {rate}")
+            continue
+        print(f"{os.path.basename(p)}: last stamped call: {last.group(5)} waves, median {float(last.group(2)):.3f} GHz "
+              f"(min {float(last.group(3)):.3f}, max {float(last.group(4)):.3f}); {rate}")
 
 
 def main() -> int:

@@ -20,7 +20,8 @@
 #   profile    tools/profile.sh TAG (kernel trace + PMC passes of the headline leg)
 #   ab         tools/ab_arms.sh $AB_ARMS (alternating A/B arms: lib/variants builds or env settings;
 #              $AB_MODE = headline / legs / host)
-#   clock      tools/clock_probe.py over the HLC_CLOCK_PROBE builds in $CLOCK_VARIANTS, two alternating rounds
+#   clock      tools/clock_probe.py (the library's k_rec_main clock stamps), two rounds; $CLOCK_VARIANTS names
+#              lib/variants/libhlc_NAME.so builds to alternate with the shipped library ("shipped")
 set -o pipefail
 TAG=$1
 shift
@@ -112,8 +113,9 @@ for step in "$@"; do
     bash tools/ab_arms.sh $AB_ARMS || exit 1 ;;
   clock)
     for round in 1 2; do
-      for v in $CLOCK_VARIANTS; do
-        HLC_LIB=$PWD/hashgraph-like-consensus_amd/lib/variants/libhlc_$v.so timeout -k 10 200 python tools/clock_probe.py \
+      for v in shipped $CLOCK_VARIANTS; do
+        L=""; [ $v != shipped ] && L=$PWD/hashgraph-like-consensus_amd/lib/variants/libhlc_$v.so
+        HLC_LIB=$L timeout -k 10 200 python tools/clock_probe.py \
           run --tag $v > $O/clock_${TAG}_${v}_$round.log 2>&1 || fail clock $O/clock_${TAG}_${v}_$round.log
       done
     done
