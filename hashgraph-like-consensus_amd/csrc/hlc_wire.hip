@@ -58,13 +58,16 @@ struct GSrc {
   const uint8_t* g;
   __device__ __forceinline__ uint32_t operator[](uint64_t pos) const { return g[pos]; }
 };
+// the staged window as an LDS (address space 3) pointer: ds_read_u8, not a flat load that goes the
+// long way round through the vector memory pipeline and waits on both counters
+typedef const __attribute__((address_space(3))) uint8_t* lds_bytes;
 struct WinSrc {
   const uint8_t* g;
-  const uint8_t* lds;
+  lds_bytes lds;
   uint64_t wlo, wlen;
   __device__ __forceinline__ uint32_t operator[](uint64_t pos) const {
     const uint64_t d = pos - wlo;
-    return d < wlen ? (uint32_t)lds[d] : (uint32_t)g[pos];
+    return d < wlen ? (uint32_t)lds[(uint32_t)d] : (uint32_t)g[pos];
   }
 };
 
@@ -473,7 +476,7 @@ __global__ void __launch_bounds__(64) k_wire_walk_lds(const uint8_t* __restrict_
   uint32_t nv = 0;
   int err = HLC_WIRE_OK;
   uint64_t pos = base;
-  const WinSrc src{wire, win + (size_t)threadIdx.x * LW_WIN, my_lo, my_len};
+  const WinSrc src{wire, (lds_bytes)(win + (size_t)threadIdx.x * LW_WIN), my_lo, my_len};
   while (pos < end)
     if ((err = walk_field(src, wire, pos, base, end, o, nv, slab_off + m * SLAB, slab_len + m * SLAB, SLAB))) break;
   if (nv > SLAB) atomicOr(big, 1u);
@@ -753,7 +756,7 @@ __device__ __forceinline__ WinSrc stage_records(uint8_t* win, unsigned long long
   if (wlen > VOTE_WIN) wlen = 0;
   if (wlen) load_window(win, wire, wlo, wlo + wlen, aligned != 0);
   __syncthreads();
-  return WinSrc{wire, win, wlo, wlen};
+  return WinSrc{wire, (lds_bytes)win, wlo, wlen};
 }
 
 // One Vote record (prost message::merge -> merge_loop, consensus.proto:19-29): fields are read from the
