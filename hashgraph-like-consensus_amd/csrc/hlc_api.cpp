@@ -1073,8 +1073,10 @@ int first_batch() {
 // aux2, each with its own per-lane scratch), once its upload (ev_up[k]) has landed.
 int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, uint64_t m, const uint8_t* dbytes,
                  const uint64_t* sig_off, size_t off_stride, const uint32_t* sig_len, size_t len_stride,
-                 std::vector<RecFront>& fronts, hipEvent_t ready = nullptr) {
+                 std::vector<RecFront>& fronts, hipEvent_t ready = nullptr, uint64_t cap_waves = 0) {
   if (!m) return 0;
+  // cap_waves != 0: this range's grid holds at most that many waves (wire_front_cap)
+  const uint64_t lanes = cap_waves ? std::min<uint64_t>(c->rec_lanes, cap_waves * 64) : c->rec_lanes;
   // the first range's prep is on the call's critical path with the device otherwise idle: one vote
   // per lane (no batched inversion), so its dependent chain is an eighth as long
   const hlc::RecRange range{a0, m, c->rec_works[k]->as<uint32_t>(), k == 0 ? first_batch() : 0};
@@ -1084,7 +1086,7 @@ int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, u
   HIPCHK(hipStreamWaitEvent(a, ready ? ready : c->ev_up[k], 0));
   hlc::launch_recover_prep(n, dbytes, sig_off, off_stride, sig_len, len_stride, c->rec_work.as<uint32_t>(), a,
                            nullptr, &range);
-  hlc::launch_recover_main(n, dbytes, sig_off, off_stride, scratch, c->rec_lanes, c->rec_work.as<uint32_t>(), a,
+  hlc::launch_recover_main(n, dbytes, sig_off, off_stride, scratch, lanes, c->rec_work.as<uint32_t>(), a,
                            c->rec_force_exact, &range);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_main[k], a));
@@ -1518,6 +1520,16 @@ void wire_ranges(const uint64_t* moff, const uint32_t* mlen, uint64_t nm, std::v
   }
 }
 
+// Waves per recovery grid of every message range but the last (HLC_WIRE_FRONT_CAP, default 1536 of the
+// 2,048 a full grid holds; 0 = full grids).  Two overlapping full grids hold every VGPR of the device, so
+// the next range's decode and prep wait until one drains (profiles/r05/wire_host_call_timeline.txt);
+// capped grids leave them room.  +0.5 to +2.3% from host buffers over four A/B sessions
+// (profiles/r05/ab_wire_front_cap.txt); the last range runs alone at the end and keeps the full grid.
+uint64_t wire_front_cap() {
+  const char* e = std::getenv("HLC_WIRE_FRONT_CAP");
+  return e ? (uint64_t)std::max(0LL, std::atoll(e)) : 1536;
+}
+
 // bytes per staging / upload piece of the wire host entry (HLC_WIRE_CHUNK, default 4 MiB; 8 MiB measured
 // 1-2% slower with non-temporal staging copies): piece j+1 is copied into page-locked memory while piece
 // j's DMA runs
@@ -1627,7 +1639,9 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
   CHK(st.up(0, o[3]));
   const bool wire_pinned = is_pinned(wire, U);
   const uint64_t chunk = wire_chunk();
+  const uint64_t front_cap = wire_front_cap();
   tr.fact("ranges", (double)R);
+  tr.fact("front_cap_waves", (double)front_cap);
   tr.fact("wire_pinned", wire_pinned ? 1 : 0);
   tr.fact("pool_cpus", (double)c->pool_cpus.size());
   uint64_t N = 0, base = 0;  // per-vote capacity (fixed after range 0), votes decoded so far
@@ -1732,7 +1746,7 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     if (nv) {
       CHK(c->rec_works[k]->ensure(hlc::recover_range_words(nv) * 4));
       CHK(launch_front(c, tr, N, k, base, nv, dwire, dk.field_off + HLC_F_SIGNATURE, HLC_NFIELDS,
-                       dk.field_len + HLC_F_SIGNATURE, HLC_NFIELDS, fronts, c->ev_dec[k]));
+                       dk.field_len + HLC_F_SIGNATURE, HLC_NFIELDS, fronts, c->ev_dec[k], k + 1 < R ? front_cap : 0));
     }
     base += nv;
     return 0;
