@@ -405,14 +405,11 @@ def traced_phases(eng, call, calls: int = 3) -> dict:
     """The host-buffer call's phase times (HLC_HOST_TRACE=2, hlc_ctx_last_host_trace) over `calls`
     extra untimed calls: per phase the median ms from the call's start, plus the trace's facts."""
     import statistics
-    os.environ["HLC_HOST_TRACE"] = "2"
     runs = []
-    try:
+    with eng.options(host_trace=2):  # HLC_OPT_HOST_TRACE: kept for hlc_ctx_last_host_trace only
         for _ in range(calls):
             call()
             runs.append(eng.last_host_trace())
-    finally:
-        os.environ.pop("HLC_HOST_TRACE", None)
     runs = [r for r in runs if r]
     if not runs:
         return {}
@@ -550,18 +547,15 @@ def wire_leg(eng, w, db, dev, stream, handle, args, world, dist, np, torch, synt
             return (time.perf_counter() - t0) / args.steps
 
         hel = timed_host()
-        # the unpipelined arm of the same entry (HLC_WIRE_PIPELINE=0: the whole buffer uploaded, then
+        # the unpipelined arm of the same entry (HLC_OPT_WIRE_PIPELINE 0: the whole buffer uploaded, then
         # decoded, then validated) beside it -- what the message-range pipeline gains
-        os.environ["HLC_WIRE_PIPELINE"] = "0"
-        try:
+        with eng.options(wire_pipeline=0):
             pel = timed_host()
-        finally:
-            os.environ.pop("HLC_WIRE_PIPELINE", None)
         host = {"value": db.n / hel, "unit": "votes/s", "ms_per_call": hel * 1e3,
                 "what": "hlc_validate_wire_proposals from host buffers (PCIe-inclusive; pageable bytes, decoded and "
                         "recovered message range by message range as they land)",
                 "unpipelined": {"value": db.n / pel, "unit": "votes/s", "ms_per_call": pel * 1e3,
-                                "what": "the same entry with HLC_WIRE_PIPELINE=0 (upload all, decode, validate)"},
+                                "what": "the same entry with HLC_OPT_WIRE_PIPELINE 0 (upload all, decode, validate)"},
                 "phases": traced_phases(eng, host_call)}
     return {
         "metric": "verified votes/s from wire bytes (device protobuf decode + validation)",
@@ -689,9 +683,10 @@ def e2e_leg_concurrent(eng, w, args, np, contexts: int = 3, threads: int = 4):
 
     from hashgraph_like_consensus.engine import Engine
     b, d = w.batch, w.desc
-    old = os.environ.get("HLC_HOST_THREADS")
-    os.environ["HLC_HOST_THREADS"] = str(threads)
+    old = eng.get_option("host_threads")
     engs = [eng] + [Engine(eng.device) for _ in range(contexts - 1)]
+    for e in engs:
+        e.set_option("host_threads", threads)  # HLC_OPT_HOST_THREADS per context
     try:
         for e in engs:
             e.validate_proposals(b, d, w.now, want_votes=True)
@@ -722,10 +717,7 @@ def e2e_leg_concurrent(eng, w, args, np, contexts: int = 3, threads: int = 4):
     finally:
         for e in engs[1:]:
             e.close()
-        if old is None:
-            os.environ.pop("HLC_HOST_THREADS", None)
-        else:
-            os.environ["HLC_HOST_THREADS"] = old
+        eng.set_option("host_threads", old)
     return {
         "metric": "verified votes/s, host buffers in and out (PCIe-inclusive hlc_validate_proposals), "
                   f"{contexts} callers at once (one context + one thread each, {threads} staging threads per "
@@ -889,6 +881,124 @@ def config4_shard(rank: int):
     return start, min(per, CONFIG4_PROPOSALS - start)
 
 
+def config4_shard_leg(eng, args, torch, synth, DeviceBatch, dev):
+    """Secondary line at N = 1: rank 0's shard of config 4 -- 195,313 proposals x 64 =
+    12,500,032 votes, generated and signed on this GPU -- through exactly the per-rank step of the N > 1
+    runs (hlc_validate_proposals_device + the outcome counters; the exchange has nothing to gather at one
+    rank), so the driver's 1 -> 8 scaling curve has a same-workload N = 1 point (`scaling_basis`)."""
+    from hashgraph_like_consensus.parallel import ShardExchange
+    start, P = config4_shard(0)
+    V = 64
+    t = time.perf_counter()
+    db = DeviceBatch.synthetic(eng, P, V, V, True, synth.config_seed(4), start_proposal=start, device=dev)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t
+    eng.reserve(db.n, P, db.bytes_len)
+    s = torch.cuda.Stream(device=dev)
+    ex = ShardExchange(P, 1, dev, engine=eng)
+
+    def step():
+        eng.validate_proposals_device(db, s.cuda_stream)
+        with torch.cuda.stream(s):
+            ex.local_counters(db.results, db.status, P, db.n)
+
+    step()
+    torch.cuda.synchronize()
+    res = db.results_numpy()
+    assert (res["status"] == 0).all() and (res["total"] == V).all() and (db.status_numpy() == 0).all()
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t) / args.steps
+    counters = ex.summary()
+    assert counters["verified_votes"] == db.n
+    n = db.n
+    del db
+    torch.cuda.empty_cache()
+    return {
+        "metric": "verified votes/s, config 4 rank-0 shard (195,313 proposals x 64 = 12.5M votes) on one GPU, "
+                  "the per-rank step of the N > 1 runs",
+        "value": n / el,
+        "unit": "votes/s",
+        "ms_per_step": el * 1e3,
+        "votes_per_step": n,
+        "proposals": P,
+        "gen_seconds": gen_s,
+    }
+
+
+# the bench line printed on stdout carries the headline and one number per leg (VERDICT r05 item 2: a
+# ~10 KB line was cut in the driver's tail); everything else -- phase traces, NUMA facts, per-kernel
+# traffic, status histograms, rocprof kernel times -- goes to this side file, written by the same run
+DETAIL_PATH = os.environ.get("HLC_BENCH_DETAIL") or os.path.join(ROOT, "profiles", "bench_detail.json")
+LEG_NAMES = ("wire", "wire_from_host", "end_to_end", "end_to_end_pinned", "end_to_end_concurrent", "stream",
+             "config3", "config5", "config4_shard")
+
+
+def _value(d):
+    return d.get("value") if isinstance(d, dict) else None
+
+
+def compact_line(out: dict, detail_path: str) -> dict:
+    """The stdout line from the full record: the driver's contract keys, a flat `legs` object of votes/s,
+    the roofline and CPU-baseline essentials, and where the rest went (kept well under 4 KB)."""
+    legs = {k: _value(out.get(k)) for k in LEG_NAMES}
+    w = out.get("wire")
+    if isinstance(w, dict):
+        legs["wire_from_host"] = _value(w.get("from_host_buffers"))
+    errors = {k: v["error"][:160] for k, v in out.items() if isinstance(v, dict) and "error" in v}
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config") if k in out}
+    line["legs"] = {k: v for k, v in legs.items() if v is not None}
+    if "scaling_basis" in out:
+        line["scaling_basis"] = out["scaling_basis"]
+    rf = out.get("roofline", {})
+    live = rf.get("live_k_rec_main_clock") or {}
+    line["roofline"] = {
+        **{k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_per_vote",
+                                  "frac_rocprof_chain", "valu_lane_op_frac", "valu_issue_frac", "kernel_ms_avg")},
+        "kernel": "recovery: k_rec_prep + k_rec_main + k_rec_comb + k_rec_final + k_rec_addr (HIP events)",
+        "valu_instr_per_vote_k_rec_main": (rf.get("valu_instr_per_vote") or {}).get("k_rec_main"),
+        "live_k_rec_main_GHz": live.get("median_GHz"),
+    }
+    cb = out.get("cpu_baseline")
+    if isinstance(cb, dict) and "value" in cb:
+        line["cpu_baseline"] = {**{k: cb.get(k) for k in ("value", "unit", "cores", "kind", "cpu_model")},
+                                "sample": (cb.get("sample") or "")[:200],
+                                "single_thread": _value(cb.get("single_thread")),
+                                "whole_host_estimate": _value(cb.get("whole_host_estimate"))}
+    for k in ("gpu_over_cpu", "gpu_over_cpu_whole_host_estimate", "counters_per_step", "gathered_results", "probe"):
+        if k in out:
+            line[k] = out[k]
+    ct = out.get("chain_tally")
+    if isinstance(ct, dict):
+        line["chain_tally"] = {"ms_per_call": ct.get("ms_per_call"), "GBps": ct.get("GBps")}
+    ex = out.get("exchange")
+    if isinstance(ex, dict):
+        line["exchange_ms_per_step"] = ex.get("ms_per_step_max_over_ranks")
+    if errors:
+        line["leg_errors"] = errors
+    line["detail"] = os.path.relpath(detail_path, ROOT) if detail_path else None
+    return line
+
+
+def write_detail(out: dict, path: str):
+    """The full record (every leg's phases, NUMA facts, traffic detail, histograms) as JSON; the path
+    on success, None when it cannot be written (a read-only tree: the stdout line still prints)."""
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return path
+    except OSError as e:
+        print(f"bench: detail not written ({e})", file=sys.stderr, flush=True)
+        return None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -907,6 +1017,8 @@ def main() -> int:
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 leg (1M-vote chain, ~10 s to generate)")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 leg (1/3 Byzantine votes)")
+    ap.add_argument("--no-config4-shard", action="store_true",
+                    help="skip the N = 1 config-4 shard leg (12.5M votes, the N > 1 per-rank workload)")
     args = ap.parse_args()
 
     import numpy as np
@@ -1179,6 +1291,14 @@ def main() -> int:
         eng.set_kernel_timing(False)
     if world == 1 and not args.no_config5:
         leg("config5", lambda: config5_leg(eng, args, torch, synth, DeviceBatch, dev))
+    if world == 1 and not args.no_config4_shard:
+        leg("config4_shard", lambda: config4_shard_leg(eng, args, torch, synth, DeviceBatch, dev))
+    # what the per-GPU workload of each N is (the driver computes scaling from the per-N values)
+    out["scaling_basis"] = {
+        "n1_headline": "config 2: 640,000 votes per GPU per step (BASELINE.json configs[1])",
+        "n_gt_1": "config 4 shards: 195,313 proposals x 64 = 12.5M votes per GPU per step",
+        "n1_same_workload": "legs.config4_shard: rank 0's config-4 shard on one GPU, the per-rank step of N > 1",
+    }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         leg("cpu_baseline", lambda: cpu_baseline(w.batch, w.desc, w.now, min(args.cpu_sample_proposals, P),
                                                  min(args.cpu_single_proposals, P)))
@@ -1204,7 +1324,8 @@ def main() -> int:
     if probe:
         out["probe"] = "HLC_BENCH_PROBE=1: a timing-probe build, results not checked (not a valid measurement)"
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        detail = write_detail(out, DETAIL_PATH)
+        print(json.dumps(compact_line(out, detail)), flush=True)
     if dist is not None:
         dist.destroy_process_group()
     eng.close()

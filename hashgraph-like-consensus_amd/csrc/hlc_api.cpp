@@ -4,6 +4,8 @@
 
 #include <pthread.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -130,17 +132,17 @@ __attribute__((target("avx2"))) void copy_nt_avx2(uint8_t* dst, const uint8_t* s
   _mm_sfence();
 }
 #endif
-std::atomic<bool> g_nt_copy{false};  // refreshed from the environment by every host-buffer call (host_resources)
-void refresh_nt_copy() {
+bool cpu_has_avx2() {
 #ifdef HLC_HAVE_NT_COPY
-  const char* e = std::getenv("HLC_NT_COPY");
-  g_nt_copy.store((!e || std::atoi(e) != 0) && __builtin_cpu_supports("avx2"), std::memory_order_relaxed);
+  return __builtin_cpu_supports("avx2");
+#else
+  return false;
 #endif
 }
-bool nt_copy_enabled() { return g_nt_copy.load(std::memory_order_relaxed); }
-void stage_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+// nt: the context's HLC_OPT_NT_COPY (and the CPU has AVX2)
+void stage_copy(uint8_t* dst, const uint8_t* src, size_t n, bool nt) {
 #ifdef HLC_HAVE_NT_COPY
-  if (n >= 4096 && nt_copy_enabled()) {
+  if (nt && n >= 4096) {
     copy_nt_avx2(dst, src, n);
     return;
   }
@@ -177,6 +179,17 @@ class HostPool {
     for (auto& t : th_) t.join();
   }
   int threads() const { return (int)th_.size() + 1; }
+  // moves every worker to another CPU set (empty: any CPU of the process's affinity mask)
+  void rebind(const std::vector<int>& cpus) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (cpus.empty()) {
+      if (sched_getaffinity(0, sizeof set, &set) != 0) return;
+    } else {
+      for (int c : cpus) CPU_SET(c, &set);
+    }
+    for (auto& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
+  }
   int chunks() const { return 4 * threads(); }
   void run(const std::function<void(int, int)>& fn) {
     {
@@ -225,6 +238,83 @@ class HostPool {
   bool stop_ = false;
 };
 
+// A context's tunables (hlc_ctx_set_option, HLC_OPT_* in hlc.h).  Their defaults come from the
+// environment, read once when the context is created (read_env, the only getenv site of the library) --
+// never inside a call, so an embedder's threads may setenv freely and the Rust binding sets them per
+// context.
+struct Options {
+  int host_threads = 16;      // HLC_OPT_HOST_THREADS: staging threads incl. the caller
+  int pool_bind = HLC_POOL_BIND_GPU;  // HLC_OPT_POOL_BIND
+  int nt_copy = 1;            // HLC_OPT_NT_COPY: non-temporal staging copies (AVX2)
+  std::vector<uint64_t> split_votes{98304, 196608};  // HLC_OPT_SPLIT_VOTES (split_ranges)
+  int host_trace = 0;         // HLC_OPT_HOST_TRACE
+  int first_batch = 1;        // HLC_OPT_FIRST_BATCH
+  int rest_pieces = 3;        // HLC_OPT_REST_PIECES
+  std::vector<uint64_t> wire_split_bytes{8ull << 20, 16ull << 20, 24ull << 20, 32ull << 20};  // (wire_ranges)
+  uint64_t wire_front_cap = 1536;  // HLC_OPT_WIRE_FRONT_CAP (waves; 0 = full grids)
+  uint64_t wire_chunk = 4ull << 20;  // HLC_OPT_WIRE_CHUNK
+  int rec_force_exact = 0;    // HLC_OPT_REC_FORCE_EXACT: every vote through the checked chains (tests)
+  int serial_stages = 0;      // HLC_OPT_SERIAL_STAGES: prep + main after the prehash on one stream
+  int wire_pipeline = 1;      // HLC_OPT_WIRE_PIPELINE: 0 = the unpipelined wire host entry (A/B arm)
+  int wire_walk = -1;         // HLC_OPT_WIRE_WALK: -1 the build's default walker, 0 per lane, 1 LDS
+};
+
+// The CPUs the cgroup (v2) quota grants the process, or 0 when there is none.
+double cgroup_cpu_quota() {
+  std::FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r");
+  if (!f) return 0;
+  char q[64] = {0};
+  double per = 0;
+  const int got = std::fscanf(f, "%63s %lf", q, &per);
+  std::fclose(f);
+  if (got != 2 || per <= 0 || std::strcmp(q, "max") == 0) return 0;
+  return std::atof(q) / per;
+}
+
+std::vector<uint64_t> parse_list(const char* p) {
+  std::vector<uint64_t> out;
+  while (*p) {
+    char* end = nullptr;
+    const uint64_t x = std::strtoull(p, &end, 10);
+    if (end == p) break;
+    out.push_back(x);
+    p = *end == ',' ? end + 1 : end;
+  }
+  return out;
+}
+
+// The defaults of a new context's options, from the environment (the HLC_* variables the tools set).
+// Staging workers (HLC_HOST_THREADS): by default 16 -- the GPU box's CPU share per GPU -- capped by the
+// hardware threads and by this process's share of the CPUs: the cgroup quota (or the hardware threads)
+// divided by the ranks on the node (LOCAL_WORLD_SIZE, set by torch.distributed.run), so that 8 ranks do
+// not run 8 x 16 staging threads on one node's quota.  Measured on two boxes with the chunked pool: 16
+// threads 86.9 / 88.3 M votes/s, 12: 86.0 / 88.0, 8: 85.2 / 87.1 (profiles/r04/host_pool_threads.txt).
+Options read_env() {
+  Options o;
+  const char* e;
+  const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+  int ranks = 1;
+  if ((e = std::getenv("LOCAL_WORLD_SIZE"))) ranks = std::max(1, std::atoi(e));
+  const double quota = cgroup_cpu_quota();
+  const double share = (quota > 0 ? std::min(quota, (double)hw) : (double)hw) / ranks;
+  o.host_threads = std::max(1, std::min({16, hw, (int)(share + 1e-9)}));
+  if ((e = std::getenv("HLC_HOST_THREADS"))) o.host_threads = std::max(1, std::min(std::atoi(e), 64));
+  if ((e = std::getenv("HLC_POOL_BIND"))) o.pool_bind = std::max(0, std::min(std::atoi(e), 2));
+  if ((e = std::getenv("HLC_NT_COPY"))) o.nt_copy = std::atoi(e) != 0;
+  if ((e = std::getenv("HLC_SPLIT_VOTES"))) o.split_votes = parse_list(e);
+  if ((e = std::getenv("HLC_HOST_TRACE"))) o.host_trace = std::max(0, std::min(std::atoi(e), 2));
+  if ((e = std::getenv("HLC_FIRST_BATCH"))) o.first_batch = std::max(0, std::atoi(e));
+  if ((e = std::getenv("HLC_REST_PIECES"))) o.rest_pieces = std::max(1, std::min(std::atoi(e), 64));
+  if ((e = std::getenv("HLC_WIRE_SPLIT_BYTES"))) o.wire_split_bytes = parse_list(e);
+  if ((e = std::getenv("HLC_WIRE_FRONT_CAP"))) o.wire_front_cap = (uint64_t)std::max(0LL, std::atoll(e));
+  if ((e = std::getenv("HLC_WIRE_CHUNK"))) o.wire_chunk = std::max<uint64_t>(std::strtoull(e, nullptr, 10), 4096);
+  if ((e = std::getenv("HLC_REC_FORCE_EXACT"))) o.rec_force_exact = std::atoi(e) != 0;
+  if ((e = std::getenv("HLC_SERIAL_STAGES"))) o.serial_stages = std::atoi(e) != 0;
+  if ((e = std::getenv("HLC_WIRE_PIPELINE"))) o.wire_pipeline = std::atoi(e) != 0;
+  if ((e = std::getenv("HLC_WIRE_WALK"))) o.wire_walk = std::strcmp(e, "lane") == 0 ? 0 : 1;
+  return o;
+}
+
 }  // namespace
 
 struct hlc_ctx {
@@ -235,8 +325,7 @@ struct hlc_ctx {
   std::mutex mu;
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
-  int rec_force_exact = 0;  // HLC_REC_FORCE_EXACT=1: every vote through the checked chains (tests)
-  int serial_stages = 0;    // HLC_SERIAL_STAGES=1: prep + main after the prehash on one stream (clock probes, isolated kernel traces)
+  Options opt;  // hlc_ctx_set_option; defaults from the environment at creation (read_env)
   // hlc_validate_proposals (host buffers): a second recovery slot (stream, per-lane scratch, per-vote
   // records) so that two k_rec_main grids over the two vote ranges of a call overlap; an upload stream;
   // the page-locked staging of the inputs and outputs and their device copies (allocated on first use)
@@ -250,14 +339,14 @@ struct hlc_ctx {
   std::vector<hipEvent_t> ev_cnt, ev_dec;  // wire host entry, per message range: vote count read back, decoded
   PBuf pin_cnt;                            // wire host entry: the ranges' vote counts (page-locked)
   uint64_t wire_hint = 0;                  // wire host entry: the largest vote count a call decoded
-  std::string last_trace;                  // the last host-buffer call's HLC_HOST_TRACE JSON
+  std::string last_trace;                  // the last host-buffer call's host trace JSON (HLC_OPT_HOST_TRACE)
   hipEvent_t ev_rest = nullptr, ev_done = nullptr;
   std::unique_ptr<HostPool> pool;  // staging workers (HLC_HOST_THREADS)
-  std::vector<int> pool_cpus;      // the CPU set its workers are bound to (host_pool_cpus)
-  int pool_bind = -1;              // the HLC_POOL_BIND setting the pool was made with
+  std::vector<int> pool_cpus;      // the CPU set its workers are bound to now (empty: unbound)
+  int pool_node = -2;              // the NUMA node they are bound to (-1: unbound, -2: not yet decided)
   // staged host inputs (host-buffer entry points)
   DBuf in_vote_id, in_pid, in_ts, in_vote, in_bytes, in_off, in_len, in_props;
-  DBuf in_off2, in_len2, in_off3, in_len3, in_priv, byz_key;
+  DBuf in_off2, in_len2, in_off3, in_len3, in_priv, byz_key, in_verdict;
   // outputs staged on device
   DBuf out_res, out_status, out_reason, out_rec, out_misc;
   // internal workspace
@@ -405,12 +494,26 @@ struct RecFront {
 // already in flight over those ranges (validate_host); one finish over all votes waits for them.
 // (One finish, not one per range: its k_rec_final / k_rec_addr are short low-occupancy kernels, and
 // per range they cost 0.95 ms against 0.67 ms for one launch over 640k votes.)
+// verdicts != nullptr (the *_verdicts entries, any ConsensusSignatureScheme): the scheme step is the
+// caller's per-vote verdict; the prehash runs without the Ethereum checks and keccak, and no recovery runs.
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t np,
                uint64_t now, uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, uint8_t* chain_code,
-               hipStream_t s, const RecFront* fronts = nullptr, int nfronts = 0, uint64_t rec_stride = 0) {
+               hipStream_t s, const RecFront* fronts = nullptr, int nfronts = 0, uint64_t rec_stride = 0,
+               const uint8_t* verdicts = nullptr) {
   const uint64_t n = dv->n;
   CHK(c->pre.ensure(n));
   CHK(c->pre_reason.ensure(n));
+  if (verdicts) {
+    hlc::launch_prehash_fused(dv, n, vote_prop, dprops, nullptr, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
+                              c->flag.as<uint32_t>(), s, false);
+    hlc::launch_prehash_stream(dv, n, vote_prop, dprops, c->flag.as<uint32_t>(), nullptr, c->pre.as<uint8_t>(),
+                               c->pre_reason.as<uint8_t>(), s, false);
+    if (chain_code) hlc::launch_chain_small(dv, dprops, np, chain_code, red, s);
+    hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), verdicts,
+                            status, reason, red, s);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   CHK(c->verify.ensure(n));
   CHK(c->kec_dig.ensure(n * 32));
   CHK(ensure_recover_scratch(c));
@@ -423,7 +526,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   // address).  Measured recovery time = prep bracket (aux) + main start (aux) .. finish end (s).
   // (HLC_SERIAL_STAGES=1: everything on `s`, prep + main after the prehash and the chain kernel --
   // the measurement of k_rec_main running alone)
-  hipStream_t aux = c->serial_stages ? s : c->aux;
+  hipStream_t aux = c->opt.serial_stages ? s : c->aux;
   hipEvent_t p0 = nullptr, p1 = nullptr, r0 = nullptr, r1 = nullptr;
   if (c->timing && !fronts) {
     p0 = c->take_event();
@@ -457,14 +560,14 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     for (int k = 0; k < nfronts; ++k) HIPCHK(hipStreamWaitEvent(s, fronts[k].done, 0));
     hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
                                dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(),
-                               c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->rec_force_exact,
+                               c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->opt.rec_force_exact,
                                rec_stride);
     hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
                             c->verify.as<uint8_t>(), status, reason, red, s);
     HIPCHK(hipGetLastError());
     return 0;
   }
-  if (c->serial_stages) {
+  if (c->opt.serial_stages) {
     CHK(prehash_and_chain());
   } else {
     HIPCHK(hipEventRecord(c->ev_fork, s));
@@ -488,16 +591,16 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     clk = c->clk_buf.as<unsigned long long>();
   }
   hlc::launch_recover_main(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, c->rec_scratch.as<uint32_t>(),
-                           c->rec_lanes, c->rec_work.as<uint32_t>(), aux, c->rec_force_exact, nullptr, clk,
+                           c->rec_lanes, c->rec_work.as<uint32_t>(), aux, c->opt.rec_force_exact, nullptr, clk,
                            clk ? &c->clk_waves : nullptr);
-  if (!c->serial_stages) {
+  if (!c->opt.serial_stages) {
     HIPCHK(hipEventRecord(c->ev_join, aux));
     CHK(prehash_and_chain());
     HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
   }
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_OWNER,
                              HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
-                             drec, s, c->rec_force_exact);
+                             drec, s, c->opt.rec_force_exact);
   if (c->timing) {
     HIPCHK(hipEventRecord(r1, s));
     c->rec_ev.emplace_back(r0, r1);
@@ -529,7 +632,8 @@ int reserve_validate(hlc_ctx* c, uint64_t n, uint64_t np) {
 // Device-resident validate-many (every pointer is device memory).
 int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops, uint64_t np, uint64_t now,
                     hlc_result* dres, uint8_t* dstatus, uint8_t* dreason, uint8_t* drec, hipStream_t s,
-                    const RecFront* fronts = nullptr, int nfronts = 0, uint64_t rec_stride = 0) {
+                    const RecFront* fronts = nullptr, int nfronts = 0, uint64_t rec_stride = 0,
+                    const uint8_t* verdicts = nullptr) {
   const uint64_t n = dv->n;
   if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
   hipEvent_t call0 = nullptr, call1 = nullptr;
@@ -565,7 +669,7 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   // recovery's main stage: k_vote_status reports each proposal's first failing vote)
   if (n)
     CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, np, now, status, reason, drec, c->red.as<uint32_t>(),
-                   c->chain_code.as<uint8_t>(), s, fronts, nfronts, rec_stride));
+                   c->chain_code.as<uint8_t>(), s, fronts, nfronts, rec_stride, verdicts));
   hipEvent_t ch0 = nullptr, ch1 = nullptr;
   if (c->timing) {  // chain check + duplicate detection + tally (+ k_chain_small's bracket in vote_stage)
     ch0 = c->take_event();
@@ -615,7 +719,7 @@ int decode_device(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const uint
     hlc::launch_wire_touch(wire, wire_len, c->w_big.as<uint32_t>() + 1, s);
     hlc::launch_wire_walk(0, wire, moff, mlen, nm, vcount, nullptr, dwout, dprops, scope, n_scope,
                           c->w_slab_off.as<uint64_t>(), c->w_slab_len.as<uint32_t>(), c->w_big.as<uint32_t>(), nullptr,
-                          nullptr, nullptr, c->w_huge.as<uint64_t>(), s);
+                          nullptr, nullptr, c->w_huge.as<uint64_t>(), s, nullptr, c->opt.wire_walk);
     // The huge-message count rides on the vote-total synchronisation; only when a message took the
     // parallel path (skipped by the walker, vote_count 0 so far) is there a second round trip.
     auto scan_totals = [&](uint64_t* h) -> int {
@@ -752,6 +856,15 @@ int check_votes_host(const hlc_votes* v) {
   return 0;
 }
 
+// A caller-side scheme's verdicts (the *_verdicts entries): HLC_VERIFY_TRUE / _FALSE / Err up to HLC_VERIFY_ERR
+int check_verdicts(const uint8_t* verdicts, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i)
+    if (verdicts[i] > HLC_VERIFY_ERR)
+      return set_err(HLC_EINVAL, "verdict " + std::to_string(verdicts[i]) + " at vote " + std::to_string(i) +
+                                     " above HLC_VERIFY_ERR");
+  return 0;
+}
+
 // Stage host votes on the device; returns a device-pointer view in *dv.
 int stage_votes(hlc_ctx* c, const hlc_votes* v, hlc_votes* dv, hipStream_t s) {
   const uint64_t n = v->n;
@@ -786,55 +899,42 @@ void destroy_ctx(hlc_ctx* ctx) {
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// The CPUs the cgroup (v2) quota grants the process, or 0 when there is none.
-double cgroup_cpu_quota() {
-  std::FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r");
-  if (!f) return 0;
-  char q[64] = {0};
-  double per = 0;
-  const int got = std::fscanf(f, "%63s %lf", q, &per);
-  std::fclose(f);
-  if (got != 2 || per <= 0 || std::strcmp(q, "max") == 0) return 0;
-  return std::atof(q) / per;
-}
-
-// Staging workers of the host-buffer entries (including the calling thread): HLC_HOST_THREADS, or by
-// default 16 -- the GPU box's CPU share per GPU -- capped by the hardware threads and by this
-// process's share of the CPUs: the cgroup quota (or the hardware threads) divided by the ranks on
-// the node (LOCAL_WORLD_SIZE, set by torch.distributed.run), so that 8 ranks do not run 8 x 16
-// staging threads on one node's quota.  Measured on two boxes with the chunked pool: 16 threads
-// 86.9 / 88.3 M votes/s, 12: 86.0 / 88.0, 8: 85.2 / 87.1 (profiles/r04/host_pool_threads.txt).
-int host_threads() {
-  if (const char* e = std::getenv("HLC_HOST_THREADS")) return std::max(1, std::min(std::atoi(e), 64));
-  const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-  int ranks = 1;
-  if (const char* r = std::getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, std::atoi(r));
-  const double quota = cgroup_cpu_quota();
-  const double share = (quota > 0 ? std::min(quota, (double)hw) : (double)hw) / ranks;
-  return std::max(1, std::min({16, hw, (int)(share + 1e-9)}));
-}
-
-// The CPUs of the device's NUMA node that this process may run on (sysfs: the device's PCI address ->
-// numa_node -> that node's cpulist, intersected with the affinity mask), or {} when unknown or when
-// HLC_POOL_BIND=0.  The host pool's workers are bound to them: their staging copies then write the
-// page-locked buffer from the socket the GPU hangs off (the DMA reads it from there).
-std::vector<int> host_pool_cpus(int device) {
-  std::vector<int> out;
-  const char* e = std::getenv("HLC_POOL_BIND");
-  if (e && std::atoi(e) == 0) return out;
+// The NUMA node of HIP device `device` (sysfs: the device's PCI address -> numa_node), or -1.
+int device_node(int device) {
   char bus[64] = {0};
   if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
     (void)hipGetLastError();
-    return out;
+    return -1;
   }
   for (char* q = bus; *q; ++q) *q = (char)std::tolower((unsigned char)*q);
   int node = -1;
-  {
-    std::FILE* f = std::fopen((std::string("/sys/bus/pci/devices/") + bus + "/numa_node").c_str(), "r");
-    if (!f) return out;
-    if (std::fscanf(f, "%d", &node) != 1) node = -1;
-    std::fclose(f);
-  }
+  std::FILE* f = std::fopen((std::string("/sys/bus/pci/devices/") + bus + "/numa_node").c_str(), "r");
+  if (!f) return -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
+
+// The node most of the sampled pages of [p, p + len) are on (move_pages without a target: a query,
+// nothing moves), or -1 when unknown (not yet touched, or the call is refused).
+int memory_node(const void* p, size_t len) {
+  if (!p || !len) return -1;
+  const uintptr_t page = 4096, a = (uintptr_t)p & ~(page - 1), b = ((uintptr_t)p + len - 1) & ~(page - 1);
+  const uint64_t pages = (b - a) / page + 1, k = std::min<uint64_t>(pages, 16);
+  void* addr[16];
+  int status[16];
+  for (uint64_t j = 0; j < k; ++j) addr[j] = reinterpret_cast<void*>(a + page * (k > 1 ? (pages - 1) * j / (k - 1) : 0));
+  if (syscall(SYS_move_pages, 0, (unsigned long)k, addr, nullptr, status, 0) != 0) return -1;
+  int votes[64] = {0}, best = -1;
+  for (uint64_t j = 0; j < k; ++j)
+    if (status[j] >= 0 && status[j] < 64 && ++votes[status[j]] > (best >= 0 ? votes[best] : 0)) best = status[j];
+  return best;
+}
+
+// The CPUs of NUMA node `node` that this process may run on (the node's cpulist intersected with the
+// affinity mask), or {} when unknown.
+std::vector<int> node_cpus(int node) {
+  std::vector<int> out;
   if (node < 0) return out;
   std::FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
   if (!f) return out;
@@ -859,24 +959,16 @@ std::vector<int> host_pool_cpus(int device) {
   return out;
 }
 
-// The recovery ranges of a host-buffer call of n items (HLC_SPLIT_VOTES="a,b,...", default
-// "98304,196608"; "0" = one range): a range of each listed size while at least twice that many
+// The recovery ranges of a host-buffer call of n items (HLC_OPT_SPLIT_VOTES: the first range; the
+// environment's HLC_SPLIT_VOTES="a,b,..." a list; default "98304,196608"; 0 = one range): a range of
+// each listed size while at least twice that many
 // items remain, then ranges of twice the previous size on the same rule (a large batch keeps the
 // device busy while the host gathers the next range's signatures; at most 16 ranges), then one
 // range for the rest.  Range k's k_rec_main grid starts once its signatures
 // have landed; ranges alternate between two streams (and two per-lane scratch buffers), so each
 // range's waves take the SIMD slots the previous range's waves free.
-std::vector<uint64_t> split_ranges(uint64_t n) {
-  std::vector<uint64_t> sizes, b{0};
-  const char* e = std::getenv("HLC_SPLIT_VOTES");
-  const char* p = e ? e : "98304,196608";
-  while (*p) {
-    char* end = nullptr;
-    const uint64_t x = std::strtoull(p, &end, 10);
-    if (end == p) break;
-    sizes.push_back(x);
-    p = *end == ',' ? end + 1 : end;
-  }
+std::vector<uint64_t> split_ranges(uint64_t n, const std::vector<uint64_t>& sizes) {
+  std::vector<uint64_t> b{0};
   uint64_t x = 0;
   for (size_t k = 0; k < 15; ++k) {
     x = k < sizes.size() ? sizes[k] : 2 * x;
@@ -920,8 +1012,12 @@ bool is_pinned(const void* p, size_t len) {
 // fired when the second k_rec_main ended, 4 ms after its DMA, and the prehash waited for it.  So the
 // upload stream takes the greatest priority and the second recovery stream the least: each draws
 // its queue from a pool of its own, apart from the normal-priority launch / aux streams.
-int host_resources(hlc_ctx* c) {
-  refresh_nt_copy();
+// The staging pool's workers are bound by HLC_OPT_POOL_BIND: to the CPUs of the GPU's NUMA node (their
+// copies then write the page-locked buffer from the socket the GPU hangs off; the DMA reads it from
+// there), or to those of the node the call's largest input (`src`, its arena) lives on (the copies then
+// read the caller's pages locally -- a cross-socket read costs more than a cross-socket write, DESIGN.md
+// §5), or not at all.  A node with fewer usable CPUs than workers is not bound to.
+int host_resources(hlc_ctx* c, const void* src = nullptr, size_t src_len = 0) {
   int least = 0, greatest = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   if (!c->copy) HIPCHK(hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, greatest));
@@ -930,13 +1026,20 @@ int host_resources(hlc_ctx* c) {
   if (!c->wlk) HIPCHK(hipStreamCreateWithPriority(&c->wlk, hipStreamNonBlocking, greatest));
   for (hipEvent_t* e : {&c->ev_rest, &c->ev_done})
     if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  if (!c->pool || c->pool->threads() != c->opt.host_threads) {
+    c->pool.reset(new HostPool(c->opt.host_threads - 1));
+    c->pool_node = -2;
+  }
   {
-    const char* e = std::getenv("HLC_POOL_BIND");
-    const int bind = e ? (std::atoi(e) != 0) : 1;
-    if (!c->pool || c->pool->threads() != host_threads() || c->pool_bind != bind) {
-      c->pool_cpus = host_pool_cpus(c->device);  // sysfs reads: once per pool
-      c->pool.reset(new HostPool(host_threads() - 1, c->pool_cpus));
-      c->pool_bind = bind;
+    int node = -1;
+    if (c->opt.pool_bind == HLC_POOL_BIND_GPU) node = device_node(c->device);
+    else if (c->opt.pool_bind == HLC_POOL_BIND_SOURCE) node = memory_node(src, src_len);
+    if (node != c->pool_node) {  // sysfs reads and the rebinding: only when the node changes
+      std::vector<int> cpus = node_cpus(node);
+      if ((int)cpus.size() < c->opt.host_threads - 1) cpus.clear();
+      c->pool->rebind(cpus);
+      c->pool_cpus = cpus;
+      c->pool_node = node;
     }
   }
   CHK(ensure_recover_scratch(c));
@@ -950,7 +1053,7 @@ int host_resources(hlc_ctx* c) {
 // JSON kept for hlc_ctx_last_host_trace only (bench.py's per-phase figures), nothing printed.
 struct HostTrace {
   using clk = std::chrono::steady_clock;
-  bool on = false, print = false;
+  bool on = false, print = false;  // HLC_OPT_HOST_TRACE 1: print + keep, 2: keep
   std::string* sink = nullptr;
   clk::time_point t0;
   std::vector<std::pair<std::string, double>> host, facts;
@@ -960,12 +1063,8 @@ struct HostTrace {
   void fact(const std::string& what, double v) {
     if (on) facts.emplace_back(what, v);
   }
-  explicit HostTrace(std::string* keep) : sink(keep) {
-    if (const char* e = std::getenv("HLC_HOST_TRACE")) {
-      const int v = std::atoi(e);
-      on = v != 0;
-      print = v == 1;
-    }
+  HostTrace(std::string* keep, int level) : on(level != 0), print(level == 1), sink(keep) {
+    if (sink) sink->clear();  // hlc_ctx_last_host_trace: "" after a call made without tracing
   }
   void start(hipStream_t s) {
     if (!on) return;
@@ -1018,6 +1117,7 @@ struct Staging {
   hlc_ctx* c;
   uint8_t* P;
   uint8_t* D;
+  bool nt = false;  // non-temporal staging copies (HLC_OPT_NT_COPY on a CPU with AVX2)
   int up(size_t off, size_t len) {
     if (len) HIPCHK(hipMemcpyAsync(D + off, P + off, len, hipMemcpyHostToDevice, c->copy));
     return 0;
@@ -1047,7 +1147,7 @@ struct DrainOnExit {
 
 // The recovery ranges of a host-buffer call (split_ranges) with their per-vote records and events.
 int prepare_ranges(hlc_ctx* c, uint64_t n, std::vector<uint64_t>& rb) {
-  rb = split_ranges(n);
+  rb = split_ranges(n, c->opt.split_votes);
   const size_t R = rb.size() - 1;
   CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   while (c->rec_works.size() < R) c->rec_works.emplace_back(new DBuf());
@@ -1062,11 +1162,7 @@ int prepare_ranges(hlc_ctx* c, uint64_t n, std::vector<uint64_t>& rb) {
   return 0;
 }
 
-// votes per k_rec_prep lane in the first recovery range (HLC_FIRST_BATCH, default 1; 8 = as the rest)
-int first_batch() {
-  const char* e = std::getenv("HLC_FIRST_BATCH");
-  return e ? std::atoi(e) : 1;
-}
+// votes per k_rec_prep lane in the first recovery range: HLC_OPT_FIRST_BATCH, default 1 (8 = as the rest)
 
 // Range k's front half of the recovery -- k_rec_prep + k_rec_main over its m items, signatures read
 // through (sig_off, sig_len) from the device arena -- on the aux streams in turn (k even: aux, odd:
@@ -1079,7 +1175,7 @@ int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, u
   const uint64_t lanes = cap_waves ? std::min<uint64_t>(c->rec_lanes, cap_waves * 64) : c->rec_lanes;
   // the first range's prep is on the call's critical path with the device otherwise idle: one vote
   // per lane (no batched inversion), so its dependent chain is an eighth as long
-  const hlc::RecRange range{a0, m, c->rec_works[k]->as<uint32_t>(), k == 0 ? first_batch() : 0};
+  const hlc::RecRange range{a0, m, c->rec_works[k]->as<uint32_t>(), k == 0 ? c->opt.first_batch : 0};
   const bool odd = k % 2;
   hipStream_t a = odd ? c->aux2 : c->aux;
   uint32_t* scratch = (odd ? c->rec_scratch2 : c->rec_scratch).as<uint32_t>();
@@ -1087,7 +1183,7 @@ int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, u
   hlc::launch_recover_prep(n, dbytes, sig_off, off_stride, sig_len, len_stride, c->rec_work.as<uint32_t>(), a,
                            nullptr, &range);
   hlc::launch_recover_main(n, dbytes, sig_off, off_stride, scratch, lanes, c->rec_work.as<uint32_t>(), a,
-                           c->rec_force_exact, &range);
+                           c->opt.rec_force_exact, &range);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_main[k], a));
   tr.ev("main_end_" + std::to_string(k), a);
@@ -1112,7 +1208,8 @@ int stage_rows(Staging& st, HostPool& pool, Arr* arr, int na, uint64_t a0, uint6
     const uint64_t b0 = a0 + (a1 - a0) * t / T, b1 = a0 + (a1 - a0) * (t + 1) / T;
     for (int q = 0; q < na; ++q)
       if (!arr[q].pinned && b1 > b0)
-        stage_copy(st.P + arr[q].dst + arr[q].elem * b0, arr[q].src + arr[q].elem * b0, arr[q].elem * (b1 - b0));
+        stage_copy(st.P + arr[q].dst + arr[q].elem * b0, arr[q].src + arr[q].elem * b0, arr[q].elem * (b1 - b0),
+                   st.nt);
     if (also) also(t, b0, b1);
   });
   for (int q = 0; q < na; ++q) {
@@ -1130,18 +1227,13 @@ int stage_span(Staging& st, HostPool& pool, const uint8_t* bytes, bool pinned, s
   if (pinned) return st.up_from(o_arena + lo, bytes + lo, hi - lo);
   pool.run([&](int t, int T) {
     const uint64_t d0 = lo + (hi - lo) * t / T, d1 = lo + (hi - lo) * (t + 1) / T;
-    if (d1 > d0) stage_copy(st.P + o_arena + d0, bytes + d0, d1 - d0);
+    if (d1 > d0) stage_copy(st.P + o_arena + d0, bytes + d0, d1 - d0, st.nt);
   });
   return st.up(o_arena + lo, hi - lo);
 }
 
-// Pieces the inputs other than the signatures are staged and uploaded in (HLC_REST_PIECES, default 3):
-// piece k+1 is copied into page-locked memory while piece k's DMA runs.
-int rest_pieces() {
-  const char* e = std::getenv("HLC_REST_PIECES");
-  const int k = e ? std::atoi(e) : 3;
-  return std::max(1, std::min(k, 64));
-}
+// Pieces the inputs other than the signatures are staged and uploaded in: HLC_OPT_REST_PIECES (default
+// 3): piece k+1 is copied into page-locked memory while piece k's DMA runs.
 
 // The signatures of items [a0, a1) (sig_off / sig_len with stride `stride`) gathered by the host
 // pool into the dense staging array at o_sig (65 B per item; slots of other lengths left as they
@@ -1201,9 +1293,9 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
                   hlc_result* out_res, uint8_t* out_st, uint8_t* out_rs, uint8_t* out_rec) {
   const uint64_t n = v->n;
   const uint64_t blen = v->bytes ? v->bytes_len : 0;
-  CHK(host_resources(c));
+  CHK(host_resources(c, v->bytes, blen));
   HostPool& pool = *c->pool;
-  HostTrace tr(&c->last_trace);
+  HostTrace tr(&c->last_trace, c->opt.host_trace);
   tr.start(c->copy);
   // inputs, page-locked and on the device alike: dense signatures | signature lengths | vote_id |
   // proposal_id | timestamp | vote | field_off | field_len | proposals | arena
@@ -1233,7 +1325,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   CHK(reserve_validate(c, n, np));
   std::vector<uint64_t> rb;
   CHK(prepare_ranges(c, n, rb));
-  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>(), c->opt.nt_copy && cpu_has_avx2()};
   DrainOnExit guard{st};
   const uint8_t* D = st.D;
   const int parts = pool.chunks();
@@ -1271,7 +1363,7 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
   }
   CHK(stage_rows(st, pool, &parr, 1, 0, np));
   std::vector<int> bad(parts, 0);
-  const int K = rest_pieces();
+  const int K = c->opt.rest_pieces;
   for (int k = 0; k < K; ++k) {
     const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K;
     CHK(stage_rows(st, pool, arr, 6, v0, v1, [&](int t, uint64_t b0, uint64_t b1) {
@@ -1342,9 +1434,9 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
                 const uint32_t* id_len, const uint64_t* pay_off, const uint32_t* pay_len, const uint64_t* sig_off,
                 const uint32_t* sig_len, uint8_t* out_status, uint8_t* out_addr) {
   const uint64_t blen = bytes ? bytes_len : 0;
-  CHK(host_resources(c));
+  CHK(host_resources(c, bytes, blen));
   HostPool& pool = *c->pool;
-  HostTrace tr(&c->last_trace);
+  HostTrace tr(&c->last_trace, c->opt.host_trace);
   tr.start(c->copy);
   // inputs: dense signatures | signature lengths | identity / payload lengths | identity / payload
   // offsets | arena
@@ -1366,7 +1458,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   CHK(c->kec_dig.ensure(n * 32 + 32));
   std::vector<uint64_t> rb;
   CHK(prepare_ranges(c, n, rb));
-  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>(), c->opt.nt_copy && cpu_has_avx2()};
   DrainOnExit guard{st};
   const uint8_t* D = st.D;
   const int parts = pool.chunks();
@@ -1390,7 +1482,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   for (Arr& x : arr) x.pinned = is_pinned(x.src, x.elem * n);
   const bool arena_pinned = is_pinned(bytes, blen);
   std::vector<int> bad(parts, 0);
-  const int K = rest_pieces();
+  const int K = c->opt.rest_pieces;
   for (int k = 0; k < K; ++k) {
     const uint64_t v0 = n * k / K, v1 = n * (k + 1) / K;
     CHK(stage_rows(st, pool, arr, 4, v0, v1, [&](int t, uint64_t b0, uint64_t b1) {
@@ -1425,7 +1517,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   if (daddr) HIPCHK(hipMemsetAsync(daddr, 0, n * 20, s));
   for (const RecFront& f : fronts) HIPCHK(hipStreamWaitEvent(s, f.done, 0));
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dbytes, did_off, 1,
-                             c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), dstat, daddr, s, c->rec_force_exact);
+                             c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), dstat, daddr, s, c->opt.rec_force_exact);
   HIPCHK(hipGetLastError());
   tr.ev("kernels_end", s);
   HIPCHK(hipMemcpyAsync(c->pin_out.p, ob, r2, hipMemcpyDeviceToHost, s));
@@ -1485,17 +1577,7 @@ int wire_host_plain(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const ui
 // shrinking tail (8,16,24,24,16,16,8) by 1-4%.  Messages that are out of order in the buffer only make a
 // range's prefix longer (an earlier range may then upload everything).
 void wire_ranges(const uint64_t* moff, const uint32_t* mlen, uint64_t nm, std::vector<uint64_t>& mb,
-                 std::vector<uint64_t>& ub) {
-  std::vector<uint64_t> sizes;
-  const char* e = std::getenv("HLC_WIRE_SPLIT_BYTES");
-  const char* p = e ? e : "8388608,16777216,25165824,33554432";
-  while (*p) {
-    char* end = nullptr;
-    const uint64_t x = std::strtoull(p, &end, 10);
-    if (end == p) break;
-    sizes.push_back(x);
-    p = *end == ',' ? end + 1 : end;
-  }
+                 std::vector<uint64_t>& ub, const std::vector<uint64_t>& sizes) {
   std::vector<uint64_t> pre(nm);  // prefix maximum of the message ends (empty messages read nothing)
   uint64_t hi = 0;
   for (uint64_t m = 0; m < nm; ++m) {
@@ -1520,24 +1602,16 @@ void wire_ranges(const uint64_t* moff, const uint32_t* mlen, uint64_t nm, std::v
   }
 }
 
-// Waves per recovery grid of every message range but the last (HLC_WIRE_FRONT_CAP, default 1536 of the
+// Waves per recovery grid of every message range but the last (HLC_OPT_WIRE_FRONT_CAP, default 1536 of the
 // 2,048 a full grid holds; 0 = full grids).  Two overlapping full grids hold every VGPR of the device, so
 // the next range's decode and prep wait until one drains (profiles/r05/wire_host_call_timeline.txt);
 // capped grids leave them room.  +0.5 to +2.3% from host buffers over four A/B sessions
 // (profiles/r05/ab_wire_front_cap.txt); the last range runs alone at the end and keeps the full grid.
-uint64_t wire_front_cap() {
-  const char* e = std::getenv("HLC_WIRE_FRONT_CAP");
-  return e ? (uint64_t)std::max(0LL, std::atoll(e)) : 1536;
-}
-
-// bytes per staging / upload piece of the wire host entry (HLC_WIRE_CHUNK, default 4 MiB; 8 MiB measured
-// 1-2% slower with non-temporal staging copies): piece j+1 is copied into page-locked memory while piece
-// j's DMA runs
-uint64_t wire_chunk() {
-  const char* e = std::getenv("HLC_WIRE_CHUNK");
-  const uint64_t x = e ? std::strtoull(e, nullptr, 10) : (4ull << 20);
-  return std::max<uint64_t>(x, 4096);
-}
+// (the option's value; launch_front gives a capped grid at least one block)
+//
+// Bytes per staging / upload piece of the wire host entry: HLC_OPT_WIRE_CHUNK, default 4 MiB (8 MiB
+// measured 1-2% slower with non-temporal staging copies): piece j+1 is copied into page-locked memory
+// while piece j's DMA runs.
 
 // hlc_validate_wire_proposals over host buffers, pipelined: gossip bytes go to
 // the device in message ranges (wire_ranges), and each range is decoded and its signatures recovered
@@ -1571,12 +1645,12 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
   for (uint64_t m = 0; m < nm && !plain; ++m) plain = mlen[m] > hlc::wire_huge_threshold();
   if (plain) return wire_host_plain(c, wire, wire_len, moff, mlen, nm, scope, n_scope, now, out_res, out_wire,
                                     out_n_votes);
-  CHK(host_resources(c));
+  CHK(host_resources(c, wire, wire_len));
   HostPool& pool = *c->pool;
-  HostTrace tr(&c->last_trace);
+  HostTrace tr(&c->last_trace, c->opt.host_trace);
   tr.start(c->copy);
   std::vector<uint64_t> mb, ub;
-  wire_ranges(moff, mlen, nm, mb, ub);
+  wire_ranges(moff, mlen, nm, mb, ub, c->opt.wire_split_bytes);
   const size_t R = mb.size() - 1;
   const uint64_t U = ub.back();
   // page-locked staging and its device copy: message offsets | lengths | scope configs | wire bytes
@@ -1619,7 +1693,7 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     c->ev_main.push_back(b);
   }
   while (c->rec_works.size() < R) c->rec_works.emplace_back(new DBuf());
-  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>()};
+  Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>(), c->opt.nt_copy && cpu_has_avx2()};
   DrainOnExit guard{st};
   uint8_t* D = st.D;
   const uint8_t* dwire = D + o[3];
@@ -1638,8 +1712,8 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
   std::memcpy(st.P + o[2], scope, n_scope * sizeof(hlc_scope_config));
   CHK(st.up(0, o[3]));
   const bool wire_pinned = is_pinned(wire, U);
-  const uint64_t chunk = wire_chunk();
-  const uint64_t front_cap = wire_front_cap();
+  const uint64_t chunk = c->opt.wire_chunk;
+  const uint64_t front_cap = c->opt.wire_front_cap;
   tr.fact("ranges", (double)R);
   tr.fact("front_cap_waves", (double)front_cap);
   tr.fact("wire_pinned", wire_pinned ? 1 : 0);
@@ -1660,7 +1734,8 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     hlc::launch_wire_walk(0, dwire, dmoff + m0, dmlen + m0, mk, vcount + m0, nullptr, dwout + m0, dprops + m0,
                           n_scope == 1 ? dscope : dscope + m0, n_scope, c->w_slab_off.as<uint64_t>() + m0 * slab,
                           c->w_slab_len.as<uint32_t>() + m0 * slab, c->w_big.as<uint32_t>(), nullptr, nullptr,
-                          nullptr, c->w_huge.as<uint64_t>(), ws, c->w_first_bad.as<uint32_t>() + m0);
+                          nullptr, c->w_huge.as<uint64_t>(), ws, c->w_first_bad.as<uint32_t>() + m0,
+                          c->opt.wire_walk);
     hlc::launch_wire_range_scan(vcount + m0, vbegin + m0, mk, cnt_dev + 4 * k, ws);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_cnt[k], ws));
@@ -1779,7 +1854,7 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
       } else {
         pool.run([&](int t, int T) {
           const uint64_t d0 = lo + (hi - lo) * t / T, d1 = lo + (hi - lo) * (t + 1) / T;
-          if (d1 > d0) stage_copy(st.P + o[3] + d0, wire + d0, d1 - d0);
+          if (d1 > d0) stage_copy(st.P + o[3] + d0, wire + d0, d1 - d0, st.nt);
         });
         CHK(st.up(o[3] + lo, hi - lo));
       }
@@ -1848,9 +1923,106 @@ void hlc_host_free(void* p) {
 
 int hlc_abi_version(void) { return HLC_ABI_VERSION; }
 
-int hlc_host_threads(void) { return host_threads(); }
+int hlc_host_threads(void) { return read_env().host_threads; }
 
-const char* hlc_ctx_last_host_trace(hlc_ctx* ctx) { return ctx ? ctx->last_trace.c_str() : ""; }
+const char* hlc_ctx_last_host_trace(hlc_ctx* ctx) {
+  // a copy taken under the context's lock, valid on this thread until its next call
+  thread_local std::string copy;
+  if (!ctx) return "";
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  copy = ctx->last_trace;
+  return copy.c_str();
+}
+
+int hlc_ctx_set_option(hlc_ctx* ctx, int option, int64_t value) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  Options& o = ctx->opt;
+  auto bad = [&]() { return set_err(HLC_EINVAL, "option " + std::to_string(option) + ": value " +
+                                                    std::to_string(value) + " out of range"); };
+  switch (option) {
+    case HLC_OPT_HOST_THREADS:
+      if (value < 1 || value > 64) return bad();
+      o.host_threads = (int)value;
+      break;
+    case HLC_OPT_POOL_BIND:
+      if (value < 0 || value > 2) return bad();
+      o.pool_bind = (int)value;
+      break;
+    case HLC_OPT_NT_COPY: o.nt_copy = value != 0; break;
+    case HLC_OPT_SPLIT_VOTES:
+      if (value < -1) return bad();
+      if (value == -1) o.split_votes = Options().split_votes;  // the library default
+      else o.split_votes.assign(1, (uint64_t)value);
+      break;
+    case HLC_OPT_HOST_TRACE:
+      if (value < 0 || value > 2) return bad();
+      o.host_trace = (int)value;
+      break;
+    case HLC_OPT_FIRST_BATCH:
+      if (value < 0 || value > 64) return bad();
+      o.first_batch = (int)value;
+      break;
+    case HLC_OPT_REST_PIECES:
+      if (value < 1 || value > 64) return bad();
+      o.rest_pieces = (int)value;
+      break;
+    case HLC_OPT_WIRE_SPLIT_BYTES:
+      if (value < -1) return bad();
+      if (value == -1) o.wire_split_bytes = Options().wire_split_bytes;  // the library default
+      else o.wire_split_bytes.assign(1, (uint64_t)value);
+      break;
+    case HLC_OPT_WIRE_FRONT_CAP:
+      if (value < 0) return bad();
+      o.wire_front_cap = (uint64_t)value;
+      break;
+    case HLC_OPT_SPLIT_VOTES_APPEND:
+      if (value < 0 || o.split_votes.size() >= 16) return bad();
+      o.split_votes.push_back((uint64_t)value);
+      break;
+    case HLC_OPT_WIRE_SPLIT_BYTES_APPEND:
+      if (value < 0 || o.wire_split_bytes.size() >= 16) return bad();
+      o.wire_split_bytes.push_back((uint64_t)value);
+      break;
+    case HLC_OPT_WIRE_CHUNK:
+      if (value < 4096) return bad();
+      o.wire_chunk = (uint64_t)value;
+      break;
+    case HLC_OPT_REC_FORCE_EXACT: o.rec_force_exact = value != 0; break;
+    case HLC_OPT_SERIAL_STAGES: o.serial_stages = value != 0; break;
+    case HLC_OPT_WIRE_PIPELINE: o.wire_pipeline = value != 0; break;
+    case HLC_OPT_WIRE_WALK:
+      if (value < -1 || value > 1) return bad();
+      o.wire_walk = (int)value;
+      break;
+    default: return set_err(HLC_EINVAL, "unknown option " + std::to_string(option));
+  }
+  return 0;
+}
+
+int hlc_ctx_get_option(hlc_ctx* ctx, int option, int64_t* value) {
+  if (!ctx || !value) return set_err(HLC_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const Options& o = ctx->opt;
+  switch (option) {
+    case HLC_OPT_HOST_THREADS: *value = o.host_threads; break;
+    case HLC_OPT_POOL_BIND: *value = o.pool_bind; break;
+    case HLC_OPT_NT_COPY: *value = o.nt_copy; break;
+    case HLC_OPT_SPLIT_VOTES: *value = o.split_votes.empty() ? 0 : (int64_t)o.split_votes[0]; break;
+    case HLC_OPT_HOST_TRACE: *value = o.host_trace; break;
+    case HLC_OPT_FIRST_BATCH: *value = o.first_batch; break;
+    case HLC_OPT_REST_PIECES: *value = o.rest_pieces; break;
+    case HLC_OPT_WIRE_SPLIT_BYTES: *value = o.wire_split_bytes.empty() ? 0 : (int64_t)o.wire_split_bytes[0]; break;
+    case HLC_OPT_WIRE_FRONT_CAP: *value = (int64_t)o.wire_front_cap; break;
+    case HLC_OPT_WIRE_CHUNK: *value = (int64_t)o.wire_chunk; break;
+    case HLC_OPT_REC_FORCE_EXACT: *value = o.rec_force_exact; break;
+    case HLC_OPT_SERIAL_STAGES: *value = o.serial_stages; break;
+    case HLC_OPT_WIRE_PIPELINE: *value = o.wire_pipeline; break;
+    case HLC_OPT_WIRE_WALK: *value = o.wire_walk; break;
+    default: return set_err(HLC_EINVAL, "unknown option " + std::to_string(option));
+  }
+  return 0;
+}
 
 int hlc_ctx_create(int device, hlc_ctx** out) {
   if (!out) return set_err(HLC_EINVAL, "out is NULL");
@@ -1864,8 +2036,7 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
     return set_err(HLC_ENODEV, std::string("libhlc is built for gfx950, device is ") + prop.gcnArchName);
   hlc_ctx* c = new hlc_ctx();
   c->device = device;
-  if (const char* fx = std::getenv("HLC_REC_FORCE_EXACT")) c->rec_force_exact = std::atoi(fx) != 0;
-  if (const char* ss = std::getenv("HLC_SERIAL_STAGES")) c->serial_stages = std::atoi(ss) != 0;
+  c->opt = read_env();  // the options' defaults: the environment, read here only
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       create_aux(c) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -2137,7 +2308,7 @@ int hlc_validate_wire_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire
   CHK(check_wire_host(wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope));
   std::lock_guard<std::mutex> lk(ctx->mu);
   CHK(activate(ctx));
-  if (const char* e = std::getenv("HLC_WIRE_PIPELINE"); e && std::atoi(e) == 0)  // A/B arm: unpipelined
+  if (!ctx->opt.wire_pipeline)  // A/B arm: unpipelined
     return wire_host_plain(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, now, out_results, out_wire,
                            out_n_votes);
   return validate_wire_host(ctx, wire, wire_len, msg_off, msg_len, n_msgs, scope, n_scope, now, out_results, out_wire,
@@ -2149,9 +2320,13 @@ int hlc_validate_wire_proposals(hlc_ctx* ctx, const uint8_t* wire, uint64_t wire
 namespace {
 
 // process_incoming_vote over device-resident inputs (see hlc_process_votes); outputs on device.
+// (owner_off != nullptr: owners is an arena of any-length identities; verdicts != nullptr: the scheme step
+// is the caller's, hlc_process_votes_verdicts)
 int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vsess, hlc_session* dss,
                          uint64_t n_sessions, const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
-                         uint64_t now, uint8_t* st, uint8_t* tr, uint8_t* ins, uint8_t* reason, hipStream_t s) {
+                         uint64_t now, uint8_t* st, uint8_t* tr, uint8_t* ins, uint8_t* reason, hipStream_t s,
+                         const uint64_t* owner_off = nullptr, const uint32_t* owner_len = nullptr,
+                         const uint8_t* verdicts = nullptr) {
   const uint64_t n = dv->n;
   CHK(ctx->s_props.ensure(n_sessions * sizeof(hlc_proposal) + 16));
   hlc_proposal* dprops = ctx->s_props.as<hlc_proposal>();
@@ -2165,7 +2340,9 @@ int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vses
   }
   CHK(ctx->flag.ensure(16));
   HIPCHK(hipMemsetAsync(ctx->flag.p, 0, sizeof(uint32_t), s));
-  if (n) CHK(vote_stage(ctx, dv, vsess, dprops, n_sessions, now, ctx->status.as<uint8_t>(), rs, nullptr, nullptr, nullptr, s));
+  if (n)
+    CHK(vote_stage(ctx, dv, vsess, dprops, n_sessions, now, ctx->status.as<uint8_t>(), rs, nullptr, nullptr, nullptr, s,
+                   nullptr, 0, 0, verdicts));
   // 2. each session's votes in delivery order
   CHK(ctx->s_keys.ensure(n * 4 + 4));
   CHK(ctx->s_iota.ensure(n * 4 + 4));
@@ -2191,7 +2368,7 @@ int process_votes_device(hlc_ctx* ctx, const hlc_votes* dv, const uint32_t* vses
   hlc::launch_stream_init(n, vsess, ctx->status.as<uint8_t>(), st, tr, ins, s);
   uint32_t* tab = ctx->s_tab.as<uint32_t>();
   hlc::launch_dup_flags(tab, tab + cap, (uint32_t)(cap - 1), owners, owner_session, n_owners, dv, vsess, st,
-                        ctx->s_slot.as<uint32_t>(), ctx->s_dup.as<uint8_t>(), s);
+                        ctx->s_slot.as<uint32_t>(), ctx->s_dup.as<uint8_t>(), s, owner_off, owner_len);
   hlc::launch_apply_votes(dss, n_sessions, ctx->s_segb.as<uint32_t>(), ctx->s_sege.as<uint32_t>(),
                           ctx->s_order.as<uint32_t>(), dv, now, ctx->s_dup.as<uint8_t>(), st, tr, ins, s);
   HIPCHK(hipGetLastError());
@@ -2261,6 +2438,149 @@ int hlc_process_votes(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote
     HIPCHK(hipMemcpyAsync(sessions, dss, n_sessions * sizeof(hlc_session), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return 0;
+}
+
+int hlc_process_votes_verdicts(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote_session,
+                               hlc_session* sessions, uint64_t n_sessions, const uint8_t* owner_bytes,
+                               uint64_t owner_bytes_len, const uint64_t* owner_off, const uint32_t* owner_len,
+                               const uint32_t* owner_session, uint64_t n_owners, uint64_t now, const uint8_t* verdicts,
+                               uint8_t* out_status, uint8_t* out_transition, uint8_t* out_inserted,
+                               uint8_t* out_reason) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  CHK(check_votes_host(votes));
+  const uint64_t n = votes->n;
+  if (n && (!vote_session || !out_status || !out_transition || !out_inserted || !verdicts))
+    return set_err(HLC_EINVAL, "NULL vote_session / verdicts / output array");
+  if (n_sessions && !sessions) return set_err(HLC_EINVAL, "sessions is NULL");
+  if (n_owners && (!owner_off || !owner_len || !owner_session)) return set_err(HLC_EINVAL, "NULL owner arrays");
+  if (n_sessions >= hlc::NO_PROP || n + n_owners > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "batch too large");
+  CHK(check_verdicts(verdicts, n));
+  for (uint64_t i = 0; i < n; ++i)
+    if (vote_session[i] != hlc::NO_PROP && vote_session[i] >= n_sessions)
+      return set_err(HLC_EINVAL, "vote_session index out of range");
+  for (uint64_t k = 0; k < n_owners; ++k) {
+    if (owner_session[k] >= n_sessions) return set_err(HLC_EINVAL, "owner_session index out of range");
+    if (owner_len[k] && (!owner_bytes || owner_off[k] + owner_len[k] > owner_bytes_len ||
+                         owner_off[k] + owner_len[k] < owner_off[k]))
+      return set_err(HLC_EINVAL, "owner (offset, length) outside owner_bytes");
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  hlc_votes dv;
+  CHK(stage_votes(ctx, votes, &dv, s));
+  CHK(upload(ctx->s_vsess, vote_session, n, s));
+  CHK(upload(ctx->s_sessions, sessions, n_sessions, s));
+  CHK(upload(ctx->s_owners, owner_bytes, owner_bytes ? owner_bytes_len : 0, s));
+  CHK(upload(ctx->in_off3, owner_off, n_owners, s));
+  CHK(upload(ctx->in_len3, owner_len, n_owners, s));
+  CHK(upload(ctx->s_osess, owner_session, n_owners, s));
+  CHK(upload(ctx->in_verdict, verdicts, n, s));
+  CHK(ctx->s_st.ensure(n + 1));
+  CHK(ctx->s_tr.ensure(n + 1));
+  CHK(ctx->s_ins.ensure(n + 1));
+  CHK(ctx->reason.ensure(n + 1));
+  hlc_session* dss = ctx->s_sessions.as<hlc_session>();
+  CHK(process_votes_device(ctx, &dv, ctx->s_vsess.as<uint32_t>(), dss, n_sessions, ctx->s_owners.as<uint8_t>(),
+                           ctx->s_osess.as<uint32_t>(), n_owners, now, ctx->s_st.as<uint8_t>(), ctx->s_tr.as<uint8_t>(),
+                           ctx->s_ins.as<uint8_t>(), ctx->reason.as<uint8_t>(), s, ctx->in_off3.as<uint64_t>(),
+                           ctx->in_len3.as<uint32_t>(), ctx->in_verdict.as<uint8_t>()));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(out_status, ctx->s_st.p, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_transition, ctx->s_tr.p, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out_inserted, ctx->s_ins.p, n, hipMemcpyDeviceToHost, s));
+    if (out_reason) HIPCHK(hipMemcpyAsync(out_reason, ctx->reason.p, n, hipMemcpyDeviceToHost, s));
+  }
+  if (n_sessions)
+    HIPCHK(hipMemcpyAsync(sessions, dss, n_sessions * sizeof(hlc_session), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hlc_validate_proposals_verdicts_device(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,
+                                           uint64_t n_proposals, uint64_t now, const uint8_t* verdicts,
+                                           hlc_result* out_results, uint8_t* out_vote_status,
+                                           uint8_t* out_vote_reason, void* stream) {
+  if (!ctx || !votes || (votes->n && !verdicts) || (n_proposals && (!proposals || !out_results)))
+    return set_err(HLC_EINVAL, "NULL argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+  return validate_device(ctx, votes, proposals, n_proposals, now, out_results, out_vote_status, out_vote_reason,
+                         nullptr, s, nullptr, 0, 0, verdicts);
+}
+
+int hlc_validate_proposals_verdicts(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,
+                                    uint64_t n_proposals, uint64_t now, const uint8_t* verdicts,
+                                    hlc_result* out_results, uint8_t* out_vote_status, uint8_t* out_vote_reason) {
+  if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
+  CHK(check_votes_host(votes));
+  const uint64_t n = votes->n;
+  if (n && !verdicts) return set_err(HLC_EINVAL, "verdicts is NULL");
+  if (n_proposals && (!proposals || !out_results)) return set_err(HLC_EINVAL, "NULL proposals/results");
+  for (uint64_t p = 0; p < n_proposals; ++p) {
+    if (proposals[p].vote_begin + proposals[p].vote_count > n ||
+        proposals[p].vote_begin + proposals[p].vote_count < proposals[p].vote_begin)
+      return set_err(HLC_EINVAL, "proposal vote range outside the vote batch");
+  }
+  if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
+  CHK(check_verdicts(verdicts, n));
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  hlc_votes dv;
+  CHK(stage_votes(ctx, votes, &dv, s));
+  CHK(upload(ctx->in_props, proposals, n_proposals, s));
+  CHK(upload(ctx->in_verdict, verdicts, n, s));
+  CHK(ctx->out_res.ensure(n_proposals * sizeof(hlc_result) + 16));
+  CHK(ctx->out_status.ensure(n + 1));
+  CHK(ctx->out_reason.ensure(n + 1));
+  CHK(validate_device(ctx, &dv, ctx->in_props.as<hlc_proposal>(), n_proposals, now, ctx->out_res.as<hlc_result>(),
+                      ctx->out_status.as<uint8_t>(), ctx->out_reason.as<uint8_t>(), nullptr, s, nullptr, 0, 0,
+                      ctx->in_verdict.as<uint8_t>()));
+  if (n_proposals)
+    HIPCHK(hipMemcpyAsync(out_results, ctx->out_res.p, n_proposals * sizeof(hlc_result), hipMemcpyDeviceToHost, s));
+  if (n && out_vote_status) HIPCHK(hipMemcpyAsync(out_vote_status, ctx->out_status.p, n, hipMemcpyDeviceToHost, s));
+  if (n && out_vote_reason) HIPCHK(hipMemcpyAsync(out_vote_reason, ctx->out_reason.p, n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+int hlc_encode_vote_payloads(hlc_ctx* ctx, const hlc_votes* votes, uint64_t* out_off, uint32_t* out_len,
+                             uint8_t* out_bytes, uint64_t cap, uint64_t* out_total) {
+  if (!ctx || !out_total) return set_err(HLC_EINVAL, "NULL argument");
+  CHK(check_votes_host(votes));
+  const uint64_t n = votes->n;
+  if (n && (!out_off || !out_len)) return set_err(HLC_EINVAL, "NULL out_off / out_len");
+  if (n > 0x7FFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^31-16)");
+  *out_total = 0;
+  if (!n) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  CHK(activate(ctx));
+  hipStream_t s = ctx->stream;
+  hlc_votes dv;
+  CHK(stage_votes(ctx, votes, &dv, s));
+  CHK(ctx->kec_sz.ensure(n * 8));
+  CHK(ctx->kec_off.ensure(n * 8));
+  CHK(ctx->out_misc.ensure(n * 4 + 16));
+  hlc::launch_payload_sizes(&dv, n, ctx->kec_sz.as<uint64_t>(), ctx->out_misc.as<uint32_t>(), s);
+  HIPCHK(hipGetLastError());
+  uint64_t total = 0;
+  CHK(scan_sizes(ctx, n, ctx->kec_sz.as<uint64_t>(), ctx->kec_off.as<uint64_t>(), &total, s));  // (synchronises)
+  *out_total = total;
+  HIPCHK(hipMemcpyAsync(out_off, ctx->kec_off.p, n * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(out_len, ctx->out_misc.p, n * 4, hipMemcpyDeviceToHost, s));
+  int rc = 0;
+  if (out_bytes && total > cap) {
+    rc = set_err(HLC_ERANGE, "payload capacity too small: " + std::to_string(total) + " bytes needed");
+  } else if (out_bytes && total) {
+    CHK(ctx->kec_buf.ensure(total + 16));
+    hlc::launch_encode_payloads(&dv, n, ctx->kec_off.as<uint64_t>(), ctx->kec_buf.as<uint8_t>(), s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out_bytes, ctx->kec_buf.p, total, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  return rc;
 }
 
 int hlc_compute_vote_hashes(hlc_ctx* ctx, const hlc_votes* votes, uint8_t* out_hash32) {

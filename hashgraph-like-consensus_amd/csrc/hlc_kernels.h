@@ -48,13 +48,20 @@ void launch_verify_prehash(uint64_t n, const uint8_t* bytes, const uint64_t* pay
                            uint8_t* verify_out, hipStream_t s);
 // fused byte stage (sizes + SHA-256 compare + EIP-191 keccak + pre-status) for votes whose
 // messages fit the per-lane LDS window; others get PRE_GENERAL and *general is set non-zero
+// eth == false (a caller-side scheme, the *_verdicts entries): no Ethereum length checks and no EIP-191
+// keccak -- every vote that passes the vote-hash compare becomes PRE_PENDING for the caller's verdict
 void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                          uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason, uint32_t* general, hipStream_t s);
+                          uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason, uint32_t* general, hipStream_t s,
+                          bool eth = true);
 // general path without host round trips: streams the PRE_GENERAL votes' messages from the arena
 // (SHA-256 compare + EIP-191 keccak + pre-status); exits at once unless *flags has FLAG_GENERAL_PATH
 void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                            const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason,
-                           hipStream_t s);
+                           hipStream_t s, bool eth = true);
+// the scheme payload of every vote (utils.rs:150-152: prost encoding, signature cleared): sizes (u64 for
+// the scan and u32 for the caller), then the bytes at the scanned offsets
+void launch_payload_sizes(const hlc_votes* v, uint64_t n, uint64_t* sz64, uint32_t* sz32, hipStream_t s);
+void launch_encode_payloads(const hlc_votes* v, uint64_t n, const uint64_t* off, uint8_t* out, hipStream_t s);
 // general-path pre-status: decides only the votes marked PRE_GENERAL
 void launch_pre_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                        const uint32_t* sha_digest, uint8_t* pre, uint8_t* pre_reason, hipStream_t s);
@@ -142,7 +149,8 @@ void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, co
                       uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout, hlc_proposal* pout,
                       const hlc_scope_config* scope, uint64_t n_scope, uint64_t* slab_off, uint32_t* slab_len,
                       uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, uint64_t* huge,
-                      hipStream_t s, uint32_t* first_bad = nullptr);  // mode 0: first_bad[m] = ~0 when given
+                      hipStream_t s, uint32_t* first_bad = nullptr,  // mode 0: first_bad[m] = ~0 when given
+                      int walk = -1);  // HLC_OPT_WIRE_WALK: -1 the build's default walker, 0 per lane, 1 LDS
 // Messages longer than wire_huge_threshold() are skipped by the walker (mode 0 appends (m, len) to
 // huge[1..], count in huge[0]) and decoded by launch_huge_decode: parallel field-boundary discovery
 // (next[] per byte offset + pointer jumping), records into hoff/hlen in stream order, then
@@ -190,10 +198,13 @@ void launch_sessions_to_props(const hlc_session* ss, uint64_t m, hlc_proposal* p
 hipError_t launch_sort_by_session(const uint32_t* vote_session, uint64_t n, uint32_t* keys_out, uint32_t* iota,
                             uint32_t* order, void* temp, size_t& temp_bytes, hipStream_t s);
 void launch_segments(const uint32_t* keys, uint64_t n, uint32_t* seg_begin, uint32_t* seg_end, hipStream_t s);
-// duplicate flags: tab (pre-set to ~0), minv (pre-set to ~0) sized mask + 1; slot_of[n], dup[n]
+// duplicate flags: tab (pre-set to ~0), minv (pre-set to ~0) sized mask + 1; slot_of[n], dup[n].
+// Existing owner k: owner_off == nullptr -> owners[20 k .. + 20] (hlc_process_votes); else
+// owners[owner_off[k] .. + owner_len[k]] (any identity length, hlc_process_votes_verdicts)
 void launch_dup_flags(uint32_t* tab, uint32_t* minv, uint32_t mask, const uint8_t* owners,
                       const uint32_t* owner_session, uint64_t n_owners, const hlc_votes* v, const uint32_t* vote_session,
-                      const uint8_t* st, uint32_t* slot_of, uint8_t* dup, hipStream_t s);
+                      const uint8_t* st, uint32_t* slot_of, uint8_t* dup, hipStream_t s,
+                      const uint64_t* owner_off = nullptr, const uint32_t* owner_len = nullptr);
 void launch_stream_init(uint64_t n, const uint32_t* vote_session, const uint8_t* vstatus, uint8_t* st, uint8_t* tr,
                         uint8_t* ins, hipStream_t s);
 void launch_apply_votes(hlc_session* ss, uint64_t m, const uint32_t* seg_begin, const uint32_t* seg_end,

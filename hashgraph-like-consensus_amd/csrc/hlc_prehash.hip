@@ -280,7 +280,7 @@ __global__ void k_vote_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop
     uint64_t ts = v.timestamp[i];
     if (vr >= 2) {
       st = HLC_SIGNATURE_SCHEME;
-      rs = vr - 1;
+      rs = min(vr - 1, HLC_SCHEME_PLUGIN);  // (a caller's verdict above HLC_VERIFY_ERR reads as it)
     } else if (vr == HLC_VERIFY_FALSE) {
       st = HLC_INVALID_VOTE_SIGNATURE;
     } else if (ts < p.timestamp) {
@@ -698,6 +698,9 @@ struct LdsCursor {
   }
 };
 
+// ETH == false (a caller-side scheme's verdicts, hlc_validate_proposals_verdicts): the scheme's own checks
+// (ethereum.rs:71-82) and the EIP-191 keccak are not this engine's: a vote whose hash matches is PRE_PENDING
+template <bool ETH>
 __global__ void __launch_bounds__(FUSED_TPB) k_prehash_fused(hlc_votes v, uint64_t n, const uint32_t* vote_prop,
                                                              const hlc_proposal* props, uint32_t* kec_dig,
                                                              uint8_t* pre, uint8_t* pre_reason, uint32_t* general) {
@@ -725,7 +728,7 @@ __global__ void __launch_bounds__(FUSED_TPB) k_prehash_fused(hlc_votes v, uint64
     const uint64_t el = vote_enc_len(v, i);
     const uint64_t kec_len = 26 + dec_digits(el) + el;
     const uint64_t kec_sz = (kec_len / 136 + 1) * 136;
-    if (sha_sz > FBUF || kec_sz > FBUF) {
+    if (sha_sz > FBUF || (ETH && kec_sz > FBUF)) {
       pre[i] = PRE_GENERAL;
       pre_reason[i] = 0;
       atomicOr(general, FLAG_GENERAL_PATH);
@@ -769,6 +772,8 @@ __global__ void __launch_bounds__(FUSED_TPB) k_prehash_fused(hlc_votes v, uint64
     }
     if (!eq) {
       st = HLC_INVALID_VOTE_HASH;
+    } else if (!ETH) {
+      // the caller's scheme decides the signature step (st stays PRE_PENDING)
     } else if (ls != 65) {
       st = HLC_SIGNATURE_SCHEME;
       rs = HLC_SCHEME_SIG_LEN;
@@ -910,7 +915,8 @@ struct SegStream {
 };
 
 __global__ void k_prehash_stream(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                                 const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason) {
+                                 const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason,
+                                 bool eth) {
   if (!(*flags & FLAG_GENERAL_PATH)) return;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -965,6 +971,8 @@ __global__ void k_prehash_stream(hlc_votes v, uint64_t n, const uint32_t* vote_p
     }
     if (!eq) {
       st = HLC_INVALID_VOTE_HASH;
+    } else if (!eth) {
+      // the caller's scheme decides the signature step (st stays PRE_PENDING)
     } else if (ls != 65) {
       st = HLC_SIGNATURE_SCHEME;
       rs = HLC_SCHEME_SIG_LEN;
@@ -1104,6 +1112,36 @@ __global__ void k_verify_prehash(uint64_t n, const uint8_t* bytes, const uint64_
   }
 }
 
+// The payload `Signer::verify` gets for a vote (utils.rs:150-152): the prost encoding of the Vote with
+// its signature cleared (consensus.proto:19-29), for a caller-side scheme (hlc_encode_vote_payloads).
+// One lane per vote; sizes first, the bytes at the scanned offsets after.
+__global__ void k_payload_sizes(hlc_votes v, uint64_t n, uint64_t* sz64, uint32_t* sz32) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t e = vote_enc_len(v, i);
+  sz64[i] = e;
+  sz32[i] = (uint32_t)e;
+}
+
+__global__ void k_encode_payloads(hlc_votes v, uint64_t n, const uint64_t* off, uint8_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Cursor c{out + off[i], 0};
+  const uint32_t id = v.vote_id[i], pid = v.proposal_id[i];
+  const uint64_t ts = v.timestamp[i];
+  if (id) { c.put(0xA0); c.put(0x01); c.put_varint(id); }
+  const uint32_t lo = flen(v, i, HLC_F_OWNER);
+  if (lo) { c.put(0xAA); c.put(0x01); c.put_varint(lo); c.put_bytes(fptr(v, i, HLC_F_OWNER), lo); }
+  if (pid) { c.put(0xB0); c.put(0x01); c.put_varint(pid); }
+  if (ts) { c.put(0xB8); c.put(0x01); c.put_varint(ts); }
+  if (v.vote[i]) { c.put(0xC0); c.put(0x01); c.put(0x01); }
+  const uint8_t keys[3] = {0xCA, 0xD2, 0xDA};
+  for (int f = HLC_F_PARENT; f <= HLC_F_VOTE_HASH; ++f) {
+    const uint32_t l = flen(v, i, f);
+    if (l) { c.put(keys[f - HLC_F_PARENT]); c.put(0x01); c.put_varint(l); c.put_bytes(fptr(v, i, f), l); }
+  }
+}
+
 inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB); }
 
 }  // namespace
@@ -1122,10 +1160,24 @@ hipError_t launch_exclusive_scan(const uint64_t* in, uint64_t* out, uint64_t n, 
 }
 
 void launch_prehash_fused(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                          uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason, uint32_t* general, hipStream_t s) {
-  if (n)
-    hipLaunchKernelGGL(k_prehash_fused, dim3((unsigned)((n + FUSED_TPB - 1) / FUSED_TPB)), dim3(FUSED_TPB), 0, s, *v,
-                       n, vote_prop, props, kec_dig, pre, pre_reason, general);
+                          uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason, uint32_t* general, hipStream_t s,
+                          bool eth) {
+  if (!n) return;
+  const dim3 grid((unsigned)((n + FUSED_TPB - 1) / FUSED_TPB));
+  if (eth)
+    hipLaunchKernelGGL(k_prehash_fused<true>, grid, dim3(FUSED_TPB), 0, s, *v, n, vote_prop, props, kec_dig, pre,
+                       pre_reason, general);
+  else
+    hipLaunchKernelGGL(k_prehash_fused<false>, grid, dim3(FUSED_TPB), 0, s, *v, n, vote_prop, props, kec_dig, pre,
+                       pre_reason, general);
+}
+
+void launch_payload_sizes(const hlc_votes* v, uint64_t n, uint64_t* sz64, uint32_t* sz32, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_payload_sizes, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, sz64, sz32);
+}
+
+void launch_encode_payloads(const hlc_votes* v, uint64_t n, const uint64_t* off, uint8_t* out, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_encode_payloads, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, off, out);
 }
 
 
@@ -1207,13 +1259,13 @@ void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, co
 
 void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                            const uint32_t* flags, uint32_t* kec_dig, uint8_t* pre, uint8_t* pre_reason,
-                           hipStream_t s) {
+                           hipStream_t s, bool eth) {
   if (!n) return;
   // one block per CU at most: the grid exits at once unless k_prehash_fused deferred a vote (rare),
   // and a small grid keeps the queued no-op from occupying the dispatcher behind k_rec_main
   const unsigned blocks = (unsigned)std::min<uint64_t>(blocks_for(n), 256);
   hipLaunchKernelGGL(k_prehash_stream, dim3(blocks), dim3(TPB), 0, s, *v, n, vote_prop, props, flags, kec_dig, pre,
-                     pre_reason);
+                     pre_reason, eth);
 }
 
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,

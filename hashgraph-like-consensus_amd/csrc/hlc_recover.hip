@@ -490,6 +490,7 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (m + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
+  if (blocks == 0) blocks = 1;  // a capped grid (HLC_OPT_WIRE_FRONT_CAP below one block) still runs
   if (clk_waves) *clk_waves = blocks * (REC_TPB / 64);
   hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, f.st, bytes, sig_off, off_stride,
                      scratch, (uint64_t)blocks * REC_TPB, f.b.rec, f.b.q, f.b.mst, force_exact, f.b.ctr, f.b.list,

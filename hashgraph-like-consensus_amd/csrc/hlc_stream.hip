@@ -29,13 +29,24 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-__device__ __forceinline__ uint32_t owner_hash(uint32_t session, const uint8_t* owner) {
+// (session, owner) key hash: word-wise for 20-byte addresses (EthereumConsensusSigner identities),
+// byte-wise for any other identity length (a caller-side scheme, hlc_process_votes_verdicts)
+__device__ __forceinline__ uint32_t owner_hash(uint32_t session, const uint8_t* owner, uint32_t len) {
   uint32_t h = 0x9E3779B9u ^ session * 0x85EBCA6Bu;
+  if (len == 20) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    h ^= ld_le32(owner + 4 * k) * 0xCC9E2D51u;
-    h = (h << 13) | (h >> 19);
-    h = h * 5u + 0xE6546B64u;
+    for (int k = 0; k < 5; ++k) {
+      h ^= ld_le32(owner + 4 * k) * 0xCC9E2D51u;
+      h = (h << 13) | (h >> 19);
+      h = h * 5u + 0xE6546B64u;
+    }
+  } else {
+    h ^= len * 0x27D4EB2Fu;
+    for (uint32_t k = 0; k < len; ++k) {
+      h ^= (uint32_t)owner[k] * 0xCC9E2D51u;
+      h = (h << 13) | (h >> 19);
+      h = h * 5u + 0xE6546B64u;
+    }
   }
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -44,47 +55,67 @@ __device__ __forceinline__ uint32_t owner_hash(uint32_t session, const uint8_t* 
 }
 
 struct OwnerKeys {
-  const uint8_t* owners;          // existing owners, 20 B each
+  const uint8_t* owners;          // existing owners: 20 B rows, or an arena indexed by owner_off / owner_len
+  const uint64_t* owner_off;      // nullptr: 20-byte rows
+  const uint32_t* owner_len;
   const uint32_t* owner_session;  // their sessions
   uint64_t n_owners;
   const uint8_t* bytes;           // vote arena
   const uint64_t* field_off;      // [n][HLC_NFIELDS]
+  const uint32_t* field_len;      // [n][HLC_NFIELDS]
   const uint32_t* vote_session;   // [n]
 };
 
-__device__ __forceinline__ void key_of(const OwnerKeys& k, uint32_t ref, uint32_t& session, const uint8_t*& owner) {
+__device__ __forceinline__ void existing_owner(const OwnerKeys& k, uint64_t r, const uint8_t*& owner, uint32_t& len) {
+  if (k.owner_off) {
+    owner = k.owners + k.owner_off[r];
+    len = k.owner_len[r];
+  } else {
+    owner = k.owners + 20ull * r;
+    len = 20;
+  }
+}
+
+__device__ __forceinline__ void key_of(const OwnerKeys& k, uint32_t ref, uint32_t& session, const uint8_t*& owner,
+                                       uint32_t& len) {
   if (ref < k.n_owners) {
     session = k.owner_session[ref];
-    owner = k.owners + 20ull * ref;
+    existing_owner(k, ref, owner, len);
   } else {
     const uint64_t v = ref - k.n_owners;
     session = k.vote_session[v];
     owner = k.bytes + k.field_off[v * HLC_NFIELDS + HLC_F_OWNER];
+    len = k.field_len[v * HLC_NFIELDS + HLC_F_OWNER];
   }
 }
 
-__device__ __forceinline__ bool same_owner(const uint8_t* a, const uint8_t* b) {
+__device__ __forceinline__ bool same_owner(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+  if (al != bl) return false;
   uint32_t d = 0;
+  if (al == 20) {
 #pragma unroll
-  for (int k = 0; k < 20; ++k) d |= (uint32_t)(a[k] ^ b[k]);
+    for (int k = 0; k < 20; ++k) d |= (uint32_t)(a[k] ^ b[k]);
+  } else {
+    for (uint32_t k = 0; k < al; ++k) d |= (uint32_t)(a[k] ^ b[k]);
+  }
   return d == 0;
 }
 
 // Slot of key (session, owner), claiming an empty one with `ref` when the key is absent.
 // Slots are never deleted, so every lane re-finds a key another lane inserted.
 __device__ uint32_t key_slot(uint32_t* tab, uint32_t mask, const OwnerKeys& k, uint32_t session,
-                             const uint8_t* owner, uint32_t ref) {
-  uint32_t slot = owner_hash(session, owner) & mask;
+                             const uint8_t* owner, uint32_t len, uint32_t ref) {
+  uint32_t slot = owner_hash(session, owner, len) & mask;
   for (;;) {
     uint32_t cur = __hip_atomic_load(tab + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == EMPTY) {
       cur = atomicCAS(tab + slot, EMPTY, ref);
       if (cur == EMPTY) return slot;
     }
-    uint32_t s2;
+    uint32_t s2, l2;
     const uint8_t* o2;
-    key_of(k, cur, s2, o2);
-    if (s2 == session && same_owner(o2, owner)) return slot;
+    key_of(k, cur, s2, o2, l2);
+    if (s2 == session && same_owner(o2, l2, owner, len)) return slot;
     slot = (slot + 1) & mask;
   }
 }
@@ -134,7 +165,10 @@ __global__ void __launch_bounds__(TPB) k_segments(const uint32_t* __restrict__ k
 __global__ void __launch_bounds__(TPB) k_owner_insert(uint32_t* tab, uint32_t* minv, uint32_t mask, OwnerKeys k) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= k.n_owners) return;
-  const uint32_t slot = key_slot(tab, mask, k, k.owner_session[r], k.owners + 20ull * r, (uint32_t)r);
+  const uint8_t* owner;
+  uint32_t len;
+  existing_owner(k, r, owner, len);
+  const uint32_t slot = key_slot(tab, mask, k, k.owner_session[r], owner, len, (uint32_t)r);
   atomicMin(minv + slot, 0u);
 }
 
@@ -144,7 +178,8 @@ __global__ void __launch_bounds__(TPB) k_vote_owner_insert(uint64_t n, const uin
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || st[i] != HLC_OK) return;  // only votes that passed validate_vote reach add_vote
   const uint8_t* owner = k.bytes + k.field_off[i * HLC_NFIELDS + HLC_F_OWNER];
-  const uint32_t slot = key_slot(tab, mask, k, k.vote_session[i], owner, (uint32_t)(k.n_owners + i));
+  const uint32_t len = k.field_len[i * HLC_NFIELDS + HLC_F_OWNER];
+  const uint32_t slot = key_slot(tab, mask, k, k.vote_session[i], owner, len, (uint32_t)(k.n_owners + i));
   atomicMin(minv + slot, (uint32_t)(i + 1));
   slot_of[i] = slot;
 }
@@ -257,9 +292,13 @@ void launch_segments(const uint32_t* keys, uint64_t n, uint32_t* seg_begin, uint
 }
 
 static OwnerKeys owner_keys(const uint8_t* owners, const uint32_t* owner_session, uint64_t n_owners,
-                            const hlc_votes* v, const uint32_t* vote_session) {
+                            const hlc_votes* v, const uint32_t* vote_session, const uint64_t* owner_off,
+                            const uint32_t* owner_len) {
   OwnerKeys k;
   k.owners = owners;
+  k.owner_off = owner_off;
+  k.owner_len = owner_len;
+  k.field_len = v->field_len;
   k.owner_session = owner_session;
   k.n_owners = n_owners;
   k.bytes = v->bytes;
@@ -270,8 +309,9 @@ static OwnerKeys owner_keys(const uint8_t* owners, const uint32_t* owner_session
 
 void launch_dup_flags(uint32_t* tab, uint32_t* minv, uint32_t mask, const uint8_t* owners,
                       const uint32_t* owner_session, uint64_t n_owners, const hlc_votes* v, const uint32_t* vote_session,
-                      const uint8_t* st, uint32_t* slot_of, uint8_t* dup, hipStream_t s) {
-  const OwnerKeys k = owner_keys(owners, owner_session, n_owners, v, vote_session);
+                      const uint8_t* st, uint32_t* slot_of, uint8_t* dup, hipStream_t s, const uint64_t* owner_off,
+                      const uint32_t* owner_len) {
+  const OwnerKeys k = owner_keys(owners, owner_session, n_owners, v, vote_session, owner_off, owner_len);
   if (n_owners) hipLaunchKernelGGL(k_owner_insert, dim3(blocks_for(n_owners)), dim3(TPB), 0, s, tab, minv, mask, k);
   const uint64_t n = v->n;
   if (!n) return;

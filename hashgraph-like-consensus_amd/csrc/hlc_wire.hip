@@ -959,19 +959,16 @@ inline unsigned blocks_for(uint64_t n) { return (unsigned)((n + TPB - 1) / TPB);
 
 static int is_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// the mode-0 walker (HLC_WIRE_WALK: "lds" = k_wire_walk_lds, "lane" = k_wire_walk; default below)
-static bool walk_lds() {
-  const char* e = std::getenv("HLC_WIRE_WALK");
-  return e ? std::strcmp(e, "lane") != 0 : WIRE_WALK_LDS_DEFAULT;
-}
+// the mode-0 walker (HLC_OPT_WIRE_WALK: 1 = k_wire_walk_lds, 0 = k_wire_walk, -1 = the default below)
+static bool walk_lds(int walk) { return walk < 0 ? WIRE_WALK_LDS_DEFAULT : walk != 0; }
 
 void launch_wire_walk(int mode, const uint8_t* wire, const uint64_t* msg_off, const uint32_t* msg_len, uint64_t nm,
                       uint64_t* vote_count, const uint64_t* vote_begin, hlc_wire_proposal* wout, hlc_proposal* pout,
                       const hlc_scope_config* scope, uint64_t n_scope, uint64_t* slab_off, uint32_t* slab_len,
                       uint32_t* big, uint64_t* vrec_off, uint32_t* vrec_len, uint32_t* vrec_msg, uint64_t* huge,
-                      hipStream_t s, uint32_t* first_bad) {
+                      hipStream_t s, uint32_t* first_bad, int walk) {
   if (!nm) return;
-  if (mode == 0 && walk_lds()) {
+  if (mode == 0 && walk_lds(walk)) {
     hipLaunchKernelGGL(k_wire_walk_lds, dim3((unsigned)((nm + LW_MPW - 1) / LW_MPW)), dim3(64), 0, s, wire,
                        is_aligned16(wire), msg_off, msg_len, nm, vote_count, wout, pout, scope, n_scope, slab_off,
                        slab_len, big, huge, first_bad);

@@ -137,7 +137,23 @@ EXPORTED_SYMBOLS = (
     "hlc_process_votes", "hlc_process_votes_device", "hlc_synth_arena_bytes", "hlc_synth_votes_device",
     "hlc_synth_byzantine_device", "hlc_outcome_counts_device", "hlc_host_alloc", "hlc_host_free",
     "hlc_host_threads", "hlc_ctx_last_host_trace", "hlc_ctx_set_clock_probe", "hlc_ctx_clock_probe",
+    "hlc_validate_proposals_verdicts", "hlc_validate_proposals_verdicts_device", "hlc_encode_vote_payloads",
+    "hlc_process_votes_verdicts", "hlc_ctx_set_option", "hlc_ctx_get_option",
 )
+
+# hlc_ctx_set_option / hlc_ctx_get_option (include/hlc.h HLC_OPT_*): the host-buffer entries' tunables
+OPTIONS = {
+    "host_threads": 1, "pool_bind": 2, "nt_copy": 3, "split_votes": 4, "host_trace": 5, "first_batch": 6,
+    "rest_pieces": 7, "wire_split_bytes": 8, "wire_front_cap": 9, "wire_chunk": 10, "rec_force_exact": 11,
+    "serial_stages": 12, "wire_pipeline": 13, "wire_walk": 14, "split_votes_append": 15,
+    "wire_split_bytes_append": 16,
+}
+LIST_OPTIONS = {"split_votes": "split_votes_append", "wire_split_bytes": "wire_split_bytes_append"}
+POOL_BIND_NONE, POOL_BIND_GPU, POOL_BIND_SOURCE = 0, 1, 2
+
+# ConsensusSignatureScheme::verify outcomes as the ABI codes them (include/hlc.h)
+VERIFY_TRUE, VERIFY_FALSE, SCHEME_PLUGIN = 0, 1, 7
+VERIFY_ERR = 1 + SCHEME_PLUGIN
 
 _lib = None
 
@@ -222,6 +238,21 @@ def load_library(path: str = LIB_PATH):
     lib.hlc_ctx_take_kernel_time.restype = c_int
     lib.hlc_ctx_take_chain_time.argtypes = [vp, POINTER(ctypes.c_double), u64p]
     lib.hlc_ctx_take_chain_time.restype = c_int
+    lib.hlc_ctx_set_option.argtypes = [vp, c_int, ctypes.c_int64]
+    lib.hlc_ctx_set_option.restype = c_int
+    lib.hlc_ctx_get_option.argtypes = [vp, c_int, POINTER(ctypes.c_int64)]
+    lib.hlc_ctx_get_option.restype = c_int
+    lib.hlc_validate_proposals_verdicts.argtypes = [vp, POINTER(hlc_votes), POINTER(hlc_proposal), c_uint64,
+                                                    c_uint64, u8p, POINTER(hlc_result), u8p, u8p]
+    lib.hlc_validate_proposals_verdicts.restype = c_int
+    lib.hlc_validate_proposals_verdicts_device.argtypes = [vp, POINTER(hlc_votes), POINTER(hlc_proposal), c_uint64,
+                                                           c_uint64, vp, vp, vp, vp, vp]
+    lib.hlc_validate_proposals_verdicts_device.restype = c_int
+    lib.hlc_encode_vote_payloads.argtypes = [vp, POINTER(hlc_votes), u64p, u32p, u8p, c_uint64, u64p]
+    lib.hlc_encode_vote_payloads.restype = c_int
+    lib.hlc_process_votes_verdicts.argtypes = [vp, POINTER(hlc_votes), u32p, vp, c_uint64, u8p, c_uint64, u64p, u32p,
+                                               u32p, c_uint64, c_uint64, u8p, u8p, u8p, u8p, u8p]
+    lib.hlc_process_votes_verdicts.restype = c_int
     if hasattr(lib, "hlc_ctx_set_clock_probe"):  # (diagnostics: absent from older builds loaded for A/B runs)
         lib.hlc_ctx_set_clock_probe.argtypes = [vp, c_int]
         lib.hlc_ctx_set_clock_probe.restype = c_int

@@ -60,6 +60,39 @@ class Engine:
         except Exception:
             pass
 
+    def set_option(self, name: str, value) -> None:
+        """hlc_ctx_set_option: one of _ffi.OPTIONS (the host-buffer entries' tunables) on this context.  The
+        range-size lists (split_votes, wire_split_bytes) also take a sequence or an "a,b,..." string."""
+        if name in _ffi.LIST_OPTIONS and not isinstance(value, (int, np.integer)):
+            sizes = [int(x) for x in (value.split(",") if isinstance(value, str) else value)]
+            _ffi.check(self.lib.hlc_ctx_set_option(self.ctx, _ffi.OPTIONS[name], sizes[0]))
+            for x in sizes[1:]:
+                _ffi.check(self.lib.hlc_ctx_set_option(self.ctx, _ffi.OPTIONS[_ffi.LIST_OPTIONS[name]], x))
+            return
+        _ffi.check(self.lib.hlc_ctx_set_option(self.ctx, _ffi.OPTIONS[name], int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64(0)
+        _ffi.check(self.lib.hlc_ctx_get_option(self.ctx, _ffi.OPTIONS[name], ctypes.byref(v)))
+        return int(v.value)
+
+    def options(self, **kv):
+        """Context manager: the given options set for the block, restored after it (a range-size list to
+        the library default)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_option(k) for k in kv}
+            try:
+                for k, v in kv.items():
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_option(k, -1 if k in _ffi.LIST_OPTIONS else v)
+        return cm()
+
     def reserve(self, max_votes: int, max_proposals: int, max_bytes: int = 0) -> None:
         _ffi.check(self.lib.hlc_ctx_reserve(self.ctx, max_votes, max_proposals, max_bytes))
 
@@ -80,6 +113,75 @@ class Engine:
             _ffi.ptr(vst, c_uint8), _ffi.ptr(vrs, c_uint8), _ffi.ptr(rec, c_uint8)))
         return (res, vst[:n] if vst is not None else None, vrs[:n] if vrs is not None else None,
                 rec[:n] if rec is not None else None)
+
+    # ---- any ConsensusSignatureScheme (service.rs:39-51): the caller's verdicts -------------------
+    def encode_vote_payloads(self, batch: VoteBatch) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """hlc_encode_vote_payloads: the payload Signer::verify gets per vote (utils.rs:150-152, the prost
+        encoding with the signature cleared), built on the device -> (arena u8, off u64[n], len u32[n])."""
+        n = batch.n
+        off = np.zeros(max(n, 1), np.uint64)
+        lens = np.zeros(max(n, 1), np.uint32)
+        total = c_uint64(0)
+        view = batch.view()
+        _ffi.check(self.lib.hlc_encode_vote_payloads(self.ctx, ctypes.byref(view), _ffi.ptr(off, c_uint64),
+                                                     _ffi.ptr(lens, c_uint32), None, 0, ctypes.byref(total)))
+        arena = np.zeros(max(int(total.value), 1), np.uint8)
+        _ffi.check(self.lib.hlc_encode_vote_payloads(self.ctx, ctypes.byref(view), _ffi.ptr(off, c_uint64),
+                                                     _ffi.ptr(lens, c_uint32), _ffi.ptr(arena, c_uint8), arena.size,
+                                                     ctypes.byref(total)))
+        return arena[:int(total.value)], off[:n], lens[:n]
+
+    def validate_proposals_verdicts(self, batch: VoteBatch, desc: np.ndarray, now: int, verdicts: np.ndarray,
+                                    want_votes: bool = True):
+        """hlc_validate_proposals_verdicts: validate-many with the scheme step given per vote by the caller
+        (HLC_VERIFY_TRUE / _FALSE / _ERR) -> (results[np], vote_status[n], vote_reason[n])."""
+        n = batch.n
+        verdicts = np.ascontiguousarray(verdicts, dtype=np.uint8).reshape(-1)
+        if verdicts.shape[0] != n:
+            raise ValueError(f"verdicts has {verdicts.shape[0]} entries for {n} votes")
+        res = np.zeros(desc.shape[0], dtype=_ffi.RESULT_DTYPE)
+        vst = np.zeros(max(n, 1), np.uint8) if want_votes else None
+        vrs = np.zeros(max(n, 1), np.uint8) if want_votes else None
+        view = batch.view()
+        desc = np.ascontiguousarray(desc)
+        vbuf = verdicts if n else np.zeros(1, np.uint8)
+        _ffi.check(self.lib.hlc_validate_proposals_verdicts(
+            self.ctx, ctypes.byref(view), proposals_ptr(desc), desc.shape[0], now, _ffi.ptr(vbuf, c_uint8),
+            results_ptr(res), _ffi.ptr(vst, c_uint8), _ffi.ptr(vrs, c_uint8)))
+        return res, vst[:n] if vst is not None else None, vrs[:n] if vrs is not None else None
+
+    def validate_proposals_verdicts_device(self, dbatch, verdicts_ptr: int, stream_handle: int = 0) -> None:
+        """hlc_validate_proposals_verdicts_device on a device.DeviceBatch (verdicts: raw device pointer)."""
+        vp = lambda p: ctypes.cast(p, c_void_p)  # noqa: E731
+        _ffi.check(self.lib.hlc_validate_proposals_verdicts_device(
+            self.ctx, ctypes.byref(dbatch.view), ctypes.cast(dbatch.props_ptr, ctypes.POINTER(_ffi.hlc_proposal)),
+            dbatch.n_proposals, dbatch.now, c_void_p(verdicts_ptr), vp(dbatch.results_ptr), vp(dbatch.status_ptr),
+            vp(dbatch.reason_ptr), c_void_p(stream_handle) if stream_handle else None))
+
+    def process_votes_verdicts(self, batch: VoteBatch, vote_session: np.ndarray, sessions: np.ndarray,
+                               owners: Sequence[bytes], owner_session: np.ndarray, now: int, verdicts: np.ndarray):
+        """hlc_process_votes_verdicts: process_incoming_vote (service.rs:286-305) for every vote, in order,
+        with the caller's scheme verdicts and owner maps of any identity length.  `sessions` (SESSION_DTYPE)
+        is updated in place.  -> (status, transition, inserted, reason)."""
+        n = batch.n
+        vote_session = np.ascontiguousarray(vote_session, dtype=np.uint32)
+        verdicts = np.ascontiguousarray(verdicts, dtype=np.uint8).reshape(-1)
+        if verdicts.shape[0] != n or vote_session.shape[0] != n:
+            raise ValueError("verdicts / vote_session must have one entry per vote")
+        assert sessions.dtype == _ffi.SESSION_DTYPE and sessions.flags.c_contiguous
+        oarena, ooff, olen, ototal = _arena(list(owners))
+        osess = np.ascontiguousarray(owner_session, dtype=np.uint32)
+        m = len(owners)
+        out = [np.zeros(max(n, 1), np.uint8) for _ in range(4)]
+        view = batch.view()
+        one32, one64 = np.zeros(1, np.uint32), np.zeros(1, np.uint64)
+        _ffi.check(self.lib.hlc_process_votes_verdicts(
+            self.ctx, ctypes.byref(view), _ffi.ptr(vote_session if n else one32, c_uint32),
+            c_void_p(sessions.ctypes.data) if sessions.shape[0] else None, sessions.shape[0],
+            _ffi.ptr(oarena, c_uint8), ototal, _ffi.ptr(ooff if m else one64, c_uint64),
+            _ffi.ptr(olen if m else one32, c_uint32), _ffi.ptr(osess if m else one32, c_uint32), m, now,
+            _ffi.ptr(verdicts if n else np.zeros(1, np.uint8), c_uint8), *[_ffi.ptr(o, c_uint8) for o in out]))
+        return tuple(o[:n] for o in out)
 
     def compute_vote_hashes(self, batch: VoteBatch) -> np.ndarray:
         out = np.zeros((max(batch.n, 1), 32), np.uint8)

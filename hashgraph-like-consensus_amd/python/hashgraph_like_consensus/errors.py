@@ -61,6 +61,7 @@ SCHEME_REASONS = {
     4: "r or s out of range",
     5: "r is not the x-coordinate of a curve point",
     6: "recovered key is the identity",
+    7: "the signature scheme rejected the input",  # HLC_SCHEME_PLUGIN: a caller-side scheme's Err(Verify)
 }
 
 _BY_CODE = {cls.code: cls for cls in (

@@ -17,7 +17,12 @@ accepted sessions are kept in a plain dict so a second delivery of the same prop
 rejected exactly as the reference's storage lookup does.
 
 Every hash, signature and tally is computed on the GPU through libhlc.so (engine.py); this module
-only marshals and maps status codes to exceptions.
+only marshals and maps status codes to exceptions.  The service is generic over the signature scheme
+like the reference's `ConsensusService<.., Signer>` (service.rs:39-51): with the default
+EthereumConsensusSigner the device runs the whole validation; with any other
+`ConsensusSignatureScheme` (e.g. the reference's StubSigner, tests/custom_scheme_tests.rs) the scheme's
+`verify_batch` decides the signature step of each vote and the device runs everything else
+(hlc_validate_proposals_verdicts / hlc_process_votes_verdicts).
 """
 from __future__ import annotations
 
@@ -31,6 +36,7 @@ from . import errors
 from .batch import ProposalConfig, pack_proposals, pack_votes
 from .engine import Engine
 from .protos import Proposal, Vote
+from .signing import scheme_verdicts
 
 GOSSIPSUB, P2P = "gossipsub", "p2p"
 DEFAULT_THRESHOLD = 2.0 / 3.0
@@ -121,21 +127,35 @@ def _outcomes(proposals: Sequence[Proposal], res: np.ndarray) -> List[ProposalOu
     return out
 
 
+def _device_scheme(scheme) -> bool:
+    return scheme is None or getattr(scheme, "DEVICE_SCHEME", False)
+
+
+def validate_batch(eng: Engine, batch, desc: np.ndarray, now: int, scheme=None) -> np.ndarray:
+    """from_proposal over a packed batch under `scheme` (None: EthereumConsensusSigner) -> results."""
+    if _device_scheme(scheme):
+        res, _, _, _ = eng.validate_proposals(batch, desc, now, want_votes=False)
+    else:
+        verdicts = scheme_verdicts(scheme, batch, eng)
+        res, _, _ = eng.validate_proposals_verdicts(batch, desc, now, verdicts, want_votes=False)
+    return res
+
+
 def validate_proposals(proposals: Sequence[Proposal], now: int, configs: Optional[Sequence[ConsensusConfig]] = None,
-                       engine: Optional[Engine] = None) -> List[ProposalOutcome]:
-    """Batched `ConsensusSession::from_proposal` validation (session.rs:198-300 incl. utils.rs:106-225):
-    one GPU call for every proposal."""
+                       engine: Optional[Engine] = None, scheme=None) -> List[ProposalOutcome]:
+    """Batched `ConsensusSession::from_proposal::<Signer>` validation (session.rs:198-300 incl.
+    utils.rs:106-225): one GPU call for every proposal.  `scheme` is the `Signer` type (default
+    EthereumConsensusSigner)."""
     eng = engine or Engine.default()
     cfgs = [(configs[i] if configs is not None else ConsensusConfig()).to_proposal_config() for i in range(len(proposals))]
     batch, desc = pack_proposals(proposals, cfgs)
-    res, _, _, _ = eng.validate_proposals(batch, desc, now, want_votes=False)
-    return _outcomes(proposals, res)
+    return _outcomes(proposals, validate_batch(eng, batch, desc, now, scheme))
 
 
 def validate_proposal(proposal: Proposal, now: int, config: Optional[ConsensusConfig] = None,
-                      engine: Optional[Engine] = None) -> ProposalOutcome:
+                      engine: Optional[Engine] = None, scheme=None) -> ProposalOutcome:
     """utils.rs:106 + session.rs:198: raises the reference's ConsensusError on rejection."""
-    o = validate_proposals([proposal], now, [config] if config else None, engine)[0]
+    o = validate_proposals([proposal], now, [config] if config else None, engine, scheme)[0]
     if o.error is not None:
         raise o.error
     return o
@@ -204,9 +224,13 @@ class SessionRecord:
 class ConsensusService:
     """service.rs:63-280 restricted to the incoming-proposal path (see module docstring)."""
 
-    def __init__(self, engine: Optional[Engine] = None, default_config: Optional[ConsensusConfig] = None):
+    def __init__(self, engine: Optional[Engine] = None, default_config: Optional[ConsensusConfig] = None,
+                 scheme=None):
+        """`scheme`: the service's `Signer` type (service.rs:39-51), a ConsensusSignatureScheme subclass;
+        None = EthereumConsensusSigner."""
         self.engine = engine or Engine.default()
         self.default_config = default_config or ConsensusConfig.gossipsub()
+        self.scheme = scheme
         self.scope_configs: Dict[bytes, ConsensusConfig] = {}
         self.sessions: Dict[Tuple[bytes, int], SessionRecord] = {}
 
@@ -245,7 +269,7 @@ class ConsensusService:
         cfgs = [resolve_config(base, proposals[i]) for i in todo]
         sub = [proposals[i] for i in todo]
         if sub:
-            res = validate_proposals(sub, now, cfgs, self.engine)
+            res = validate_proposals(sub, now, cfgs, self.engine, self.scheme)
             # an id that fails validation is not stored, so a later copy in the batch would be
             # validated in the reference; re-run those (rare) in a second pass.
             retry: List[int] = []
@@ -332,18 +356,27 @@ class ConsensusService:
             vsess[i] = index[v.proposal_id]
         sarr = np.zeros(len(recs), _ffi.SESSION_DTYPE)
         orows, osess = [], []
+        generic = not _device_scheme(self.scheme)
         for k, r in enumerate(recs):
             p, c = r.proposal, r.config
             sarr[k] = (p.timestamp, p.expiration_timestamp, p.proposal_id, p.expected_voters_count, r.round, r.total,
                        r.yes, c.max_rounds, c.consensus_threshold, r.state, int(c.use_gossipsub_rounds),
                        int(p.liveness_criteria_yes), (0,) * 5)
             for o in r.owners:
-                if len(o) == 20:
+                if generic:
+                    orows.append(bytes(o))
+                    osess.append(k)
+                elif len(o) == 20:  # (EthereumConsensusSigner admits only 20-byte identities)
                     orows.append(np.frombuffer(o, np.uint8))
                     osess.append(k)
-        owners = np.stack(orows) if orows else np.zeros((0, 20), np.uint8)
-        st, tr, ins, rs = self.engine.process_votes(pack_votes(votes), vsess, sarr, owners,
-                                                    np.array(osess, np.uint32), now)
+        batch = pack_votes(votes)
+        if generic:
+            verdicts = scheme_verdicts(self.scheme, batch, self.engine)
+            st, tr, ins, rs = self.engine.process_votes_verdicts(batch, vsess, sarr, orows, np.array(osess, np.uint32),
+                                                                 now, verdicts)
+        else:
+            owners = np.stack(orows) if orows else np.zeros((0, 20), np.uint8)
+            st, tr, ins, rs = self.engine.process_votes(batch, vsess, sarr, owners, np.array(osess, np.uint32), now)
         for k, r in enumerate(recs):
             s = sarr[k]
             r.round, r.total, r.yes = int(s["round"]), int(s["total"]), int(s["yes"])
@@ -380,7 +413,7 @@ class ConsensusService:
         scope_cfg = np.zeros(1, _ffi.SCOPE_CONFIG_DTYPE)
         scope_cfg[0] = (base.consensus_threshold, base.max_rounds, int(base.use_gossipsub_rounds), (0, 0, 0))
         props, winfo, batch = self.engine.decode_proposals(wire, off, lens, scope_cfg)
-        res, _, _, _ = self.engine.validate_proposals(batch, props, now, want_votes=False)
+        res = validate_batch(self.engine, batch, props, now, self.scheme)
         out: List[ProposalOutcome] = []
         for m, msg in enumerate(messages):
             if int(winfo[m]["decode_status"]) != 0:

@@ -66,11 +66,13 @@ extern "C" {
 #define HLC_SCHEME_SCALAR_RANGE 4   /* r or s zero or >= n (k256 from_scalars via to_k256) */
 #define HLC_SCHEME_NO_POINT 5       /* R = decompress(r) does not exist */
 #define HLC_SCHEME_INFINITY 6       /* recovered key is the identity */
+#define HLC_SCHEME_PLUGIN 7         /* Err(Verify) returned by a caller-side scheme (the *_verdicts entries) */
 
 /* Outcome of `ConsensusSignatureScheme::verify` (signing.rs:60-73) per item. */
 #define HLC_VERIFY_TRUE 0           /* Ok(true)  */
 #define HLC_VERIFY_FALSE 1          /* Ok(false) */
 /* values >= 2: Err(ConsensusSchemeError::Verify), value - 1 == HLC_SCHEME_* reason */
+#define HLC_VERIFY_ERR (1 + HLC_SCHEME_PLUGIN) /* a caller-side scheme's Err(Verify) */
 
 /* SessionTransition (types.rs:29-34) */
 #define HLC_STILL_ACTIVE 0
@@ -227,15 +229,50 @@ int hlc_abi_version(void);
 int hlc_host_alloc(uint64_t bytes, void** out);
 void hlc_host_free(void* p);
 
-/* Host threads (including the caller's) the host-buffer entries (hlc_validate_proposals,
- * hlc_validate_wire_proposals, hlc_eth_verify_batch) stage their copies with: HLC_HOST_THREADS when
- * set, else min(16, hardware threads, the process's CPU share = the cgroup CPU quota (or the hardware
- * threads) / LOCAL_WORLD_SIZE, the ranks on the node).  Read when a context first stages. */
+/* ---- Context options ------------------------------------------------------------------------
+ * The host-buffer entries' tunables, per context.  hlc_ctx_create reads each one's default from the
+ * environment variable named beside it, once; no library call reads the environment after that (an
+ * embedder's threads may setenv at any time), and hlc_ctx_set_option changes a context's value. */
+#define HLC_OPT_HOST_THREADS 1     /* staging threads incl. the caller, 1..64 (HLC_HOST_THREADS; default
+                                      hlc_host_threads()) */
+#define HLC_OPT_POOL_BIND 2        /* the staging workers' CPUs: HLC_POOL_BIND_* (HLC_POOL_BIND) */
+#define HLC_OPT_NT_COPY 3          /* 1: non-temporal staging copies on AVX2 CPUs (HLC_NT_COPY; default 1) */
+#define HLC_OPT_SPLIT_VOTES 4      /* votes of the first recovery range of hlc_validate_proposals /
+                                      hlc_eth_verify_batch, later ranges doubling; 0: one range; -1:
+                                      the default (HLC_SPLIT_VOTES, a list "a,b,..."; 98304,196608) */
+#define HLC_OPT_HOST_TRACE 5       /* 0 off; 1 phase trace on stderr and in hlc_ctx_last_host_trace; 2 the
+                                      latter only (HLC_HOST_TRACE; default 0) */
+#define HLC_OPT_FIRST_BATCH 6      /* votes per prep lane of the first recovery range (HLC_FIRST_BATCH; 1) */
+#define HLC_OPT_REST_PIECES 7      /* pieces the non-signature inputs are staged in, 1..64 (HLC_REST_PIECES; 3) */
+#define HLC_OPT_WIRE_SPLIT_BYTES 8 /* bytes of the first message range of hlc_validate_wire_proposals,
+                                      later ranges doubling; 0: one range; -1: the default
+                                      (HLC_WIRE_SPLIT_BYTES, a list; 8, 16, 24, 32 MiB) */
+#define HLC_OPT_WIRE_FRONT_CAP 9   /* waves per recovery grid of every message range but the last; 0: full
+                                      grids (HLC_WIRE_FRONT_CAP; default 1536) */
+#define HLC_OPT_WIRE_CHUNK 10      /* bytes per wire staging piece, >= 4096 (HLC_WIRE_CHUNK; 4 MiB) */
+#define HLC_OPT_REC_FORCE_EXACT 11 /* 1: every vote through the recovery's checked chains (tests; 0) */
+#define HLC_OPT_SERIAL_STAGES 12   /* 1: the recovery's prep + main after the prehash on one stream
+                                      (isolated kernel traces; HLC_SERIAL_STAGES; 0) */
+#define HLC_OPT_WIRE_PIPELINE 13   /* 0: the unpipelined wire host entry (A/B arm; HLC_WIRE_PIPELINE; 1) */
+#define HLC_OPT_WIRE_WALK 14       /* -1 the build's wire walker, 0 one lane per message, 1 the LDS walker
+                                      (HLC_WIRE_WALK = "lane" / "lds") */
+#define HLC_OPT_SPLIT_VOTES_APPEND 15      /* appends a range size to HLC_OPT_SPLIT_VOTES' list ("a,b,...") */
+#define HLC_OPT_WIRE_SPLIT_BYTES_APPEND 16 /* appends a range size to HLC_OPT_WIRE_SPLIT_BYTES' list */
+#define HLC_POOL_BIND_NONE 0       /* workers run on any CPU of the process's affinity mask */
+#define HLC_POOL_BIND_GPU 1        /* the CPUs of the GPU's NUMA node (default) */
+#define HLC_POOL_BIND_SOURCE 2     /* the CPUs of the NUMA node the call's input arena lives on, per call */
+int hlc_ctx_set_option(hlc_ctx* ctx, int option, int64_t value);  /* HLC_EINVAL: unknown / out of range */
+int hlc_ctx_get_option(hlc_ctx* ctx, int option, int64_t* value);  /* list options: their first entry */
+
+/* Host threads (including the caller's) a new context stages host-buffer copies with by default:
+ * HLC_HOST_THREADS when set, else min(16, hardware threads, the process's CPU share = the cgroup CPU
+ * quota (or the hardware threads) / LOCAL_WORLD_SIZE, the ranks on the node). */
 int hlc_host_threads(void);
 
-/* With HLC_HOST_TRACE=1 (also printed on stderr) or 2 in the environment: the last host-buffer call's
- * phase times on this context as JSON -- {"host": {phase: ms}, "device": {event: ms}}, ms from the
- * call's start; "" otherwise.  Valid until the next call on the context. */
+/* With HLC_OPT_HOST_TRACE 1 or 2: the last host-buffer call's phase times on this context as JSON --
+ * {"host": {phase: ms}, "device": {event: ms}, "facts": {...}}, ms from the call's start; "" after a
+ * call made without tracing.  A copy taken under the context's lock, valid on the calling thread until
+ * its next hlc_ctx_last_host_trace. */
 const char* hlc_ctx_last_host_trace(hlc_ctx* ctx);
 
 /* ---- Measurement hooks (bench.py roofline): HIP events on the launch stream ------ */
@@ -315,6 +352,40 @@ int hlc_validate_proposals_device(hlc_ctx* ctx, const hlc_votes* votes,
                                   uint64_t now, hlc_result* out_results,
                                   uint8_t* out_vote_status, uint8_t* out_vote_reason,
                                   uint8_t* out_recovered, void* stream);
+
+/* ---- Scheme-generic validate-many (any `ConsensusSignatureScheme`) --------------------------
+ * `ConsensusService<Scope, Storage, Event, Signer>` is generic over the signature scheme
+ * (service.rs:39-51, signing.rs:46-74); the reference's tests/custom_scheme_tests.rs runs it with a
+ * non-Ethereum StubSigner.  These entries are hlc_validate_proposals with the scheme step of
+ * validate_vote (utils.rs:150-158: `Signer::verify(vote_owner, encode(vote, signature cleared),
+ * signature)`) supplied by the caller: verdicts[v] is that call's outcome for vote v --
+ * HLC_VERIFY_TRUE, HLC_VERIFY_FALSE, or Err(Verify) as HLC_VERIFY_ERR (any value 2..HLC_VERIFY_ERR is
+ * an Err whose value - 1 is reported back as the HLC_SCHEME_* reason, so hlc_eth_verify_batch's
+ * statuses can be passed straight in).  Everything else runs on the device as in
+ * hlc_validate_proposals: the proposal_id match, the empty-field checks and the SHA-256 vote-hash
+ * recompute (which precede the scheme step, so a verdict is read only for votes that reach it),
+ * the timestamp checks, validate_vote_chain, the duplicate-owner and count checks, the round limit
+ * and the tally, with the first-error precedence of SURVEY.md Appendix B.  No Ethereum assumption
+ * is made: identities and signatures may have any length, and no secp256k1 recovery runs.
+ * Host buffers, blocking; verdicts has votes->n entries (HLC_EINVAL for a value above HLC_VERIFY_ERR). */
+int hlc_validate_proposals_verdicts(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,
+                                    uint64_t n_proposals, uint64_t now, const uint8_t* verdicts,
+                                    hlc_result* out_results, uint8_t* out_vote_status, uint8_t* out_vote_reason);
+
+/* Same with every pointer in DEVICE memory, enqueued on `stream` (NULL: the context's stream) without
+ * host synchronisation.  A verdict above HLC_VERIFY_ERR is read as HLC_VERIFY_ERR. */
+int hlc_validate_proposals_verdicts_device(hlc_ctx* ctx, const hlc_votes* votes, const hlc_proposal* proposals,
+                                           uint64_t n_proposals, uint64_t now, const uint8_t* verdicts,
+                                           hlc_result* out_results, uint8_t* out_vote_status,
+                                           uint8_t* out_vote_reason, void* stream);
+
+/* The payload a scheme verifies for each vote (utils.rs:150-152): the prost encoding of the Vote with
+ * its signature cleared (consensus.proto:19-29: tags 20-27, proto3 defaults omitted), built on the
+ * device.  out_off[n] / out_len[n] receive every payload's place in out_bytes and *out_total the bytes
+ * they need; out_bytes (capacity `cap`) may be NULL to query the size.  When cap < *out_total nothing
+ * is written to out_bytes and HLC_ERANGE is returned (out_off / out_len are still written). */
+int hlc_encode_vote_payloads(hlc_ctx* ctx, const hlc_votes* votes, uint64_t* out_off, uint32_t* out_len,
+                             uint8_t* out_bytes, uint64_t cap, uint64_t* out_total);
 
 /* Batched `ConsensusService::handle_consensus_timeout` (service.rs:323-373)
  * over n sessions: a session already in ConsensusReached(r) keeps it; otherwise
@@ -412,6 +483,18 @@ int hlc_process_votes_device(hlc_ctx* ctx, const hlc_votes* votes, const uint32_
                              const uint32_t* owner_session, uint64_t n_owners, uint64_t now,
                              uint8_t* out_status, uint8_t* out_transition, uint8_t* out_inserted,
                              uint8_t* out_reason, void* stream);
+
+/* Scheme-generic form of hlc_process_votes (any `ConsensusSignatureScheme`, service.rs:39-51): the
+ * scheme step of validate_vote is the caller's, verdicts[n] exactly as for
+ * hlc_validate_proposals_verdicts, and the existing owner maps hold identities of any length: owner k
+ * is owner_bytes[owner_off[k] .. + owner_len[k]] (inside [0, owner_bytes_len)) of session
+ * owner_session[k].  Host buffers, blocking; the outcomes are those of hlc_process_votes. */
+int hlc_process_votes_verdicts(hlc_ctx* ctx, const hlc_votes* votes, const uint32_t* vote_session,
+                               hlc_session* sessions, uint64_t n_sessions, const uint8_t* owner_bytes,
+                               uint64_t owner_bytes_len, const uint64_t* owner_off, const uint32_t* owner_len,
+                               const uint32_t* owner_session, uint64_t n_owners, uint64_t now,
+                               const uint8_t* verdicts, uint8_t* out_status, uint8_t* out_transition,
+                               uint8_t* out_inserted, uint8_t* out_reason);
 
 /* ---- Wire decode -------------------------------------------------- */
 

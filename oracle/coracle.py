@@ -58,6 +58,8 @@ def load():
     lib.hlco_check_round_limit.restype = c_int
     lib.hlco_update_round.argtypes = [c_int, c_uint32, c_uint64]
     lib.hlco_update_round.restype = c_uint32
+    lib.hlco_stub_sign.argtypes = [u8p, c_uint32, u8p, c_size_t, u8p]
+    lib.hlco_stub_sign.restype = c_int
     _lib = lib
     return lib
 
@@ -89,11 +91,13 @@ def eip191_hash(b: bytes) -> bytes:
     return out.tobytes()
 
 
-REVERIFY, GLV = 1, 2  # hlco_* flags (hlc_oracle.c)
+REVERIFY, GLV, STUB = 1, 2, 4  # hlco_* flags (hlc_oracle.c)
 
 
-def _flags(reverify: bool, glv: bool) -> int:
-    return (REVERIFY if reverify else 0) | (GLV if glv else 0)
+def _flags(reverify: bool, glv: bool, scheme: str = "ethereum") -> int:
+    if scheme not in ("ethereum", "stub"):
+        raise ValueError(f"unknown scheme {scheme!r}")
+    return (REVERIFY if reverify else 0) | (GLV if glv else 0) | (STUB if scheme == "stub" else 0)
 
 
 def ecrecover(prehash: bytes, sig: bytes, reverify: bool = True, glv: bool = False):
@@ -139,8 +143,10 @@ def encode_vote(batch, i: int) -> bytes:
 
 
 def validate_proposals(batch, desc: np.ndarray, now: int, threads: int = 8, reverify: bool = False,
-                       glv: bool = False):
-    """-> (results structured array, vote_status u8[n], vote_reason u8[n], recovered u8[n,20])"""
+                       glv: bool = False, scheme: str = "ethereum"):
+    """-> (results structured array, vote_status u8[n], vote_reason u8[n], recovered u8[n,20]).
+    scheme "stub": the votes' scheme is tests/custom_scheme_tests.rs's StubSigner (8-byte identity,
+    signature = SHA256(identity || payload)) instead of EthereumConsensusSigner."""
     from hashgraph_like_consensus import _ffi  # struct layout only
     n = batch.n
     res = np.zeros(desc.shape[0], dtype=_ffi.RESULT_DTYPE)
@@ -149,7 +155,8 @@ def validate_proposals(batch, desc: np.ndarray, now: int, threads: int = 8, reve
     rec = np.zeros((max(n, 1), 20), np.uint8)
     view = batch.view()
     load().hlco_validate_proposals(ctypes.byref(view), desc.ctypes.data, desc.shape[0], now,
-                                   res.ctypes.data, _u8(vst), _u8(vrs), _u8(rec), threads, _flags(reverify, glv))
+                                   res.ctypes.data, _u8(vst), _u8(vrs), _u8(rec), threads,
+                                   _flags(reverify, glv, scheme))
     return res, vst[:n], vrs[:n], rec[:n]
 
 
@@ -177,3 +184,10 @@ def check_round_limit(gossipsub: bool, max_rounds: int, t: float, n: int, round_
 def update_round(gossipsub: bool, round_: int, vote_count: int) -> int:
     """session.rs:351-366 restated in C (P2P saturating at u32::MAX)."""
     return int(load().hlco_update_round(int(gossipsub), round_, vote_count))
+
+
+def stub_sign(identity: bytes, payload: bytes) -> bytes:
+    """StubSigner::sign (tests/custom_scheme_tests.rs:42-47, 55-57): SHA256(identity || payload)."""
+    out = np.zeros(32, np.uint8)
+    load().hlco_stub_sign(_u8(_buf(identity)), len(identity), _u8(_buf(payload)), len(payload), _u8(out))
+    return out.tobytes()

@@ -36,6 +36,10 @@
  * k256-class GLV path instead of the independent non-GLV checker */
 #define HLCO_REVERIFY 1
 #define HLCO_GLV 2
+/* the scheme is tests/custom_scheme_tests.rs's StubSigner (:33-74) instead of EthereumConsensusSigner:
+ * an 8-byte identity, signature = SHA256(identity || payload) -- ConsensusService is generic over the
+ * scheme (src/service.rs:39-51, src/signing.rs:46-74) */
+#define HLCO_STUB 4
 
 typedef uint64_t u64;
 typedef uint32_t u32;
@@ -927,6 +931,28 @@ int hlco_verify_batch(u64 n, const u8* bytes, const u64* id_off, const u32* id_l
   return 0;
 }
 
+/* StubSigner::verify (tests/custom_scheme_tests.rs:61-73): Err(Verify) unless the identity is 8 bytes,
+ * else Ok(signature == SHA256(identity || payload)) -> HLC_VERIFY_* / 1 + HLC_SCHEME_PLUGIN */
+static int stub_verify(const u8* id, u32 idlen, const u8* payload, size_t plen, const u8* sig, u32 siglen) {
+  if (idlen != 8) return 1 + HLC_SCHEME_PLUGIN;
+  sha256_ctx c;
+  u8 h[32];
+  sha256_init(&c);
+  sha256_update(&c, id, idlen);
+  sha256_update(&c, payload, plen);
+  sha256_final(&c, h);
+  return (siglen == 32 && memcmp(sig, h, 32) == 0) ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
+}
+
+int hlco_stub_sign(const u8* id, u32 idlen, const u8* payload, size_t plen, u8 out[32]) {
+  sha256_ctx c;
+  sha256_init(&c);
+  sha256_update(&c, id, idlen);
+  sha256_update(&c, payload, plen);
+  sha256_final(&c, out);
+  return 0;
+}
+
 /* validate_vote (utils.rs:127-171) preceded by the proposal_id check (utils.rs:113-115) */
 static void validate_one(const hlc_votes* vs, u64 i, const hlc_proposal* p, u64 now, u8* st,
                          u8* reason, u8 addr[20], int flags) {
@@ -947,8 +973,11 @@ static void validate_one(const hlc_votes* vs, u64 i, const hlc_proposal* p, u64 
   u8 stackbuf[512];
   u8* enc = elen <= sizeof stackbuf ? stackbuf : (u8*)malloc(elen);
   encode_vote(&v, enc);
-  int vr = eth_verify(v.f[HLC_F_OWNER], v.flen[HLC_F_OWNER], enc, elen, v.f[HLC_F_SIGNATURE],
-                      v.flen[HLC_F_SIGNATURE], addr, flags);
+  int vr = (flags & HLCO_STUB)
+               ? stub_verify(v.f[HLC_F_OWNER], v.flen[HLC_F_OWNER], enc, elen, v.f[HLC_F_SIGNATURE],
+                             v.flen[HLC_F_SIGNATURE])
+               : eth_verify(v.f[HLC_F_OWNER], v.flen[HLC_F_OWNER], enc, elen, v.f[HLC_F_SIGNATURE],
+                            v.flen[HLC_F_SIGNATURE], addr, flags);
   if (enc != stackbuf) free(enc);
   if (vr >= 2) { *st = HLC_SIGNATURE_SCHEME; *reason = (u8)(vr - 1); return; }
   if (vr == HLC_VERIFY_FALSE) { *st = HLC_INVALID_VOTE_SIGNATURE; return; }

@@ -406,8 +406,26 @@ def ethereum_verify(identity: bytes, payload: bytes, signature: bytes) -> Tuple[
     return SCHEME_NONE, addr == identity, addr
 
 
-def validate_vote(v: Vote, expiration: int, creation: int, now: int) -> Tuple[int, int]:
-    """utils.rs:127-171 -> (status, scheme_subcode)."""
+SCHEME_PLUGIN = 7  # HLC_SCHEME_PLUGIN: Err(Verify) from a scheme other than EthereumConsensusSigner
+
+
+def stub_verify(identity: bytes, payload: bytes, signature: bytes) -> Tuple[int, Optional[bool], Optional[bytes]]:
+    """StubSigner::verify of /root/reference/tests/custom_scheme_tests.rs:61-73 (the reference's proof that
+    ConsensusService is generic over the scheme, service.rs:39-51): Err(Verify) unless the identity is
+    8 bytes, else Ok(signature == SHA256(identity || payload))."""
+    if len(identity) != 8:
+        return SCHEME_PLUGIN, None, None
+    return SCHEME_NONE, signature == stub_sign(identity, payload), None
+
+
+def stub_sign(identity: bytes, payload: bytes) -> bytes:
+    """StubSigner::sign / expected_signature (custom_scheme_tests.rs:42-47, 55-57)."""
+    return hashlib.sha256(identity + payload).digest()
+
+
+def validate_vote(v: Vote, expiration: int, creation: int, now: int, scheme=ethereum_verify) -> Tuple[int, int]:
+    """utils.rs:127-171 -> (status, scheme_subcode).  `scheme` is `Signer::verify` (signing.rs:69-73):
+    ethereum_verify (the default EthereumConsensusSigner) or stub_verify."""
     if not v.vote_owner:
         return EMPTY_VOTE_OWNER, 0
     if not v.vote_hash:
@@ -416,7 +434,7 @@ def validate_vote(v: Vote, expiration: int, creation: int, now: int) -> Tuple[in
         return EMPTY_SIGNATURE, 0
     if v.vote_hash != compute_vote_hash(v):
         return INVALID_VOTE_HASH, 0
-    sub, ok, _ = ethereum_verify(v.vote_owner, signed_payload(v), v.signature)
+    sub, ok, _ = scheme(v.vote_owner, signed_payload(v), v.signature)
     if ok is None:
         return SIGNATURE_SCHEME, sub
     if not ok:
@@ -428,11 +446,11 @@ def validate_vote(v: Vote, expiration: int, creation: int, now: int) -> Tuple[in
     return OK, 0
 
 
-def vote_status_in_proposal(p: Proposal, v: Vote, now: int) -> Tuple[int, int]:
+def vote_status_in_proposal(p: Proposal, v: Vote, now: int, scheme=ethereum_verify) -> Tuple[int, int]:
     """Per-vote body of validate_proposal's loop (utils.rs:112-117)."""
     if v.proposal_id != p.proposal_id:
         return VOTE_PROPOSAL_ID_MISMATCH, 0
-    return validate_vote(v, p.expiration_timestamp, p.timestamp, now)
+    return validate_vote(v, p.expiration_timestamp, p.timestamp, now, scheme)
 
 
 def validate_vote_chain(votes: Sequence[Vote]) -> Tuple[int, int]:
@@ -593,7 +611,7 @@ class ProposalOutcome:
 
 
 def from_proposal(p: Proposal, cfg: ConsensusConfig, now: int,
-                  vote_status: Optional[List[Tuple[int, int]]] = None) -> ProposalOutcome:
+                  vote_status: Optional[List[Tuple[int, int]]] = None, scheme=ethereum_verify) -> ProposalOutcome:
     """ConsensusSession::from_proposal (session.rs:198-221) -> validate_proposal
     (utils.rs:106-120) then initialize_with_votes (session.rs:253-298) on a clean copy
     (round reset to 1).  The second validation pass (session.rs:284-287) re-runs the same
@@ -604,7 +622,7 @@ def from_proposal(p: Proposal, cfg: ConsensusConfig, now: int,
         out.status = PROPOSAL_EXPIRED
         return out
     for i, v in enumerate(p.votes):                                 # utils.rs:112-117
-        st = vote_status[i] if vote_status is not None else vote_status_in_proposal(p, v, now)
+        st = vote_status[i] if vote_status is not None else vote_status_in_proposal(p, v, now, scheme)
         if st[0] != OK:
             out.status, out.bad_index = st[0], i
             return out

@@ -93,9 +93,10 @@ def _as_proposal(s: Session) -> po.Proposal:
 
 
 def process_incoming_votes(sessions: List[Session], votes: Sequence[po.Vote], vote_session: Sequence[int],
-                           now: int) -> List[Tuple[int, int, bool, int]]:
+                           now: int, scheme=po.ethereum_verify) -> List[Tuple[int, int, bool, int]]:
     """service.rs:286-305 for each vote in order -> [(status, transition, inserted, scheme reason)].
-    vote_session[i] = session index or -1 / 0xFFFFFFFF for "not found".  Mutates `sessions`."""
+    vote_session[i] = session index or -1 / 0xFFFFFFFF for "not found".  Mutates `sessions`.
+    `scheme` is the service's `Signer::verify` (pyoracle.ethereum_verify or pyoracle.stub_verify)."""
     out = []
     for v, si in zip(votes, vote_session):
         if si < 0 or si >= len(sessions):
@@ -104,7 +105,7 @@ def process_incoming_votes(sessions: List[Session], votes: Sequence[po.Vote], vo
         s = sessions[si]
         # the reference's storage lookup is keyed by vote.proposal_id, so a session of another
         # proposal can only come from a caller's mapping error: reported as the id mismatch
-        st, sub = po.vote_status_in_proposal(_as_proposal(s), v, now)
+        st, sub = po.vote_status_in_proposal(_as_proposal(s), v, now, scheme)
         if st != po.OK:
             out.append((st, po.STILL_ACTIVE, False, sub))
             continue

@@ -199,3 +199,27 @@ def test_host_threads_default_is_rank_aware():
     assert _threads_in_child({}) == max(1, min(16, hw, int(share + 1e-9)))
     assert _threads_in_child({"HLC_HOST_THREADS": "5", "LOCAL_WORLD_SIZE": "8"}) == 5
     assert _threads_in_child({"HLC_HOST_THREADS": "500"}) == 64
+
+
+def test_options_match_header_and_no_per_call_getenv():
+    """the tunables are context options (hlc_ctx_set_option); the environment is
+    read in one function (read_env, called by hlc_ctx_create / hlc_host_threads) and nowhere else."""
+    d = header_defines()
+    for name, code in _ffi.OPTIONS.items():
+        assert d["HLC_OPT_" + name.upper()] == code, name
+    assert {k for k in d if k.startswith("HLC_OPT_")} == {"HLC_OPT_" + n.upper() for n in _ffi.OPTIONS}
+    assert (d["HLC_POOL_BIND_NONE"], d["HLC_POOL_BIND_GPU"], d["HLC_POOL_BIND_SOURCE"]) == (
+        _ffi.POOL_BIND_NONE, _ffi.POOL_BIND_GPU, _ffi.POOL_BIND_SOURCE)
+    csrc = os.path.join(ROOT, "hashgraph-like-consensus_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".cpp", ".hip", ".hpp", ".h")):
+            continue
+        text = open(os.path.join(csrc, f)).read()
+        calls = [m.start() for m in re.finditer(r"std::getenv\(|\bgetenv\(", text)]
+        if f != "hlc_api.cpp":
+            assert not calls, f
+            continue
+        body = text[text.index("Options read_env() {"):]
+        body = body[:body.index("\n}\n")]
+        start = text.index(body)
+        assert calls and all(start <= c < start + len(body) for c in calls), "getenv outside read_env"

@@ -49,3 +49,44 @@ def test_bench_summary_reads_failed_legs(tmp_path):
                          capture_output=True, text=True, check=True).stdout
     assert "100.0 M votes/s" in out and "wire 96.0 M" in out
     assert "end_to_end error: RuntimeError: boom" in out and "cpu error: OSError: x" in out
+
+
+def _full_record():
+    """A full bench record of round 5 (every leg, phases, NUMA facts, histograms) plus this round's
+    config4_shard leg and scaling basis."""
+    d = json.load(open(os.path.join(ROOT, "profiles", "r05", "bench_r5h.json")))
+    d["config4_shard"] = {"metric": "m", "value": 1.07e8, "unit": "votes/s", "ms_per_step": 117.0}
+    d["scaling_basis"] = {"n1_headline": "config 2", "n_gt_1": "config 4 shards", "n1_same_workload": "x"}
+    return d
+
+
+def test_compact_line_fits_and_carries_every_leg(tmp_path):
+    """the stdout line is at most 4 KB, carries a flat `legs` object with every leg
+    (wire_from_host included) and the roofline / CPU-baseline essentials; the full record goes to the
+    side file."""
+    d = _full_record()
+    assert len(json.dumps(d)) > 12_000  # what the driver's tail cut in round 5
+    path = bench.write_detail(d, str(tmp_path / "detail.json"))
+    line = bench.compact_line(d, path)
+    text = json.dumps(line)
+    assert len(text) <= 4096, len(text)
+    assert set(line["legs"]) == set(bench.LEG_NAMES), line["legs"]
+    assert line["legs"]["wire_from_host"] == d["wire"]["from_host_buffers"]["value"]
+    assert line["legs"]["end_to_end"] == d["end_to_end"]["value"]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "config"):
+        assert line[k] == d[k], k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert line["roofline"][k] == d["roofline"][k], k
+    for k in ("value", "unit", "cores", "kind"):
+        assert line["cpu_baseline"][k] == d["cpu_baseline"][k], k
+    assert line["scaling_basis"]["n_gt_1"] == "config 4 shards"
+    assert json.load(open(path)) == d
+
+
+def test_compact_line_reports_failed_legs():
+    d = _full_record()
+    d["stream"] = {"error": "RuntimeError: " + "x" * 1000}
+    line = bench.compact_line(d, None)
+    assert "stream" not in line["legs"] and line["leg_errors"]["stream"].startswith("RuntimeError")
+    assert len(json.dumps(line)) <= 4096

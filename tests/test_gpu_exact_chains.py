@@ -23,11 +23,8 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def exact_engine():
     from hashgraph_like_consensus.engine import Engine
-    os.environ["HLC_REC_FORCE_EXACT"] = "1"
-    try:
-        eng = Engine(0)
-    finally:
-        del os.environ["HLC_REC_FORCE_EXACT"]
+    eng = Engine(0)
+    eng.set_option("rec_force_exact", 1)  # HLC_OPT_REC_FORCE_EXACT: every vote through the checked chains
     yield eng
     eng.close()
 

@@ -1,7 +1,7 @@
 """Randomised schedules of the host-buffer entries (hlc_api.cpp validate_host / verify_host): for a
 Byzantine batch, random proposal subsets in random order, random recovery ranges
-(HLC_SPLIT_VOTES), staging pieces (HLC_REST_PIECES), first-range prep batches (HLC_FIRST_BATCH)
-and host pool sizes (HLC_HOST_THREADS) must give exactly the single-range result -- itself pinned to
+(HLC_OPT_SPLIT_VOTES), staging pieces (HLC_OPT_REST_PIECES), first-range prep batches (HLC_OPT_FIRST_BATCH)
+and host pool sizes (HLC_OPT_HOST_THREADS), set per context with hlc_ctx_set_option, must give exactly the single-range result -- itself pinned to
 the C oracle in test_gpu_host_pipeline.py -- and, for a sample of the settings, the oracle again."""
 import os
 import random
@@ -14,20 +14,9 @@ from adversarial import byzantine
 from helpers import oracle_workload
 
 pytestmark = pytest.mark.gpu
-KNOBS = ("HLC_SPLIT_VOTES", "HLC_REST_PIECES", "HLC_FIRST_BATCH", "HLC_HOST_THREADS")
-
-
-def _call(engine, batch, desc, now, env):
-    old = {k: os.environ.get(k) for k in KNOBS}
-    os.environ.update(env)
-    try:
+def _call(engine, batch, desc, now, opts):
+    with engine.options(**opts):  # hlc_ctx_set_option: the context's tunables for this call
         return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
@@ -47,9 +36,9 @@ def test_gpu_host_entry_random_schedules(engine, big_byz):
         if rnd.random() < 0.5:
             sub = sub[np.array(rnd.sample(range(sub.shape[0]), sub.shape[0]))]
         sizes = [rnd.choice([1, 7, 64, 65, 100, 333, 640, 1000]) for _ in range(rnd.randrange(1, 4))]
-        env = {"HLC_SPLIT_VOTES": ",".join(map(str, sizes)), "HLC_REST_PIECES": str(rnd.randrange(1, 9)),
-               "HLC_FIRST_BATCH": str(rnd.randrange(1, 9)), "HLC_HOST_THREADS": str(rnd.randrange(1, 13))}
-        ref = _call(engine, b, sub, now, {"HLC_SPLIT_VOTES": "0"})
+        env = {"split_votes": sizes, "rest_pieces": rnd.randrange(1, 9), "first_batch": rnd.randrange(1, 9),
+               "host_threads": rnd.randrange(1, 13)}
+        ref = _call(engine, b, sub, now, {"split_votes": 0})
         got = _call(engine, b, sub, now, env)
         for x, y in zip(ref, got):
             assert np.array_equal(x, y), (trial, env, p0, p1)
@@ -69,17 +58,9 @@ def test_gpu_verify_batch_random_schedules(engine):
     for trial in range(10):
         n = rnd.randrange(1, len(ids) + 1)
         sizes = [rnd.choice([1, 5, 64, 100, 257]) for _ in range(rnd.randrange(1, 4))]
-        env = {"HLC_SPLIT_VOTES": ",".join(map(str, sizes)), "HLC_REST_PIECES": str(rnd.randrange(1, 9)),
-               "HLC_FIRST_BATCH": str(rnd.randrange(1, 9)), "HLC_HOST_THREADS": str(rnd.randrange(1, 13))}
-        old = {k: os.environ.get(k) for k in KNOBS}
-        os.environ.update(env)
-        try:
+        env = {"split_votes": sizes, "rest_pieces": rnd.randrange(1, 9), "first_batch": rnd.randrange(1, 9),
+               "host_threads": rnd.randrange(1, 13)}
+        with engine.options(**env):
             st, addr = engine.eth_verify_batch(ids[:n], pays[:n], sigs[:n])
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
         assert [int(x) for x in st] == exp_st[:n], (trial, env, n)
         assert [a.tobytes() for a in addr] == exp_addr[:n], (trial, env, n)

@@ -25,14 +25,11 @@ HLC_EINVAL = -1  # include/hlc.h
 
 
 def _run(engine, batch, desc, now, split, pieces=None):
-    os.environ["HLC_SPLIT_VOTES"] = str(split)
+    opts = {"split_votes": str(split)}
     if pieces is not None:
-        os.environ["HLC_REST_PIECES"] = str(pieces)
-    try:
+        opts["rest_pieces"] = pieces
+    with engine.options(**opts):
         return engine.validate_proposals(batch, desc, now, want_votes=True, want_recovered=True)
-    finally:
-        os.environ.pop("HLC_SPLIT_VOTES", None)
-        os.environ.pop("HLC_REST_PIECES", None)
 
 
 @pytest.fixture(scope="module")
@@ -61,12 +58,9 @@ def test_gpu_host_entry_first_range_prep_batch(engine, byz, first_batch):
     """The first range's k_rec_prep with 1, 2, 3 or 8 votes per lane (HLC_FIRST_BATCH: the lane count
     and the prefix-product layout follow it) equals the oracle bit for bit."""
     b, d, now = byz
-    os.environ["HLC_FIRST_BATCH"] = first_batch
-    try:
+    with engine.options(first_batch=int(first_batch)):
         got = _run(engine, b, d, now, "100,150")
         one = _run(engine, b, d, now, "0")
-    finally:
-        os.environ.pop("HLC_FIRST_BATCH", None)
     for x, y in zip(one, got):
         assert np.array_equal(x, y)
     cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
@@ -110,13 +104,10 @@ def _raw_call(engine, batch, desc, now, split):
     rec = np.full((n, 20), 0xAB, np.uint8)
     view = batch.view()
     desc = np.ascontiguousarray(desc)
-    os.environ["HLC_SPLIT_VOTES"] = str(split)
-    try:
+    with engine.options(split_votes=str(split)):
         rc = engine.lib.hlc_validate_proposals(engine.ctx, ctypes.byref(view), proposals_ptr(desc), desc.shape[0], now,
                                                results_ptr(res), _ffi.ptr(st, ctypes.c_uint8),
                                                _ffi.ptr(rs, ctypes.c_uint8), _ffi.ptr(rec, ctypes.c_uint8))
-    finally:
-        os.environ.pop("HLC_SPLIT_VOTES", None)
     return rc, (res.view(np.uint8), st, rs, rec)
 
 
@@ -252,12 +243,9 @@ def test_gpu_host_entry_split_registration_is_staged(engine, byz):
     cres, cvst, cvrs, crec = coracle.validate_proposals(b, d, now, threads=8)
 
     def run():
-        os.environ["HLC_HOST_TRACE"] = "2"
-        try:
+        with engine.options(host_trace=2):
             got = engine.validate_proposals(cb, d, now, want_votes=True, want_recovered=True)
             mask = int(engine.last_host_trace()["facts"]["pinned_mask"])
-        finally:
-            os.environ.pop("HLC_HOST_TRACE", None)
         assert np.array_equal(got[0], cres) and np.array_equal(got[1], cvst)
         assert np.array_equal(got[2], cvrs) and np.array_equal(got[3], crec)
         return (mask >> 4) & 1

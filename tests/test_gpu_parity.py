@@ -144,17 +144,14 @@ def test_gpu_verify_batch_sizes(engine):
 
 @pytest.mark.parametrize("split", ["0", "100", "700", "1", "200,300", "1,1,64"])
 def test_gpu_verify_batch_split_schedules(engine, split):
-    """hlc_eth_verify_batch stages the items in recovery ranges (HLC_SPLIT_VOTES: the sizes of the
+    """hlc_eth_verify_batch stages the items in recovery ranges (HLC_OPT_SPLIT_VOTES: the sizes of the
     ranges before the last), each range's k_rec_prep + k_rec_main behind its upload on two streams in
     turn: every schedule equals the oracle item for item (payloads of 0..299 bytes: 1-3 digit
     EIP-191 lengths, 1-3 keccak blocks)."""
     ids, pays, sigs = _mutated_items(1500, 11)
     exp_st, exp_addr = _oracle_verify(ids, pays, sigs)
-    os.environ["HLC_SPLIT_VOTES"] = split
-    try:
+    with engine.options(split_votes=split):
         st, addr = engine.eth_verify_batch(ids, pays, sigs)
-    finally:
-        os.environ.pop("HLC_SPLIT_VOTES", None)
     assert [int(x) for x in st] == exp_st
     assert [a.tobytes() for a in addr] == exp_addr
 
@@ -173,13 +170,9 @@ def test_gpu_verify_batch_rejects_out_of_arena_outputs_untouched(engine):
         o[which * n + n - 1] = (1 << 40) if far else arena.size + 1
         st = np.full(n, 0xAB, np.uint8)
         addr = np.full((n, 20), 0xAB, np.uint8)
-        os.environ["HLC_SPLIT_VOTES"] = "100"
-        try:
-            with pytest.raises(_ffi.HlcError):
-                engine.eth_verify_arrays(arena, o[:n], lens[:n], o[n:2 * n], lens[n:2 * n], o[2 * n:], lens[2 * n:],
-                                         out=(st, addr))
-        finally:
-            os.environ.pop("HLC_SPLIT_VOTES", None)
+        with engine.options(split_votes=100), pytest.raises(_ffi.HlcError):
+            engine.eth_verify_arrays(arena, o[:n], lens[:n], o[n:2 * n], lens[n:2 * n], o[2 * n:], lens[2 * n:],
+                                     out=(st, addr))
         assert (st == 0xAB).all() and (addr == 0xAB).all()
     st, addr = engine.eth_verify_arrays(arena, offs[:n], lens[:n], offs[n:2 * n], lens[n:2 * n], offs[2 * n:],
                                         lens[2 * n:])

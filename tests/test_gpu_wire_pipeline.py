@@ -28,19 +28,13 @@ pytestmark = pytest.mark.gpu
 THREADS = max(1, min(16, os.cpu_count() or 1))
 
 
-@contextlib.contextmanager
-def _env(**kw):
-    old = {k: os.environ.get(k) for k in kw}
-    try:
-        for k, v in kw.items():
-            os.environ[k] = str(v)
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+_OPT = {"HLC_WIRE_SPLIT_BYTES": "wire_split_bytes", "HLC_WIRE_CHUNK": "wire_chunk",
+        "HLC_WIRE_PIPELINE": "wire_pipeline", "HLC_HOST_TRACE": "host_trace"}
+
+
+def _env(engine, **kw):
+    """The context's wire tunables for a block (hlc_ctx_set_option), named by their environment defaults."""
+    return engine.options(**{_OPT[k]: (v if k == "HLC_WIRE_SPLIT_BYTES" else int(v)) for k, v in kw.items()})
 
 
 def _scope(n, gossipsub=True):
@@ -63,10 +57,10 @@ def _both(engine, wire, off, lens, scope, now, split="4096,8192", chunk=3000, mi
     """(pipelined, unpipelined) outcomes of one call; asserts they are equal bit for bit, and that the
     pipelined call took at least `min_ranges` message ranges (its HLC_HOST_TRACE facts).  Returns
     (results, wire info, decoded votes, the pipelined call's trace facts)."""
-    with _env(HLC_WIRE_SPLIT_BYTES=split, HLC_WIRE_CHUNK=chunk, HLC_WIRE_PIPELINE=1, HLC_HOST_TRACE=2):
+    with _env(engine, HLC_WIRE_SPLIT_BYTES=split, HLC_WIRE_CHUNK=chunk, HLC_WIRE_PIPELINE=1, HLC_HOST_TRACE=2):
         pr, pw, pn = engine.validate_wire_proposals(wire, off, lens, scope, now)
         facts = engine.last_host_trace()["facts"]
-    with _env(HLC_WIRE_PIPELINE=0):
+    with _env(engine, HLC_WIRE_PIPELINE=0):
         ur, uw, un = engine.validate_wire_proposals(wire, off, lens, scope, now)
     assert pn == un, f"decoded votes {pn} != {un}"
     bad = np.nonzero(pr != ur)[0]
@@ -219,7 +213,7 @@ def test_gpu_wire_pipeline_bad_extent_outputs_untouched(engine):
     resb = np.full(4 * 16, 0xAB, np.uint8)
     wi = np.full(4 * 48, 0xCD, np.uint8)
     nv = c_uint64(77)
-    with _env(HLC_WIRE_SPLIT_BYTES="512", HLC_WIRE_CHUNK=512):
+    with _env(engine, HLC_WIRE_SPLIT_BYTES="512", HLC_WIRE_CHUNK=512):
         rc = engine.lib.hlc_validate_wire_proposals(
             engine.ctx, _ffi.ptr(wire, c_uint8), wire.size, _ffi.ptr(off, c_uint64), _ffi.ptr(lens, c_uint32), 4,
             c_void_p(scope.ctypes.data), scope.shape[0], w.now, c_void_p(resb.ctypes.data), c_void_p(wi.ctypes.data),

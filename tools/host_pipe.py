@@ -71,10 +71,10 @@ def main() -> int:
     settings = [(sp, th, nt, bd) for sp in a.split.split("/") for th in a.threads.split(",")
                 for nt in a.nt.split(",") for bd in a.bind.split(",")] * max(1, a.rounds)
     for sp, th, nt, bd in settings:
-        os.environ["HLC_NT_COPY"] = nt
-        os.environ["HLC_POOL_BIND"] = bd
-        os.environ["HLC_SPLIT_VOTES"] = sp
-        os.environ["HLC_HOST_THREADS"] = th
+        eng.set_option("nt_copy", int(nt))  # hlc_ctx_set_option (the environment is read at creation only)
+        eng.set_option("pool_bind", int(bd))
+        eng.set_option("split_votes", sp)
+        eng.set_option("host_threads", int(th))
         r = eng.validate_proposals(b, d, db.now, want_votes=True)
         if ref is None:
             ref = r
@@ -92,6 +92,9 @@ def main() -> int:
         import threading
         engs = [eng] + [Engine(0) for _ in range(a.contexts - 1)]
         for e in engs[1:]:
+            for k in ("nt_copy", "pool_bind", "host_threads"):
+                e.set_option(k, eng.get_option(k))
+            e.set_option("split_votes", settings[-1][0])
             e.validate_proposals(b, d, db.now, want_votes=True)  # warm: workspace, staging, streams
         go = threading.Barrier(a.contexts + 1)
         times = [0.0] * a.contexts
@@ -110,8 +113,8 @@ def main() -> int:
         for x in th:
             x.join()
         el = max(times)
-        print(json.dumps({"contexts": a.contexts, "threads_per_context": int(os.environ["HLC_HOST_THREADS"]),
-                          "split": os.environ["HLC_SPLIT_VOTES"], "calls": a.contexts * a.steps,
+        print(json.dumps({"contexts": a.contexts, "threads_per_context": eng.get_option("host_threads"),
+                          "split": settings[-1][0], "calls": a.contexts * a.steps,
                           "votes_per_s_aggregate": a.contexts * a.steps * b.n / el,
                           "ms_per_call_mean": el / a.steps * 1e3}), flush=True)
         for e in engs[1:]:

@@ -64,19 +64,17 @@ def main() -> int:
                 for th in a.threads.split(",") for nt in a.nt.split(",") for bd in a.bind.split(",")
                 for wk in a.walk.split(",")] * max(1, a.rounds)
     for sp, ch, th, nt, bd, wk in settings:
-        if wk:
-            os.environ["HLC_WIRE_WALK"] = wk
-        else:
-            os.environ.pop("HLC_WIRE_WALK", None)
-        os.environ["HLC_NT_COPY"] = nt
-        os.environ["HLC_POOL_BIND"] = bd
-        os.environ["HLC_WIRE_PIPELINE"] = "0" if sp == "plain" else "1"
+        # hlc_ctx_set_option (the environment is read at context creation only)
+        eng.set_option("wire_walk", {"lane": 0, "lds": 1}.get(wk, -1))
+        eng.set_option("nt_copy", int(nt))
+        eng.set_option("pool_bind", int(bd))
+        eng.set_option("wire_pipeline", 0 if sp == "plain" else 1)
         if sp == "default":
-            os.environ.pop("HLC_WIRE_SPLIT_BYTES", None)
+            eng.set_option("wire_split_bytes", -1)
         elif sp != "plain":
-            os.environ["HLC_WIRE_SPLIT_BYTES"] = sp
-        os.environ["HLC_WIRE_CHUNK"] = ch
-        os.environ["HLC_HOST_THREADS"] = th
+            eng.set_option("wire_split_bytes", sp)
+        eng.set_option("wire_chunk", int(ch))
+        eng.set_option("host_threads", int(th))
         res, winfo, nv = eng.validate_wire_proposals(wire, off, lens, scope, db.now)
         assert np.array_equal(res, ref) and nv == db.n and (winfo["decode_status"] == 0).all(), sp
         t = time.perf_counter()
@@ -88,9 +86,8 @@ def main() -> int:
                "ms_per_call": el * 1e3,
                "votes_per_s": db.n / el, "wire_bytes": int(wire.size), "outputs_equal_device_soa_path": True}
         if a.trace and sp != "plain":
-            os.environ["HLC_HOST_TRACE"] = "2"
-            eng.validate_wire_proposals(wire, off, lens, scope, db.now)
-            os.environ.pop("HLC_HOST_TRACE")
+            with eng.options(host_trace=2):
+                eng.validate_wire_proposals(wire, off, lens, scope, db.now)
             row["trace"] = eng.last_host_trace()
         print(json.dumps(row), flush=True)
     if a.device_walk:
@@ -98,7 +95,7 @@ def main() -> int:
         dw = DeviceWire(np.asarray(wire), off, lens, scope, db.now)
         for _ in range(max(1, a.rounds)):
             for wk in a.device_walk.split(","):
-                os.environ["HLC_WIRE_WALK"] = wk
+                eng.set_option("wire_walk", {"lane": 0, "lds": 1}.get(wk, -1))
                 eng.validate_wire_proposals_device(dw)
                 torch.cuda.synchronize()
                 assert np.array_equal(dw.results_numpy(), ref), wk
@@ -109,7 +106,7 @@ def main() -> int:
                 el = (time.perf_counter() - t) / a.steps
                 print(json.dumps({"device_resident_walk": wk, "ms_per_call": el * 1e3, "votes_per_s": db.n / el}),
                       flush=True)
-        os.environ.pop("HLC_WIRE_WALK", None)
+        eng.set_option("wire_walk", -1)
     if arena is not None:
         arena.close()
     eng.close()
