@@ -1845,6 +1845,18 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     }
     return 0;
   };
+  // Workspace that a call of this size needed before (wire_hint: the most votes a call on this context
+  // decoded) is sized here, before the first upload: a DBuf that grows inside decode() frees its old
+  // block, and hipFree waits for the whole device -- ranges already in flight included.  A
+  // context's first call, or one larger than any before it, still grows them on the way.
+  if (c->wire_hint) {
+    CHK(size_votes(std::min(U / 2 + 1, c->wire_hint + c->wire_hint / 4 + 4096)));
+    for (size_t k = 0; k < R; ++k) {
+      const uint64_t share = (uint64_t)((double)c->wire_hint * (double)(ub[k + 1] - ub[k]) / (double)std::max<uint64_t>(U, 1));
+      CHK(c->rec_works[k]->ensure(
+          hlc::recover_range_words(std::min((ub[k + 1] - ub[k]) / 2 + 1, share + share / 4 + 4096)) * 4));
+    }
+  }
   // 2. the wire bytes, range by range, piece by piece
   for (size_t k = 0; k < R; ++k) {
     for (uint64_t lo = ub[k]; lo < ub[k + 1];) {
@@ -1985,8 +1997,8 @@ int hlc_ctx_set_option(hlc_ctx* ctx, int option, int64_t value) {
       o.wire_split_bytes.push_back((uint64_t)value);
       break;
     case HLC_OPT_WIRE_CHUNK:
-      if (value < 4096) return bad();
-      o.wire_chunk = (uint64_t)value;
+      if (value < 1) return bad();
+      o.wire_chunk = std::max<uint64_t>((uint64_t)value, 4096);  // (as the environment's value: at least 4 KiB)
       break;
     case HLC_OPT_REC_FORCE_EXACT: o.rec_force_exact = value != 0; break;
     case HLC_OPT_SERIAL_STAGES: o.serial_stages = value != 0; break;

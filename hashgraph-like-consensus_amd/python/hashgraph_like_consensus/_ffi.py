@@ -298,22 +298,42 @@ def ptr(arr, ctype):
     return arr.ctypes.data_as(POINTER(ctype))
 
 
+class _HostBlock:
+    """One hlc_host_alloc block; freed when the last reference goes.  It references nothing that
+    references it back, so the free happens by reference counting, not at a garbage-collection pass."""
+
+    def __init__(self, lib, nbytes: int):
+        self._lib = lib
+        self.p = c_void_p()
+        check(lib.hlc_host_alloc(max(int(nbytes), 1), ctypes.byref(self.p)))
+
+    def free(self):
+        if self.p is not None and self.p.value:
+            self._lib.hlc_host_free(self.p)
+        self.p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class PinnedArena:
     """Page-locked host memory from hlc_host_alloc, handed out as numpy arrays (`take`): input
-    arrays built here reach the device without the host-buffer entries' staging copy.  Freed with
-    the object, which every array taken from it keeps alive; an explicit close() frees it at once
-    (only when none of its arrays is used again)."""
+    arrays built here reach the device without the host-buffer entries' staging copy.  The block is
+    freed when the arena and every array taken from it are gone (each array's base chain holds the
+    block, not the arena: no reference cycle); an explicit close() frees it at once (only
+    when none of its arrays is used again)."""
 
     def __init__(self, nbytes: int):
         import numpy as np
         self._lib = load_library()
-        self._p = c_void_p()
-        check(self._lib.hlc_host_alloc(max(int(nbytes), 1), ctypes.byref(self._p)))
         self.nbytes = int(nbytes)
+        self._block = _HostBlock(self._lib, self.nbytes)
+        self._p = self._block.p
         buf = (ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self._p.value)
-        # every array carved out of the arena has this buffer at the root of its base chain: the
-        # arena stays alive (and its memory allocated) while any of them does (ADVICE r04)
-        buf._owner = self
+        buf._owner = self._block  # the arrays' base chain keeps the block (not the arena) alive
         self._u8 = np.frombuffer(buf, dtype=np.uint8)
         self._used = 0
 
@@ -332,12 +352,5 @@ class PinnedArena:
         return a
 
     def close(self):
-        if self._p is not None and self._p.value:
-            self._lib.hlc_host_free(self._p)
+        self._block.free()
         self._p = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass

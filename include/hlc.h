@@ -249,7 +249,8 @@ void hlc_host_free(void* p);
                                       (HLC_WIRE_SPLIT_BYTES, a list; 8, 16, 24, 32 MiB) */
 #define HLC_OPT_WIRE_FRONT_CAP 9   /* waves per recovery grid of every message range but the last; 0: full
                                       grids (HLC_WIRE_FRONT_CAP; default 1536) */
-#define HLC_OPT_WIRE_CHUNK 10      /* bytes per wire staging piece, >= 4096 (HLC_WIRE_CHUNK; 4 MiB) */
+#define HLC_OPT_WIRE_CHUNK 10      /* bytes per wire staging piece, at least 4096 (a smaller value reads as
+                                      4096; HLC_WIRE_CHUNK; 4 MiB) */
 #define HLC_OPT_REC_FORCE_EXACT 11 /* 1: every vote through the recovery's checked chains (tests; 0) */
 #define HLC_OPT_SERIAL_STAGES 12   /* 1: the recovery's prep + main after the prehash on one stream
                                       (isolated kernel traces; HLC_SERIAL_STAGES; 0) */

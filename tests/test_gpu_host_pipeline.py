@@ -262,3 +262,22 @@ def test_gpu_host_entry_split_registration_is_staged(engine, byz):
         finally:
             for o, _ in regs:
                 assert hip.hipHostUnregister(ctypes.c_void_p(base + o)) == 0
+
+
+def test_gpu_pinned_arena_freed_without_gc(engine):
+    """the page-locked block of a PinnedArena is released by reference counting once the arena
+    and its arrays are gone -- no reference cycle waiting for a garbage-collection pass."""
+    import gc
+    import weakref
+    gc.disable()
+    try:
+        arena = _ffi.PinnedArena(1 << 20)
+        a = arena.take((1000,), np.uint32)
+        a[:] = 7
+        block = weakref.ref(arena._block)
+        del arena
+        assert block() is not None and int(a.sum()) == 7000  # the array keeps the block alive
+        del a
+        assert block() is None  # freed (hlc_host_free) at once
+    finally:
+        gc.enable()

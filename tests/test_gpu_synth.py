@@ -4,8 +4,9 @@
   byte: ids, timestamps, choices, arena (owners, chained vote hashes, RFC 6979 signatures),
   offsets, proposal records -- including non-zero shard starts and the j // 1024 timestamp step.
 * Config 4 (100,000,000 votes = 1,562,500 proposals x 64 sharded by proposal over
-  8 GPUs): one rank's whole shard (195,313 proposals, 12.5M votes) generated on the device and
-  validated through hlc_validate_proposals_device; a seeded 0.1 % sample of whole proposals is
+  8 GPUs): each of the 8 rank shards (195,313 proposals, 12.5M votes; the last 195,309) generated on
+  the device and validated through hlc_validate_proposals_device, one after another on this GPU -- all
+  100M votes; full-size tally and counter properties per shard; a seeded 0.1 % sample of whole proposals is
   copied back and checked bit for bit against the C oracle, and three sampled proposals against
   the Python generator.  Proposals are independent (/root/reference/src/service.rs:263-279), so a
   shard is the whole job of its rank.
@@ -59,8 +60,12 @@ def test_gpu_synth_shard_starts():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("rank", [0, 7])
+@pytest.mark.parametrize("rank", list(range(CONFIG4_RANKS)))
 def test_gpu_config4_rank_shard(engine, rank):
+    """Every rank shard of config 4 in turn: all 100,000,000 votes through the HIP path.  Full-size
+    properties per shard (every vote valid, every proposal Ok with its 64 votes, each proposal's YES tally
+    equal to its votes' choices, each transition the reference's tally of that count, the outcome
+    counters of the exchange step equal to the statuses), plus the 0.1 % oracle sample."""
     import torch
     start, P = _shard(rank)
     V = 64
@@ -74,6 +79,20 @@ def test_gpu_config4_rank_shard(engine, rank):
     assert db.n == P * V
     assert (st == 0).all(), f"{int((st != 0).sum())} valid votes rejected"
     assert (res["status"] == 0).all() and (res["total"] == V).all()
+    # full-size tally properties: YES = the proposal's choices; transition = calculate_consensus_result
+    yes = db.choice_numpy().reshape(P, V).astype(np.int64).sum(axis=1)
+    assert np.array_equal(res["yes"].astype(np.int64), yes)
+    want = {}
+    for y in np.unique(yes):
+        r = coracle.consensus_result(V, int(y), V, 2.0 / 3.0, True, False)
+        want[int(y)] = 0 if r is None else (2 if r else 1)
+    assert np.array_equal(res["transition"], np.vectorize(want.get)(yes).astype(np.uint8))
+    # the exchange step's outcome counters (hlc_outcome_counts_device) on the whole shard
+    counts = torch.zeros(64, dtype=torch.int64, device=db.device)
+    engine.outcome_counts_device(db.status.data_ptr(), db.n, db.results.data_ptr(), P, counts.data_ptr())
+    torch.cuda.synchronize()
+    c = counts.cpu().numpy()
+    assert c[0] == db.n and c[1:32].sum() == 0 and c[32] == P and c[33:].sum() == 0
     # 0.1 % seeded sample of whole proposals, bit for bit against the C oracle
     rng = np.random.default_rng(0x484C4304 + rank)
     pick = np.sort(rng.choice(P, size=max(1, P // 1000), replace=False))

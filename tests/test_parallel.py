@@ -239,3 +239,91 @@ def test_gloo_world2_rank_shards_gather_and_counters():
         assert counters["rejected_votes_by_status"] == {str(k): int(hist_v[k]) for k in range(1, 32) if hist_v[k]}
         assert counters["proposals_ok"] == int(hist_p[0])
         assert sum(counters["rejected_votes_by_status"].values()) > 0
+
+
+# ---- config 4's true shard counts over 8 ranks ------------------------------------
+C4_PROPOSALS, C4_RANKS, C4_V = 1_562_500, 8, 64
+
+
+def _c4_span(rank: int):
+    per = -(-C4_PROPOSALS // C4_RANKS)
+    start = min(rank * per, C4_PROPOSALS)
+    return start, min(per, C4_PROPOSALS - start)
+
+
+def _c4_outputs(rank: int):
+    """A deterministic stand-in for rank `rank`'s validated shard: 16-byte result rows (status, bad
+    index, yes, total keyed to the global proposal index) and per-vote statuses with a sprinkling of
+    reject codes -- what the exchange step moves, at the true config-4 proposal counts."""
+    from hashgraph_like_consensus import _ffi
+    start, P = _c4_span(rank)
+    g = np.arange(start, start + P, dtype=np.int64)
+    res = np.zeros(P, _ffi.RESULT_DTYPE)
+    res["status"] = np.where(g % 97 == 0, 6, np.where(g % 89 == 0, 13, 0)).astype(np.uint8)
+    res["transition"] = (g % 3).astype(np.uint8) * (res["status"] == 0)
+    res["bad_index"] = np.where(res["status"] != 0, g % 64, 0xFFFFFFFF).astype(np.uint32)
+    res["yes"] = (g * 7 % 65).astype(np.uint32)
+    res["total"] = C4_V
+    st = np.zeros(P * C4_V, np.uint8)
+    bad = np.nonzero(res["status"] == 6)[0]
+    st[bad * C4_V + (g[bad] % 64)] = 6
+    return res, st
+
+
+def _worker_c4(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "hashgraph-like-consensus_amd", "python"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from hashgraph_like_consensus.parallel import ShardExchange
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res, st = _c4_outputs(rank)
+        P = res.shape[0]
+        max_p = max(_c4_span(r)[1] for r in range(world))
+        ex = ShardExchange(max_p, world, "cpu")
+        ex(torch.from_numpy(res.view(np.uint8).copy()), torch.from_numpy(st), P, st.shape[0])
+        pc = torch.tensor([P], dtype=torch.int64)
+        pcs = [torch.zeros_like(pc) for _ in range(world)]
+        dist.all_gather(pcs, pc)
+        counts = [int(x.item()) for x in pcs]
+        rows = ex.results(counts)
+        q.put((rank, counts, rows.tobytes() == b"".join(_c4_outputs(r)[0].tobytes() for r in range(world)),
+               ex.summary()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world8_config4_counts_gather_and_counters():
+    """The exchange step of an 8-GPU config-4 run at its true shard sizes (7 x 195,313 + 195,309
+    proposals, 12.5M per-vote statuses per rank), over gloo: every rank receives all 1,562,500 result
+    rows in rank order, byte for byte, and the all-reduced counters equal the union's histograms."""
+    hist_v = np.zeros(32, np.int64)
+    hist_p = np.zeros(32, np.int64)
+    for r in range(C4_RANKS):
+        res, st = _c4_outputs(r)
+        hist_v += np.bincount(st, minlength=32)[:32]
+        hist_p += np.bincount(res["status"], minlength=32)[:32]
+    assert int(hist_v.sum()) == C4_PROPOSALS * C4_V
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_c4, args=(r, C4_RANKS, port, q)) for r in range(C4_RANKS)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(g[0] for g in got) == list(range(C4_RANKS))
+    for rank, counts, rows_ok, summary in got:
+        assert counts == [195_313] * 7 + [195_309] and sum(counts) == C4_PROPOSALS
+        assert rows_ok, f"rank {rank}: gathered rows differ"
+        assert summary["verified_votes"] == int(hist_v[0])
+        assert summary["rejected_votes_by_status"] == {str(k): int(hist_v[k]) for k in range(1, 32) if hist_v[k]}
+        assert summary["proposals_ok"] == int(hist_p[0])
+        assert summary["proposals_by_status"] == {str(k): int(hist_p[k]) for k in range(1, 32) if hist_p[k]}

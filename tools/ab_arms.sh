@@ -14,7 +14,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 MODE=${AB_MODE:-headline}
-LEGS="--no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e"
+LEGS="--no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e --no-config4-shard"
 for round in 1 2 3; do
   for arm in default "$@"; do
     v=${arm%%=*}; ENVS=""
@@ -24,11 +24,11 @@ for round in 1 2 3; do
     O=gpurun_out/ab_${MODE}_$v
     case $MODE in
     headline)
-      env $ENVS timeout -k 10 200 python bench.py --steps 150 --warmup 50 $LEGS > $O.json 2> $O.err || { tail $O.err; exit 1; }
-      python -c "import json;d=json.load(open('$O.json'));print('$round $v', round(d['value']), 'votes/s rec_ms', round(d['roofline']['kernel_ms_avg'],3), 'step_ms', round(d['ms_per_step'],3))" ;;
+      HLC_BENCH_DETAIL=$PWD/$O.detail.json env $ENVS timeout -k 10 200 python bench.py --steps 150 --warmup 50 $LEGS > $O.json 2> $O.err || { tail $O.err; exit 1; }
+      python -c "import json;d=json.load(open('$O.json'));print('$round $v', round(d['value']), 'votes/s rec_ms', round(d['roofline']['kernel_ms_avg'],3), 'step_ms', round(d['ms_per_step'],3), 'GHz', d['roofline'].get('live_k_rec_main_GHz'))" ;;
     legs)
-      env $ENVS timeout -k 10 300 python bench.py --steps 20 --warmup 5 ${LEGS/--no-config5/} > $O.json 2> $O.err || { tail $O.err; exit 1; }
-      python -c "import json;d=json.load(open('$O.json'));print('$round $v headline', round(d['value']), 'config5', round(d['config5']['value']), 'votes/s')" ;;
+      HLC_BENCH_DETAIL=$PWD/$O.detail.json env $ENVS timeout -k 10 300 python bench.py --steps 20 --warmup 5 ${LEGS/--no-config5/} > $O.json 2> $O.err || { tail $O.err; exit 1; }
+      python -c "import json;d=json.load(open('$O.json'));print('$round $v headline', round(d['value']), 'config5', round(d['legs']['config5']), 'votes/s')" ;;
     host)
       env $ENVS timeout -k 10 200 python tools/host_pipe.py --threads 8 --steps 20 > $O.txt 2> $O.err || { tail $O.err; exit 1; }
       python -c "import json;d=json.loads(open('$O.txt').read().splitlines()[-1]);print('$round $v host', round(d['votes_per_s']), 'votes/s', round(d['ms_per_call'],3), 'ms')" ;;

@@ -12,7 +12,7 @@ set -o pipefail
 TAG=${1:-r04}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p $OUT
-LEGS="--no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e"
+LEGS="--no-cpu-baseline --no-config3 --no-config5 --no-wire --no-stream --no-e2e --no-config4-shard"
 BENCH="$PWD/bench.py --steps 20 --warmup 5 $LEGS"
 PBENCH="$PWD/bench.py --steps 3 --warmup 1 $LEGS"
 C3="$PWD/tools/config3_time.py 3"
