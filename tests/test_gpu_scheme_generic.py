@@ -227,3 +227,29 @@ def test_gpu_stub_streaming_matches_oracle(engine):
     assert np.array_equal(sarr, sessions_array(ss_ref))
     codes = {o[0] for o in out_ref}
     assert {po.OK, po.DUPLICATE_VOTE, po.SIGNATURE_SCHEME, po.INVALID_VOTE_SIGNATURE, 19} <= codes
+
+
+def test_gpu_stub_proposal_bytes_matches_oracle(engine):
+    """Gossip bytes under the stub scheme: ConsensusService(scheme=StubSigner).process_incoming_proposal_bytes
+    decodes on the device and validates with the scheme's verdicts; every outcome equals pyoracle's
+    from_proposal under stub_verify."""
+    from hashgraph_like_consensus.protos import encode_proposal
+    props, batch, desc, now, kinds = stub_workload(30, 6, 31, fraction=0.3)
+    msgs = []
+    for p in props:
+        pp = Proposal(name=p.name, payload=p.payload, proposal_id=p.proposal_id, proposal_owner=p.proposal_owner,
+                      votes=[Vote(**v.__dict__) for v in p.votes], expected_voters_count=p.expected_voters_count,
+                      round=1, timestamp=p.timestamp, expiration_timestamp=p.expiration_timestamp,
+                      liveness_criteria_yes=p.liveness_criteria_yes)
+        msgs.append(encode_proposal(pp))
+    svc = ConsensusService(engine, ConsensusConfig.gossipsub(), scheme=StubSigner)
+    outs = svc.process_incoming_proposal_bytes("stub-wire", msgs, now)
+    cfg = po.ConsensusConfig.gossipsub()
+    for p, o in zip(props, outs):
+        ref = po.from_proposal(p, cfg, now, scheme=po.stub_verify)
+        got = 0 if o.error is None else o.error.code
+        assert got == ref.status, (p.proposal_id, got, ref.status)
+        assert o.bad_index == ref.bad_index
+        if ref.status == po.OK:
+            assert (o.yes, o.total) == (ref.yes, ref.total)
+    assert len({0 if o.error is None else o.error.code for o in outs}) >= 3
