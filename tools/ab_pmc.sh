@@ -22,7 +22,7 @@ import csv, glob, os, sys
 out, arm = sys.argv[1], sys.argv[2]
 def per_launch(name, counter):
     rows = [r for f in glob.glob(os.path.join(out, name, "**", "*counter_collection.csv"), recursive=True)
-            for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("k_rec_main") and r["Counter_Name"] == counter]
+            for r in csv.DictReader(open(f)) if "k_rec_main(" in r["Kernel_Name"] and r["Counter_Name"] == counter]
     by = {}
     for r in rows:
         by.setdefault(r["Dispatch_Id"], 0.0)
@@ -35,7 +35,8 @@ rd, _ = per_launch("req", "TCC_EA0_RDREQ")
 r128, _ = per_launch("req", "TCC_EA0_RDREQ_128B")
 r32, _ = per_launch("req", "TCC_EA0_RDREQ_32B")
 rbytes = 128 * r128 + 64 * (rd - r128 - r32) + 32 * r32
-print(f"{arm}: k_rec_main launches {k}, VALU wave-instructions/vote {valu / V:.0f}, read B/vote {rbytes / V:.0f}, "
-      f"write B/vote {wr * 1024 / V:.0f} (WRITE_SIZE KiB x 1024)")
+print(f"{arm}: k_rec_main launches {k}, VALU instructions/vote {valu * 64 / V:.0f} (SQ_INSTS_VALU wave-instructions "
+      f"x 64 lanes / votes), read B/vote {rbytes / V:.0f} (L2 read requests by size), write B/vote {wr * 1024 / V:.0f} "
+      f"(WRITE_SIZE)")
 PY
 done
