@@ -1360,6 +1360,12 @@ int validate_host(hlc_ctx* c, const hlc_votes* v, const hlc_proposal* props, uin
     for (int q = 0; q < 6; ++q) mask |= arr[q].pinned ? 1 << q : 0;
     tr.fact("pinned_mask", mask | (parr.pinned ? 64 : 0) | (arena_pinned ? 128 : 0));
     tr.fact("pool_cpus", (double)c->pool_cpus.size());
+    if (tr.on) {  // NUMA placement of the call: the arena, the staging buffer, the workers' node, the GPU's
+      tr.fact("arena_node", memory_node(v->bytes, blen));
+      tr.fact("staging_node", memory_node(st.P, o[10]));
+      tr.fact("pool_node", c->pool_node);
+      tr.fact("gpu_node", device_node(c->device));
+    }
   }
   CHK(stage_rows(st, pool, &parr, 1, 0, np));
   std::vector<int> bad(parts, 0);

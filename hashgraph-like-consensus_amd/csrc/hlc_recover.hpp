@@ -67,13 +67,8 @@ constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
 //    each access is one coalesced 256-B row per wave): the z-ratios of the table build;
 //  * per-lane contiguous R table (RTAB_WORDS words, 64-B entries read by four 16-B vector loads):
 //    entries are gathered at lane-dependent indices, so each lane's entry must be one block.
-#ifndef HLC_TAB128
-// A/B arm: 128-B entries holding x, y and beta x (lambda R's x) -- a b2 gather
-// reads beta x from the same line instead of multiplying by beta in the chain (26 fewer
-// multiplications per vote, 16 more at the build, twice the table bytes written and held in cache)
-#define HLC_TAB128 0
-#endif
-constexpr int RTAB_ENTRY = HLC_TAB128 ? 32 : 16;  // words per entry: x, y below 2^256 in 8 x 32 bits (64 B)
+// (128-B entries with beta x beside x and y measured -8.6%: DESIGN.md §8.1, profiles/r06/ab_tab128.txt)
+constexpr int RTAB_ENTRY = 16;                  // words per entry: x, y below 2^256 in 8 x 32 bits (64 B)
 constexpr int RTAB_WORDS = RTAB_N * RTAB_ENTRY; // per lane (affine, common-Z frame)
 constexpr int ZR_OFF = 0;                       // z-ratios of the table build (9 limbs each)
 constexpr int IL_WORDS = ZR_OFF + 9 * (RTAB_N - 1);       // interleaved words per lane
@@ -426,30 +421,9 @@ struct rtab29 {
   uint32_t* g;  // the lane's RTAB_WORDS workspace words
   // an entry of the build pass (rescaled and rewritten by store_final)
   HLC_DEV void store(int e, const fe29& x, const fe29& y) const { store_ge29_tab64(x, y, g + RTAB_ENTRY * e); }
-  // an entry in its final (common-Z) frame; HLC_TAB128: beta x beside it in the same 128-B line
-  HLC_DEV void store_final(int e, const fe29& x, const fe29& y) const {
-    store_ge29_tab64(x, y, g + RTAB_ENTRY * e);
-#if HLC_TAB128
-    fe29 beta, bx;
-    fe29_beta(beta);
-    fe29_mul_uniform(bx, x, beta);
-    uint32_t w[8];
-    fe29_pack256(w, bx);
-    uint4* p = reinterpret_cast<uint4*>(g + RTAB_ENTRY * e + 16);
-    p[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    p[1] = make_uint4(w[4], w[5], w[6], w[7]);
-#endif
-  }
+  // an entry in its final (common-Z) frame
+  HLC_DEV void store_final(int e, const fe29& x, const fe29& y) const { store_ge29_tab64(x, y, g + RTAB_ENTRY * e); }
   HLC_DEV void load(ge29& q, int e) const { load_ge29_tab64(q, g + RTAB_ENTRY * e); }
-#if HLC_TAB128
-  // lambda R's multiple: (beta x, y) of entry e, one 128-B line
-  HLC_DEV void load_lambda(ge29& q, int e) const {
-    const uint4* p = reinterpret_cast<const uint4*>(g + RTAB_ENTRY * e);
-    const uint4 c = p[2], d = p[3], a = p[4], b = p[5];
-    fe29_unpack256(q.x, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w);
-    fe29_unpack256(q.y, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w);
-  }
-#endif
 };
 
 HLC_DEV void store_fe29_ws(const fe29& x, uint32_t* ws, size_t stride) {
@@ -522,18 +496,12 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const r
     // the b2 entry is loaded before the b1 addition: its gather latency hides behind that addition
     const int d2 = digit_at(win, 1);
     ge29 g2;
-#if HLC_TAB128
-    tab.load_lambda(g2, index_of(d2));
-#else
     tab.load(g2, index_of(d2));
-#endif
     fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 1) != 0));
     gej29_madd<EXACT>(acc, acc, g);
     g = g2;
     d = d2;
-#if !HLC_TAB128
     fe29_mul_uniform(g.x, g.x, beta);
-#endif
     fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 2) != 0));
     gej29_madd<EXACT>(acc, acc, g);
   }
@@ -541,13 +509,8 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const r
   for (int k = 0; k < 2; ++k) {
     if (((skews >> k) & 1) == 0) continue;
     ge29 g;
-#if HLC_TAB128
-    if (k == 1) tab.load_lambda(g, 0);
-    else tab.load(g, 0);
-#else
     tab.load(g, 0);
     if (k == 1) fe29_mul_uniform(g.x, g.x, beta);
-#endif
     fe29_cneg_lazy(g.y, g.y, ((negs >> k) & 1) == 0);
     gej29_madd<EXACT>(acc, acc, g);
   }

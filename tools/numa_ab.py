@@ -109,7 +109,8 @@ def main() -> int:
                        "votes_per_s": b.n / el, "rest_staged_ms": tr["host"].get("rest_staged"),
                        "rest_landed_ms": tr["device"].get("rest_landed"),
                        "outputs_landed_ms": tr["device"].get("outputs_landed"),
-                       "pool_cpus": tr.get("facts", {}).get("pool_cpus")}
+                       **{k: tr.get("facts", {}).get(k) for k in ("pool_cpus", "pool_node", "arena_node", "staging_node",
+                                                                  "gpu_node")}}
                 rows.setdefault((name, bind), []).append(row["votes_per_s"])
                 print(json.dumps(row), flush=True)
     eng.set_option("pool_bind", 1)
