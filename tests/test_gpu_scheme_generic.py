@@ -253,3 +253,31 @@ def test_gpu_stub_proposal_bytes_matches_oracle(engine):
         if ref.status == po.OK:
             assert (o.yes, o.total) == (ref.yes, ref.total)
     assert len({0 if o.error is None else o.error.code for o in outs}) >= 3
+
+
+def test_gpu_stub_long_fields_take_the_general_path(engine):
+    """Votes whose SHA-256 input outgrows the fused kernel's LDS window (k_prehash_fused defers them to the
+    streaming k_prehash_stream) under the stub scheme: 300-byte parent hashes and identities, re-hashed and
+    re-signed, beside ordinary votes -- every status, reason and proposal outcome equals the C oracle's."""
+    import hashlib
+    from stub_scheme import _finish, pack
+    rnd = random.Random(91)
+    props, _, _, now, _ = stub_workload(24, 6, 41)
+    for p in props:
+        for j, v in enumerate(p.votes):
+            r = rnd.random()
+            if r < 0.25:
+                v.parent_hash = hashlib.sha256(bytes([j])).digest() * 10  # 320 bytes: no such vote
+            elif r < 0.4:
+                v.vote_owner = bytes(rnd.getrandbits(8) for _ in range(300))  # the stub's Err: not 8 bytes
+            else:
+                continue
+            _finish(v)
+            if j + 1 < len(p.votes):  # keep the next vote's received link to this one
+                nxt = p.votes[j + 1]
+                nxt.received_hash = v.vote_hash
+                _finish(nxt)
+    batch, desc = pack(props)
+    res, vst, vrs, _ = _compare(engine, batch, desc, now, "long fields")
+    codes = set(res["status"].tolist())
+    assert po.SIGNATURE_SCHEME in codes and po.PARENT_HASH_MISMATCH in codes, codes
