@@ -244,7 +244,7 @@ class HostPool {
 // context.
 struct Options {
   int host_threads = 16;      // HLC_OPT_HOST_THREADS: staging threads incl. the caller
-  int pool_bind = HLC_POOL_BIND_GPU;  // HLC_OPT_POOL_BIND
+  int pool_bind = HLC_POOL_BIND_NONE;  // HLC_OPT_POOL_BIND (unbound measured best)
   int nt_copy = 1;            // HLC_OPT_NT_COPY: non-temporal staging copies (AVX2)
   std::vector<uint64_t> split_votes{98304, 196608};  // HLC_OPT_SPLIT_VOTES (split_ranges)
   int host_trace = 0;         // HLC_OPT_HOST_TRACE
@@ -1012,11 +1012,12 @@ bool is_pinned(const void* p, size_t len) {
 // fired when the second k_rec_main ended, 4 ms after its DMA, and the prehash waited for it.  So the
 // upload stream takes the greatest priority and the second recovery stream the least: each draws
 // its queue from a pool of its own, apart from the normal-priority launch / aux streams.
-// The staging pool's workers are bound by HLC_OPT_POOL_BIND: to the CPUs of the GPU's NUMA node (their
+// The staging pool's workers are bound by HLC_OPT_POOL_BIND: not at all (the default: on two boxes,
+// near and far inputs, unbound staging was the fastest arm), to the CPUs of the GPU's NUMA node (their
 // copies then write the page-locked buffer from the socket the GPU hangs off; the DMA reads it from
 // there), or to those of the node the call's largest input (`src`, its arena) lives on (the copies then
 // read the caller's pages locally -- a cross-socket read costs more than a cross-socket write, DESIGN.md
-// §5), or not at all.  A node with fewer usable CPUs than workers is not bound to.
+// §5).  A node with fewer usable CPUs than workers is not bound to.
 int host_resources(hlc_ctx* c, const void* src = nullptr, size_t src_len = 0) {
   int least = 0, greatest = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));

@@ -259,8 +259,9 @@ void hlc_host_free(void* p);
                                       (HLC_WIRE_WALK = "lane" / "lds") */
 #define HLC_OPT_SPLIT_VOTES_APPEND 15      /* appends a range size to HLC_OPT_SPLIT_VOTES' list ("a,b,...") */
 #define HLC_OPT_WIRE_SPLIT_BYTES_APPEND 16 /* appends a range size to HLC_OPT_WIRE_SPLIT_BYTES' list */
-#define HLC_POOL_BIND_NONE 0       /* workers run on any CPU of the process's affinity mask */
-#define HLC_POOL_BIND_GPU 1        /* the CPUs of the GPU's NUMA node (default) */
+#define HLC_POOL_BIND_NONE 0       /* workers run on any CPU of the process's affinity mask (default since
+                                      round 6: DESIGN.md §5, profiles/r06/numa_ab_*.txt) */
+#define HLC_POOL_BIND_GPU 1        /* the CPUs of the GPU's NUMA node (the round-5 default) */
 #define HLC_POOL_BIND_SOURCE 2     /* the CPUs of the NUMA node the call's input arena lives on, per call */
 int hlc_ctx_set_option(hlc_ctx* ctx, int option, int64_t value);  /* HLC_EINVAL: unknown / out of range */
 int hlc_ctx_get_option(hlc_ctx* ctx, int option, int64_t* value);  /* list options: their first entry */
