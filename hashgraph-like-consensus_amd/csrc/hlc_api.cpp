@@ -257,6 +257,7 @@ struct Options {
   int serial_stages = 0;      // HLC_OPT_SERIAL_STAGES: prep + main after the prehash on one stream
   int wire_pipeline = 1;      // HLC_OPT_WIRE_PIPELINE: 0 = the unpipelined wire host entry (A/B arm)
   int wire_walk = -1;         // HLC_OPT_WIRE_WALK: -1 the build's default walker, 0 per lane, 1 LDS
+  int early_comb = 0;         // HLC_OPT_EARLY_COMB: u1 G in k_rec_main's tail (k_rec_ucomb + k_rec_add)
 };
 
 // The CPUs the cgroup (v2) quota grants the process, or 0 when there is none.
@@ -312,6 +313,7 @@ Options read_env() {
   if ((e = std::getenv("HLC_SERIAL_STAGES"))) o.serial_stages = std::atoi(e) != 0;
   if ((e = std::getenv("HLC_WIRE_PIPELINE"))) o.wire_pipeline = std::atoi(e) != 0;
   if ((e = std::getenv("HLC_WIRE_WALK"))) o.wire_walk = std::strcmp(e, "lane") == 0 ? 0 : 1;
+  if ((e = std::getenv("HLC_EARLY_COMB"))) o.early_comb = std::atoi(e) != 0;
   return o;
 }
 
@@ -322,6 +324,7 @@ struct hlc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;                        // the recovery prep stage, concurrent with the prehash
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // caller stream -> aux -> caller stream
+  hipEvent_t ev_prep = nullptr;  // aux: the recovery's prep stage done (HLC_OPT_EARLY_COMB)
   std::mutex mu;
   DBuf gtab, fbtab, rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
@@ -380,6 +383,7 @@ struct hlc_ctx {
       if (e) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    if (ev_prep) (void)hipEventDestroy(ev_prep);
     for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto& pr : chain_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   }
@@ -583,6 +587,11 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     HIPCHK(hipEventRecord(p1, aux));
     c->rec_prep_ev.emplace_back(p0, p1);
   }
+  // HLC_OPT_EARLY_COMB: u1 G (k_rec_ucomb) is enqueued on `s` behind the prehash and this prep stage;
+  // k_rec_main's persistent grid holds every register until its tail, so the comb's waves take the
+  // slots its waves leave, instead of starting after its last one
+  const bool early = c->opt.early_comb && !c->opt.serial_stages;
+  if (early) HIPCHK(hipEventRecord(c->ev_prep, aux));
   if (c->timing) HIPCHK(hipEventRecord(r0, aux));
   unsigned long long* clk = nullptr;
   if (c->clock_probe) {
@@ -596,11 +605,16 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   if (!c->opt.serial_stages) {
     HIPCHK(hipEventRecord(c->ev_join, aux));
     CHK(prehash_and_chain());
+    if (early) {
+      HIPCHK(hipStreamWaitEvent(s, c->ev_prep, 0));
+      hlc::launch_recover_ucomb(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), c->gtab.as<uint32_t>(),
+                                c->rec_work.as<uint32_t>(), s, c->opt.rec_force_exact);
+    }
     HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
   }
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_OWNER,
                              HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
-                             drec, s, c->opt.rec_force_exact);
+                             drec, s, c->opt.rec_force_exact, 0, early);
   if (c->timing) {
     HIPCHK(hipEventRecord(r1, s));
     c->rec_ev.emplace_back(r0, r1);
@@ -2014,6 +2028,10 @@ int hlc_ctx_set_option(hlc_ctx* ctx, int option, int64_t value) {
       if (value < -1 || value > 1) return bad();
       o.wire_walk = (int)value;
       break;
+    case HLC_OPT_EARLY_COMB:
+      if (value < 0 || value > 1) return bad();
+      o.early_comb = (int)value;
+      break;
     default: return set_err(HLC_EINVAL, "unknown option " + std::to_string(option));
   }
   return 0;
@@ -2038,6 +2056,7 @@ int hlc_ctx_get_option(hlc_ctx* ctx, int option, int64_t* value) {
     case HLC_OPT_SERIAL_STAGES: *value = o.serial_stages; break;
     case HLC_OPT_WIRE_PIPELINE: *value = o.wire_pipeline; break;
     case HLC_OPT_WIRE_WALK: *value = o.wire_walk; break;
+    case HLC_OPT_EARLY_COMB: *value = o.early_comb; break;
     default: return set_err(HLC_EINVAL, "unknown option " + std::to_string(option));
   }
   return 0;
@@ -2059,7 +2078,8 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       create_aux(c) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming) != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     delete c;

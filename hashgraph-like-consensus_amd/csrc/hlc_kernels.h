@@ -103,7 +103,12 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gtab, uint32_t* work,
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0,
-                           uint64_t stride = 0);  // stride: the records' row stride (0 = n; the fronts' n)
+                           uint64_t stride = 0,  // stride: the records' row stride (0 = n; the fronts' n)
+                           bool early_comb = false);  // u1 G from launch_recover_ucomb: k_rec_add, not k_rec_comb
+// u1 G alone (k_rec_ucomb) over a whole call's records (row stride n), once the prehash (pre, z_digest)
+// and the prep stage are done; launch_recover_finish(..., early_comb = true) adds u2 R after k_rec_main.
+void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint32_t* gtab,
+                          uint32_t* work, hipStream_t s, int force_exact = 0);
 uint64_t recover_grid_lanes();
 uint64_t recover_scratch_words();  // per-lane workspace words of k_rec_main
 uint64_t recover_work_words(uint64_t n);

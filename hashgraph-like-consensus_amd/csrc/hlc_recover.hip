@@ -233,6 +233,47 @@ __global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_comb(uint64_t n
   store_fe_ws(qz, q + (size_t)16 * st + i, st);
 }
 
+// ---- the comb alone (HLC_OPT_EARLY_COMB): enqueued after the prehash and the prep stage, beside
+// k_rec_main, whose persistent grid holds every register until its tail, so these waves take the
+// slots its waves leave.  Every vote k_rec_prep listed (prep code 0) whose prehash checks passed:
+// u1 = -z / r and u1 G, stored with its infinity flag for k_rec_add. ----
+__global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_ucomb(uint64_t n, uint64_t st, const uint8_t* pre,
+                                                   const uint32_t* z_digest, const uint32_t* gcomb,
+                                                   const uint32_t* rec, uint32_t* g, int force_exact) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (pre && pre[i] != PRE_PENDING)) return;
+  if (((rec[(size_t)REC_FLAGS * st + i] >> 8) & 0xFFu) != 0u) return;  // not listed (skipped / scheme error)
+  fe z, u1, gx, gy, gz;
+  bool neg_g;
+  fe_from_digest(z, z_digest + 8 * i);
+  rec_u1(z, rec + i, st, u1, neg_g);
+  const uint32_t inf = rec_ucomb29(u1, neg_g, gx, gy, gz, gcomb, force_exact != 0);
+  store_fe_ws(gx, g + i, st);
+  store_fe_ws(gy, g + (size_t)8 * st + i, st);
+  store_fe_ws(gz, g + (size_t)16 * st + i, st);
+  g[(size_t)24 * st + i] = inf;
+}
+
+// ---- after k_rec_main and k_rec_ucomb: Q = u2 R + u1 G, the same states as k_rec_comb ----
+__global__ void __launch_bounds__(256) k_rec_add(uint64_t n, uint64_t st, const uint8_t* pre, uint8_t* state,
+                                                 uint32_t* q, const uint32_t* g, const uint8_t* mst) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (pre && pre[i] != PRE_PENDING)) return;
+  const uint8_t m = mst[i];
+  if (m == MST_SKIP) return;
+  if (m != MST_OK && m != MST_INF) {
+    state[i] = m;
+    return;
+  }
+  fe qx, qy, qz;
+  const int code = rec_add29(m == MST_INF, q + i, g + i, st, qx, qy, qz);
+  state[i] = code != SCHEME_NONE ? (uint8_t)(1 + code) : REC_PENDING;
+  if (code != SCHEME_NONE) return;
+  store_fe_ws(qx, q + i, st);
+  store_fe_ws(qy, q + (size_t)8 * st + i, st);
+  store_fe_ws(qz, q + (size_t)16 * st + i, st);
+}
+
 #ifndef HLC_FIN_BATCH
 #define HLC_FIN_BATCH REC_BATCH
 #endif
@@ -405,10 +446,15 @@ inline unsigned blocks_for(uint64_t n, int tpb) { return (unsigned)((n + tpb - 1
 
 uint64_t recover_scratch_words() { return SCRATCH_WORDS; }
 
-uint64_t recover_work_words(uint64_t n) {
+namespace {
+constexpr int G_WORDS = 25;  // k_rec_ucomb -> k_rec_add: Jacobian u1 G (24 words) + its infinity flag
+uint64_t core_work_words(uint64_t n) {
   const uint64_t L = (n + REC_BATCH - 1) / REC_BATCH, Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
   return n * (uint64_t)(REC_WORDS + Q_WORDS + 1) + std::max(L * REC_BATCH, Lf * FIN_BATCH) * 8 + (n + 3) / 4 + 64;
 }
+}  // namespace
+
+uint64_t recover_work_words(uint64_t n) { return core_work_words(n) + (uint64_t)G_WORDS * n; }
 
 uint64_t recover_grid_lanes() {
   int dev = 0, cus = 256, per_cu = 0;
@@ -423,7 +469,7 @@ uint64_t recover_range_words(uint64_t m) { return m + (m + REC_BATCH) * 8 + 16; 
 
 namespace {
 struct RecBufs {
-  uint32_t *rec, *q, *pfx, *list;
+  uint32_t *rec, *q, *pfx, *list, *g;
   uint8_t* mst;
   unsigned long long* ctr;  // [0] k_rec_main's grab counter, [1] the work list's length
   uint64_t L;
@@ -439,6 +485,7 @@ RecBufs rec_bufs(uint64_t n, uint32_t* work) {
   b.mst = reinterpret_cast<uint8_t*>(b.pfx + std::max(b.L * REC_BATCH, Lf * FIN_BATCH) * 8);  // n bytes
   // the two counters: 8-byte aligned inside the 64-word tail of recover_work_words(n)
   b.ctr = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(b.mst + n) + 7) & ~uintptr_t(7));
+  b.g = work + core_work_words(n);  // G_WORDS rows of n words
   return b;
 }
 // The front half's buffers for items [v0, v0 + m) of a call of n items: the per-vote records in the
@@ -497,17 +544,29 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
                      f.b.ctr + 1, clk);
 }
 
+void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint32_t* gcomb,
+                          uint32_t* work, hipStream_t s, int force_exact) {
+  if (!n) return;
+  const RecBufs b = rec_bufs(n, work);
+  hipLaunchKernelGGL(k_rec_ucomb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, n, pre, z_digest, gcomb, b.rec,
+                     b.g, force_exact);
+}
+
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb, uint32_t* work,
-                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact, uint64_t stride) {
+                           uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact, uint64_t stride,
+                           bool early_comb) {
   if (!n) return;
   const uint64_t st = stride ? stride : n;  // the records' row stride (>= n)
   const RecBufs b = rec_bufs(st, work);
   const uint64_t Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
   const unsigned fb = (unsigned)((Lf + PREP_TPB - 1) / PREP_TPB);
   const unsigned vb = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(k_rec_comb, dim3(vb), dim3(256), 0, s, n, st, pre, z_digest, gcomb, verify_out, b.rec, b.q,
-                     b.mst, force_exact);
+  if (early_comb)  // u1 G is in b.g already (launch_recover_ucomb, same stride)
+    hipLaunchKernelGGL(k_rec_add, dim3(vb), dim3(256), 0, s, n, st, pre, verify_out, b.q, b.g, b.mst);
+  else
+    hipLaunchKernelGGL(k_rec_comb, dim3(vb), dim3(256), 0, s, n, st, pre, z_digest, gcomb, verify_out, b.rec, b.q,
+                       b.mst, force_exact);
   hipLaunchKernelGGL(k_rec_final, dim3(fb), dim3(PREP_TPB), 0, s, n, st, Lf, pre, verify_out, b.q, b.pfx);
   hipLaunchKernelGGL(k_rec_addr, dim3(vb), dim3(256), 0, s, n, st, pre, bytes, id_off, off_stride, verify_out, b.q,
                      addr_out);

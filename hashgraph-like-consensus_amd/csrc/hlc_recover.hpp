@@ -62,6 +62,9 @@ constexpr int RTAB_N = 1 << (W_R - 1);          // 16 odd multiples 1..31 (per l
 constexpr int REG_E = HLC_REG_ENTRIES;
 static_assert(REG_E >= 0 && REG_E < RTAB_N, "HLC_REG_ENTRIES out of range");
 constexpr int DIG_R_WORDS = (M_R + 1) / 2;      // int16 digits, 2 per word
+#ifndef HLC_DIGIT_PREFETCH
+#define HLC_DIGIT_PREFETCH 1  // the u2 R chain's digit words read after the doublings (+0.5%, profiles/r06/ab_dpf.txt)
+#endif
 // Per-lane workspace of the main stage (persistent grid):
 //  * lane-interleaved (word w of lane t at w * lanes + t: every lane touches the same word, so
 //    each access is one coalesced 256-B row per wave): the z-ratios of the table build;
@@ -484,6 +487,21 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const r
 #pragma unroll 1
   for (int win = M_R - 1; win >= 0; --win) {
     ge29 g;
+#if HLC_DIGIT_PREFETCH
+    // Both digit words are loaded at the window's top and read after its doublings, so their
+    // latency (an L2 miss: the digits of 640k votes do not fit the L2) hides behind the doublings.
+    // Read at the top, as before, each window waited on the b1 word before its doublings and on the
+    // b2 word before the b2 gather.
+    const uint32_t w1 = word_at(win, 0), w2 = word_at(win, 1);
+    if (win != M_R - 1) {
+#pragma unroll 1
+      for (int q = 0; q < W_R - 1; ++q) gej29_double(acc, acc);
+    }
+    int d = digit16(w1, win & 1);
+    tab.load(g, index_of(d));
+    if (win != M_R - 1) gej29_double(acc, acc);
+    const int d2 = digit16(w2, win & 1);
+#else
     int d = digit_at(win, 0);
     if (win != M_R - 1) {
 #pragma unroll 1
@@ -495,6 +513,7 @@ HLC_DEV void chain_u2r29(gej29& acc, const uint32_t* rec, size_t stride, const r
     }
     // the b2 entry is loaded before the b1 addition: its gather latency hides behind that addition
     const int d2 = digit_at(win, 1);
+#endif
     ge29 g2;
     tab.load(g2, index_of(d2));
     fe29_cneg_lazy(g.y, g.y, (d < 0) != ((negs & 1) != 0));
@@ -646,6 +665,45 @@ HLC_DEV int rec_comb29(const fe& u1, bool neg_g, bool inf, const uint32_t* qin, 
   gej29 acc, ag;
   comb_mul_g29<false>(ag, u1, neg_g, gcomb);
   if (force_exact || fe29_is_zero_modp(ag.z)) comb_mul_g29<true>(ag, u1, neg_g, gcomb);
+  load_fe_ws(qx, qin, stride);
+  load_fe_ws(qy, qin + 8 * stride, stride);
+  load_fe_ws(qz, qin + 16 * stride, stride);
+  acc.inf = inf;
+  fe29_from32(acc.x, qx.v);
+  fe29_from32(acc.y, qy.v);
+  fe29_from32(acc.z, qz.v);
+  gej29_add(acc, acc, ag);
+  if (acc.inf) return SCHEME_INFINITY;
+  fe29_to32(qx.v, acc.x);
+  fe29_to32(qy.v, acc.y);
+  fe29_to32(qz.v, acc.z);
+  return SCHEME_NONE;
+}
+
+
+// The same second half in two kernels (HLC_OPT_EARLY_COMB): rec_ucomb29 runs the comb as soon as the
+// prehash and the prep stage are done (k_rec_ucomb, dispatched into k_rec_main's tail as its waves
+// leave), rec_add29 adds u2 R once k_rec_main is done (k_rec_add).  u1 G goes through memory in
+// 8 x 32 limbs: the same point, so Q and every outcome are those of rec_comb29.
+HLC_DEV uint32_t rec_ucomb29(const fe& u1, bool neg_g, fe& gx, fe& gy, fe& gz, const uint32_t* gcomb, bool force_exact) {
+  gej29 ag;
+  comb_mul_g29<false>(ag, u1, neg_g, gcomb);
+  if (force_exact || fe29_is_zero_modp(ag.z)) comb_mul_g29<true>(ag, u1, neg_g, gcomb);
+  fe29_to32(gx.v, ag.x);
+  fe29_to32(gy.v, ag.y);
+  fe29_to32(gz.v, ag.z);
+  return ag.inf;
+}
+HLC_DEV int rec_add29(bool inf, const uint32_t* qin, const uint32_t* gin, size_t stride, fe& qx, fe& qy, fe& qz) {
+  gej29 acc, ag;
+  fe gx, gy, gz;
+  load_fe_ws(gx, gin, stride);
+  load_fe_ws(gy, gin + 8 * stride, stride);
+  load_fe_ws(gz, gin + 16 * stride, stride);
+  ag.inf = gin[24 * stride];
+  fe29_from32(ag.x, gx.v);
+  fe29_from32(ag.y, gy.v);
+  fe29_from32(ag.z, gz.v);
   load_fe_ws(qx, qin, stride);
   load_fe_ws(qy, qin + 8 * stride, stride);
   load_fe_ws(qz, qin + 16 * stride, stride);

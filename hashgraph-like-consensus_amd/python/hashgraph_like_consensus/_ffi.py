@@ -146,7 +146,7 @@ OPTIONS = {
     "host_threads": 1, "pool_bind": 2, "nt_copy": 3, "split_votes": 4, "host_trace": 5, "first_batch": 6,
     "rest_pieces": 7, "wire_split_bytes": 8, "wire_front_cap": 9, "wire_chunk": 10, "rec_force_exact": 11,
     "serial_stages": 12, "wire_pipeline": 13, "wire_walk": 14, "split_votes_append": 15,
-    "wire_split_bytes_append": 16,
+    "wire_split_bytes_append": 16, "early_comb": 17,
 }
 LIST_OPTIONS = {"split_votes": "split_votes_append", "wire_split_bytes": "wire_split_bytes_append"}
 POOL_BIND_NONE, POOL_BIND_GPU, POOL_BIND_SOURCE = 0, 1, 2
