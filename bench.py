@@ -45,7 +45,23 @@ W_IMPL_LIMB_PRODUCTS_PER_VOTE = ROOFLINE["implementation"]["limb_products_per_vo
 # rocprofv3 passes of this bench (tools/profile.sh), committed under profiles/: kernel-trace
 # summary, FETCH_SIZE / WRITE_SIZE and the VALU / wave counters of the recovery kernels.
 PMC_PROFILE = os.path.join(ROOT, ROOFLINE["profile"])
-REC_KERNELS = ("k_rec_prep", "k_rec_main", "k_rec_comb", "k_rec_final", "k_rec_addr")
+# The recovery's kernels.  Round 6 on, the default schedule splits the u1 G comb off the finish
+# (HLC_OPT_EARLY_COMB): k_rec_ucomb runs in k_rec_main's tail and k_rec_add adds u2 R after it; older
+# profiles (and HLC_EARLY_COMB=0) hold the fused k_rec_comb instead.
+REC_KERNELS_FUSED = ("k_rec_prep", "k_rec_main", "k_rec_comb", "k_rec_final", "k_rec_addr")
+REC_KERNELS_EARLY = ("k_rec_prep", "k_rec_main", "k_rec_ucomb", "k_rec_add", "k_rec_final", "k_rec_addr")
+
+
+def _profile_rec_kernels():
+    path = os.path.join(PMC_PROFILE, "trace", "run_kernel_trace.csv")
+    try:
+        with open(path) as f:
+            return REC_KERNELS_EARLY if "k_rec_ucomb(" in f.read() else REC_KERNELS_FUSED
+    except OSError:
+        return REC_KERNELS_EARLY
+
+
+REC_KERNELS = _profile_rec_kernels()
 
 
 def _pmc_rows(name: str):
@@ -204,8 +220,9 @@ def valu_figures():
 
 def rocprof_kernel_ms():
     """Average durations (ms) of the recovery kernels over the timed steps of the committed
-    kernel trace of this bench command (the last 20 validate-many calls), their serial-chain sum
-    (prep -> main -> comb -> final -> addr run one after another) and the traced step period."""
+    kernel trace of this bench command (the last 20 validate-many calls), the recovery's critical
+    path (`serial_chain_sum`: k_rec_prep's duration + k_rec_main's start to k_rec_addr's end -- the
+    comb runs inside that span, after k_rec_main or in its tail) and the traced step period."""
     import csv
     import re
     import statistics
@@ -227,12 +244,14 @@ def rocprof_kernel_ms():
         for t0, t1, k in seg:
             first.setdefault(k, (t0, t1))
         if all(k in first for k in REC_KERNELS):
-            calls.append({k: (first[k][1] - first[k][0]) / 1e6 for k in REC_KERNELS} | {"_t0": first["k_rec_prep"][0]})
+            calls.append({k: (first[k][1] - first[k][0]) / 1e6 for k in REC_KERNELS}
+                         | {"_t0": first["k_rec_prep"][0],
+                            "_span": (first["k_rec_addr"][1] - first["k_rec_main"][0]) / 1e6})
     calls = calls[-20:]
     if not calls:
         return None
     out = {k: statistics.mean(c[k] for c in calls) for k in REC_KERNELS}
-    out["serial_chain_sum"] = sum(out[k] for k in REC_KERNELS)
+    out["serial_chain_sum"] = out["k_rec_prep"] + statistics.mean(c["_span"] for c in calls)
     out["traced_step_period"] = (statistics.mean((calls[i + 1]["_t0"] - calls[i]["_t0"]) / 1e6
                                                  for i in range(len(calls) - 1)) if len(calls) > 1 else None)
     out["calls"] = len(calls)
@@ -961,7 +980,7 @@ def compact_line(out: dict, detail_path: str) -> dict:
     line["roofline"] = {
         **{k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_per_vote",
                                   "frac_rocprof_chain", "valu_lane_op_frac", "valu_issue_frac", "kernel_ms_avg")},
-        "kernel": "recovery: k_rec_prep + k_rec_main + k_rec_comb + k_rec_final + k_rec_addr (HIP events)",
+        "kernel": "recovery: k_rec_prep + k_rec_main (+ k_rec_ucomb in its tail) + k_rec_add + k_rec_final + k_rec_addr (HIP events)",
         "valu_instr_per_vote_k_rec_main": (rf.get("valu_instr_per_vote") or {}).get("k_rec_main"),
         "live_k_rec_main_GHz": live.get("median_GHz"),
     }
@@ -1211,7 +1230,8 @@ def main() -> int:
         **({"exchange": exchange} if exchange is not None else {}),
         "roofline": {
             "bound": "valu",
-            "kernel": "recovery: k_rec_prep + k_rec_main (second stream, beside the prehash) + k_rec_comb + k_rec_final + k_rec_addr (HIP-event brackets)",
+            "kernel": ("recovery: k_rec_prep + k_rec_main (second stream, beside the prehash) + k_rec_ucomb (u1 G, in "
+                       "k_rec_main's tail) + k_rec_add + k_rec_final + k_rec_addr (HIP-event brackets)"),
             "achieved": achieved,
             "peak": MAD_PEAK_T_PER_S,
             "unit": "T limb-products/s (32x32->64, v_mad_u64_u32)",

@@ -1,10 +1,11 @@
 """Per-step timeline of the headline leg from a rocprofv3 kernel trace (tools/profile.sh trace/).
 
 Each validate-many call launches k_rec_prep -> k_rec_main (second stream) and k_prehash_fused ->
-k_chain_small (launch stream), then k_rec_comb -> k_rec_final -> k_rec_addr -> ... -> k_finalize.
+k_chain_small (launch stream), then k_rec_comb -> k_rec_final -> k_rec_addr -> ... -> k_finalize
+(round 6 on: k_rec_ucomb in k_rec_main's tail, then k_rec_add -> k_rec_final -> ...).
 For the last --steps calls of the trace this prints the call span (first kernel start to
-k_finalize end), the serial recovery chain (prep + main + comb + final + addr durations, which run
-one after another), the gaps between call spans (host launch overhead), and the averages -- the
+k_finalize end), the recovery's critical path (prep's duration + k_rec_main's start to k_rec_addr's
+end), the gaps between call spans (host launch overhead), and the averages -- the
 check that the chain's rocprof sum fits inside the bench line's ms_per_step.
 
     python tools/trace_steps.py profiles/r03_rocprof/trace/run_kernel_trace.csv --steps 20
@@ -17,7 +18,8 @@ import json
 import re
 import statistics
 
-CHAIN = ("k_rec_prep", "k_rec_main", "k_rec_comb", "k_rec_final", "k_rec_addr")
+CHAIN_FUSED = ("k_rec_prep", "k_rec_main", "k_rec_comb", "k_rec_final", "k_rec_addr")
+CHAIN_EARLY = ("k_rec_prep", "k_rec_main", "k_rec_ucomb", "k_rec_add", "k_rec_final", "k_rec_addr")
 
 
 def short(name: str) -> str:
@@ -33,6 +35,7 @@ def main() -> int:
     a = ap.parse_args()
     rows = sorted(({"k": short(r["Kernel_Name"]), "s": int(r["Start_Timestamp"]), "e": int(r["End_Timestamp"])}
                    for r in csv.DictReader(open(a.trace))), key=lambda r: r["s"])
+    CHAIN = CHAIN_EARLY if any(r["k"] == "k_rec_ucomb" for r in rows) else CHAIN_FUSED
     # calls are delimited by k_rec_prep launches (one per validate-many call)
     starts = [i for i, r in enumerate(rows) if r["k"] == "k_rec_prep"]
     calls = []
@@ -46,8 +49,9 @@ def main() -> int:
             continue
         t0 = min(r["s"] for r in ks if r["k"] in CHAIN + ("k_prehash_fused", "k_assign_props", "k_red_init"))
         calls.append({"t0": t0, "t1": byk["k_finalize"]["e"],
-                      "chain_ms": sum(byk[k]["e"] - byk[k]["s"] for k in CHAIN) / 1e6,
-                      "kernels_ms": {k: (byk[k]["e"] - byk[k]["s"]) / 1e6 for k in CHAIN + ("k_prehash_fused",)}})
+                      "chain_ms": (byk["k_rec_prep"]["e"] - byk["k_rec_prep"]["s"]
+                                   + byk["k_rec_addr"]["e"] - byk["k_rec_main"]["s"]) / 1e6,
+                      "kernels_ms": {k: (byk[k]["e"] - byk[k]["s"]) / 1e6 for k in CHAIN + ("k_prehash_fused",) if k in byk}})
     calls = calls[-a.steps:]
     if not calls:
         print("no complete calls found")
