@@ -2,9 +2,9 @@
 # Round-6 verification call: the whole GPU suite, smoke(), and the driver's bench command (GPU box).
 set -o pipefail
 mkdir -p gpurun_out/r06
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r06/gpu_all.txt 2>&1 || { tail -30 gpurun_out/r06/gpu_all.txt; exit 1; }
-tail -3 gpurun_out/r06/gpu_all.txt
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r06/smoke.txt 2>&1 || { tail -20 gpurun_out/r06/smoke.txt; exit 1; }
-tail -1 gpurun_out/r06/smoke.txt
-HLC_BENCH_DETAIL=$PWD/gpurun_out/r06/bench_b_detail.json timeout -k 10 300 python bench.py > gpurun_out/r06/bench_b.json 2> gpurun_out/r06/bench_b.err || { tail gpurun_out/r06/bench_b.err; exit 1; }
-python tools/bench_summary.py gpurun_out/r06/bench_b.json
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r06/gpu_all_c.txt 2>&1 || { tail -30 gpurun_out/r06/gpu_all_c.txt; exit 1; }
+tail -3 gpurun_out/r06/gpu_all_c.txt
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r06/smoke_c.txt 2>&1 || { tail -20 gpurun_out/r06/smoke_c.txt; exit 1; }
+tail -1 gpurun_out/r06/smoke_c.txt
+HLC_BENCH_DETAIL=$PWD/gpurun_out/r06/bench_d_detail.json timeout -k 10 300 python bench.py > gpurun_out/r06/bench_d.json 2> gpurun_out/r06/bench_d.err || { tail gpurun_out/r06/bench_d.err; exit 1; }
+python tools/bench_summary.py gpurun_out/r06/bench_d.json
