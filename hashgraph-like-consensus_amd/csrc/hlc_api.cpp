@@ -257,7 +257,7 @@ struct Options {
   int serial_stages = 0;      // HLC_OPT_SERIAL_STAGES: prep + main after the prehash on one stream
   int wire_pipeline = 1;      // HLC_OPT_WIRE_PIPELINE: 0 = the unpipelined wire host entry (A/B arm)
   int wire_walk = -1;         // HLC_OPT_WIRE_WALK: -1 the build's default walker, 0 per lane, 1 LDS
-  int early_comb = 1;         // HLC_OPT_EARLY_COMB: u1 G in k_rec_main's tail (k_rec_ucomb + k_rec_add; +0.65%)
+  int early_comb = 1;         // HLC_OPT_EARLY_COMB bits: 1 device-resident calls (+0.65%), 2 host-buffer calls
 };
 
 // The CPUs the cgroup (v2) quota grants the process, or 0 when there is none.
@@ -313,7 +313,7 @@ Options read_env() {
   if ((e = std::getenv("HLC_SERIAL_STAGES"))) o.serial_stages = std::atoi(e) != 0;
   if ((e = std::getenv("HLC_WIRE_PIPELINE"))) o.wire_pipeline = std::atoi(e) != 0;
   if ((e = std::getenv("HLC_WIRE_WALK"))) o.wire_walk = std::strcmp(e, "lane") == 0 ? 0 : 1;
-  if ((e = std::getenv("HLC_EARLY_COMB"))) o.early_comb = std::atoi(e) != 0;
+  if ((e = std::getenv("HLC_EARLY_COMB"))) o.early_comb = std::max(0, std::min(std::atoi(e), 3));
   return o;
 }
 
@@ -339,6 +339,7 @@ struct hlc_ctx {
   PBuf pin_in, pin_out;
   DBuf dev_in, dev_out;
   std::vector<hipEvent_t> ev_up, ev_main;  // per recovery range: inputs landed, main stage done
+  std::vector<hipEvent_t> ev_prepk;        // per recovery range: prep stage done (early comb, host entries)
   std::vector<hipEvent_t> ev_cnt, ev_dec;  // wire host entry, per message range: vote count read back, decoded
   PBuf pin_cnt;                            // wire host entry: the ranges' vote counts (page-locked)
   uint64_t wire_hint = 0;                  // wire host entry: the largest vote count a call decoded
@@ -377,6 +378,7 @@ struct hlc_ctx {
     for (auto& pr : chain_aux_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (hipEvent_t e : ev_up) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_main) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_prepk) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_cnt) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_dec) (void)hipEventDestroy(e);
     for (hipEvent_t e : {ev_rest, ev_done})
@@ -484,6 +486,7 @@ int ensure_fbtab(hlc_ctx* c) {
 struct RecFront {
   uint64_t v0, v1;
   hipEvent_t done;
+  hipEvent_t prep;  // the range's k_rec_prep done
 };
 
 // Per-vote validate_vote stage (utils.rs:127-171; plus the proposal_id match of utils.rs:113-115)
@@ -568,11 +571,19 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   };
   if (fronts) {
     CHK(prehash_and_chain());
+    // HLC_OPT_EARLY_COMB bit 1: u1 G behind the prehash and every range's prep stage, in the last
+    // range's k_rec_main tail
+    const bool early_host = (c->opt.early_comb & 2) != 0;
+    if (early_host) {
+      for (int k = 0; k < nfronts; ++k) HIPCHK(hipStreamWaitEvent(s, fronts[k].prep, 0));
+      hlc::launch_recover_ucomb(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), c->gtab.as<uint32_t>(),
+                                c->rec_work.as<uint32_t>(), s, c->opt.rec_force_exact, rec_stride);
+    }
     for (int k = 0; k < nfronts; ++k) HIPCHK(hipStreamWaitEvent(s, fronts[k].done, 0));
     hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
                                dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(),
                                c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->opt.rec_force_exact,
-                               rec_stride);
+                               rec_stride, early_host);
     hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
                             c->verify.as<uint8_t>(), status, reason, red, s);
     HIPCHK(hipGetLastError());
@@ -597,7 +608,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   // HLC_OPT_EARLY_COMB: u1 G (k_rec_ucomb) is enqueued on `s` behind the prehash and this prep stage;
   // k_rec_main's persistent grid holds every register until its tail, so the comb's waves take the
   // slots its waves leave, instead of starting after its last one
-  early = c->opt.early_comb && !c->opt.serial_stages;
+  early = (c->opt.early_comb & 1) && !c->opt.serial_stages;
   if (early) HIPCHK(hipEventRecord(c->ev_prep, aux));
   if (c->timing) HIPCHK(hipEventRecord(r0, aux));
   unsigned long long* clk = nullptr;
@@ -1176,6 +1187,11 @@ int prepare_ranges(hlc_ctx* c, uint64_t n, std::vector<uint64_t>& rb) {
     HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
     c->ev_main.push_back(b);
   }
+  while (c->ev_prepk.size() < R) {
+    hipEvent_t p = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&p, hipEventDisableTiming));
+    c->ev_prepk.push_back(p);
+  }
   for (size_t k = 0; k < R; ++k) CHK(c->rec_works[k]->ensure(hlc::recover_range_words(rb[k + 1] - rb[k]) * 4));
   return 0;
 }
@@ -1200,12 +1216,13 @@ int launch_front(hlc_ctx* c, HostTrace& tr, uint64_t n, size_t k, uint64_t a0, u
   HIPCHK(hipStreamWaitEvent(a, ready ? ready : c->ev_up[k], 0));
   hlc::launch_recover_prep(n, dbytes, sig_off, off_stride, sig_len, len_stride, c->rec_work.as<uint32_t>(), a,
                            nullptr, &range);
+  HIPCHK(hipEventRecord(c->ev_prepk[k], a));
   hlc::launch_recover_main(n, dbytes, sig_off, off_stride, scratch, lanes, c->rec_work.as<uint32_t>(), a,
                            c->opt.rec_force_exact, &range);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_main[k], a));
   tr.ev("main_end_" + std::to_string(k), a);
-  fronts.push_back(RecFront{a0, a0 + m, c->ev_main[k]});
+  fronts.push_back(RecFront{a0, a0 + m, c->ev_main[k], c->ev_prepk[k]});
   return 0;
 }
 
@@ -1716,6 +1733,11 @@ int validate_wire_host(hlc_ctx* c, const uint8_t* wire, uint64_t wire_len, const
     HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
     c->ev_main.push_back(b);
   }
+  while (c->ev_prepk.size() < R) {
+    hipEvent_t p = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&p, hipEventDisableTiming));
+    c->ev_prepk.push_back(p);
+  }
   while (c->rec_works.size() < R) c->rec_works.emplace_back(new DBuf());
   Staging st{c, c->pin_in.at(0), c->dev_in.as<uint8_t>(), c->opt.nt_copy && cpu_has_avx2()};
   DrainOnExit guard{st};
@@ -1982,7 +2004,7 @@ int hlc_ctx_set_option(hlc_ctx* ctx, int option, int64_t value) {
       o.host_threads = (int)value;
       break;
     case HLC_OPT_POOL_BIND:
-      if (value < 0 || value > 1) return bad();
+      if (value < 0 || value > 2) return bad();
       o.pool_bind = (int)value;
       break;
     case HLC_OPT_NT_COPY: o.nt_copy = value != 0; break;
@@ -2032,7 +2054,7 @@ int hlc_ctx_set_option(hlc_ctx* ctx, int option, int64_t value) {
       o.wire_walk = (int)value;
       break;
     case HLC_OPT_EARLY_COMB:
-      if (value < 0 || value > 2) return bad();
+      if (value < 0 || value > 3) return bad();
       o.early_comb = (int)value;
       break;
     default: return set_err(HLC_EINVAL, "unknown option " + std::to_string(option));

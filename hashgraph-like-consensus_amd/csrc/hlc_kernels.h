@@ -108,7 +108,7 @@ void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_dig
 // u1 G alone (k_rec_ucomb) over a whole call's records (row stride n), once the prehash (pre, z_digest)
 // and the prep stage are done; launch_recover_finish(..., early_comb = true) adds u2 R after k_rec_main.
 void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint32_t* gtab,
-                          uint32_t* work, hipStream_t s, int force_exact = 0);
+                          uint32_t* work, hipStream_t s, int force_exact = 0, uint64_t stride = 0);
 uint64_t recover_grid_lanes();
 uint64_t recover_scratch_words();  // per-lane workspace words of k_rec_main
 uint64_t recover_work_words(uint64_t n);

@@ -545,11 +545,12 @@ void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_o
 }
 
 void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint32_t* gcomb,
-                          uint32_t* work, hipStream_t s, int force_exact) {
+                          uint32_t* work, hipStream_t s, int force_exact, uint64_t stride) {
   if (!n) return;
-  const RecBufs b = rec_bufs(n, work);
-  hipLaunchKernelGGL(k_rec_ucomb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, n, pre, z_digest, gcomb, b.rec,
-                     b.g, force_exact);
+  const uint64_t st = stride ? stride : n;  // the records' row stride, as launch_recover_finish
+  const RecBufs b = rec_bufs(st, work);
+  hipLaunchKernelGGL(k_rec_ucomb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, st, pre, z_digest, gcomb,
+                     b.rec, b.g, force_exact);
 }
 
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,

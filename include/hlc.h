@@ -259,8 +259,9 @@ void hlc_host_free(void* p);
                                       (HLC_WIRE_WALK = "lane" / "lds") */
 #define HLC_OPT_SPLIT_VOTES_APPEND 15      /* appends a range size to HLC_OPT_SPLIT_VOTES' list ("a,b,...") */
 #define HLC_OPT_WIRE_SPLIT_BYTES_APPEND 16 /* appends a range size to HLC_OPT_WIRE_SPLIT_BYTES' list */
-#define HLC_OPT_EARLY_COMB 17      /* 1: device-resident calls run the u1 G comb in the u2 R stage's tail
-                                      (k_rec_ucomb + k_rec_add); 0: after it (k_rec_comb) (HLC_EARLY_COMB; 1) */
+#define HLC_OPT_EARLY_COMB 17      /* bits: 1 device-resident calls, 2 host-buffer calls run the u1 G comb in
+                                      the u2 R stage's tail (k_rec_ucomb + k_rec_add); clear: after it
+                                      (k_rec_comb) (HLC_EARLY_COMB; 1) */
 #define HLC_POOL_BIND_NONE 0       /* workers run on any CPU of the process's affinity mask (default since
                                       round 6: DESIGN.md §5, profiles/r06/numa_ab_*.txt) */
 #define HLC_POOL_BIND_GPU 1        /* the CPUs of the GPU's NUMA node (the round-5 default) */

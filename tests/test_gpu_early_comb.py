@@ -66,3 +66,33 @@ def test_gpu_early_comb_honest_and_repeated(engine, early_engine):
         got = _run(early_engine, db)
         for a, b in zip(ref, got):
             assert np.array_equal(a, b)
+
+
+def test_gpu_early_comb_host_entries(early_engine):
+    """Bit 2 of HLC_OPT_EARLY_COMB: the host-buffer entries' finish with k_rec_ucomb behind every
+    recovery range's prep stage (records at the call's row stride) equals the fused finish, for the
+    SoA entry over several recovery ranges and the pipelined wire entry over several message ranges;
+    the SoA outcomes also equal the C oracle's."""
+    from adversarial import byzantine as byz_mix
+    from helpers import oracle_workload
+    w = oracle_workload(260, 64, 64, True, 0xEC0B)
+    batch, desc, _ = byz_mix(w, fraction=1 / 3, seed=0xEC0B)
+    outs = {}
+    for mode in (0, 3):
+        with early_engine.options(early_comb=mode, split_votes=[2048, 4096]):
+            outs[mode] = early_engine.validate_proposals(batch, desc, w.now, want_recovered=True)
+    for a, b in zip(outs[0], outs[3]):
+        assert np.array_equal(a, b)
+    cres, cvst, cvrs, crec = coracle.validate_proposals(batch, desc, w.now)
+    res, vst, vrs, rec = outs[3]
+    assert np.array_equal(vst, cvst) and np.array_equal(vrs, cvrs) and np.array_equal(rec, crec)
+    assert np.array_equal(res, cres)
+    wire, off, lens, scope = synth.to_wire(batch, desc)
+    wouts = {}
+    for mode in (0, 3):
+        with early_engine.options(early_comb=mode, wire_split_bytes=[8192, 16384], wire_chunk=4096, host_trace=2):
+            wouts[mode] = early_engine.validate_wire_proposals(wire, off, lens, scope, w.now)
+            assert early_engine.last_host_trace()["facts"]["ranges"] >= 2
+    assert wouts[0][2] == wouts[3][2]
+    assert np.array_equal(wouts[0][0], wouts[3][0])
+    assert np.array_equal(wouts[0][1].view(np.uint8), wouts[3][1].view(np.uint8))
