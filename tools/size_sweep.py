@@ -1,5 +1,5 @@
 """hlc_validate_proposals_device at several batch sizes (config-2 shape: P proposals x 64 votes),
-3 timed calls each: the per-call fixed cost of the recovery kernels (run under rocprofv3
+10 timed calls each: the per-call fixed cost of the recovery kernels (run under rocprofv3
 --kernel-trace for per-kernel times)."""
 import os
 import sys
@@ -22,10 +22,10 @@ for P in [int(x) for x in (sys.argv[1:] or ["2500", "5000", "10000", "20000", "4
     eng.set_kernel_timing(True)
     eng.take_kernel_time()
     t = time.perf_counter()
-    for _ in range(3):
+    for _ in range(10):
         eng.validate_proposals_device(db, s.cuda_stream)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / 3
+    dt = (time.perf_counter() - t) / 10
     rec_ms, rec_n, _, _ = eng.take_kernel_time()
     eng.set_kernel_timing(False)
     print(f"P {P} votes {db.n} ms_per_call {dt * 1e3:.3f} rec_ms {rec_ms / max(rec_n, 1):.3f} "
