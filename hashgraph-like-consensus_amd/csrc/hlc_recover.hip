@@ -75,6 +75,38 @@ HLC_DEV bool pre_rejected(const RecSkip& k, uint64_t i) {
   return fl[HLC_F_OWNER] == 0 || fl[HLC_F_VOTE_HASH] == 0;
 }
 
+#ifndef HLC_PREP_LOADS
+#define HLC_PREP_LOADS 0  // A/B knob: k_rec_prep's per-vote loads in three round trips (see prep_vote); 2: also
+                          // the backward pass's reload in two
+#endif
+// The forward pass's per-vote inputs in three memory round trips: every word that depends only on i
+// (vote_prop, proposal_id, the owner / vote_hash lengths, the signature's length and offset) is
+// issued before any is used, then the covering proposal's id, then the signature bytes (read only
+// for a vote the checks pass).  pre_rejected + prep_sig waited on each load in turn (seven round
+// trips per vote, eight votes per lane, at ~1.2 waves/SIMD: the PMC pass shows k_rec_prep's waves
+// waiting on memory 43% of their cycles).  Same outcome as !pre_rejected && prep_sig.
+HLC_DEV bool prep_vote(const RecSkip& k, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
+                       const uint32_t* sig_len, size_t len_stride, uint64_t i, fe& r, fe& s, int& parity, int& code) {
+  const bool skip = HLC_PRE_SKIP && k.vote_prop;
+  const uint32_t slen = sig_len[i * len_stride];
+  const uint64_t soff = sig_off ? sig_off[i * off_stride] : 65 * i;
+  uint32_t p = 0, vpid = 0, flo = 1, flh = 1;
+  if (skip) {
+    const uint32_t* fl = k.field_len + i * HLC_NFIELDS;
+    p = k.vote_prop[i];
+    vpid = k.proposal_id[i];
+    flo = fl[HLC_F_OWNER];
+    flh = fl[HLC_F_VOTE_HASH];
+  }
+  if (skip && (p == NO_PROP || flo == 0 || flh == 0 || vpid != k.props[p].proposal_id)) return false;
+  if (slen != 65u) return false;
+  const uint8_t* sig = bytes + soff;  // read only for a vote the checks pass, as prep_sig
+  fe_load_be(r, sig);
+  fe_load_be(s, sig + 32);
+  code = rec_parse(s, r, sig[64], parity);
+  return true;
+}
+
 // n votes; records rec / mst of vote i at rec + i (stride `st` words between a record's rows), mst[i].
 __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t st, uint64_t L, const uint8_t* bytes,
                                                        const uint64_t* sig_off, size_t off_stride,
@@ -98,7 +130,11 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t st, 
     if (i >= n) break;
     fe r, s;
     int parity, code;
+#if HLC_PREP_LOADS
+    if (!prep_vote(sk, bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) {
+#else
     if (pre_rejected(sk, i) || !prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code)) {
+#endif
       rec[(size_t)REC_FLAGS * st + i] = PREP_SKIP << 8;
       mst[i] = MST_SKIP;
       continue;
@@ -120,8 +156,19 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_prep(uint64_t n, uint64_t st, 
     if (i >= n || !((active >> k) & 1u)) continue;
     fe r, s, prev, rinv;
     int parity, code;
+#if HLC_PREP_LOADS >= 2
+    // an active vote's signature is 65 bytes (the forward pass checked): its offset and the prefix
+    // product in one round trip, then the bytes
+    const uint64_t soff = sig_off ? sig_off[i * off_stride] : 65 * i;
+    load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
+    const uint8_t* sig = bytes + soff;
+    fe_load_be(r, sig);
+    fe_load_be(s, sig + 32);
+    code = rec_parse(s, r, sig[64], parity);
+#else
     prep_sig(bytes, sig_off, off_stride, sig_len, len_stride, i, r, s, parity, code);
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
+#endif
     sc_mont_mul(rinv, prev, cur);  // r_k^-1
     sc_mont_mul(cur, cur, r);      // acc_{k-1}^-1
     rec_prep_scalars(s, rinv, parity, rec + i, st);
@@ -278,6 +325,9 @@ __global__ void __launch_bounds__(256) k_rec_add(uint64_t n, uint64_t st, const 
 #define HLC_FIN_BATCH REC_BATCH
 #endif
 constexpr int FIN_BATCH = HLC_FIN_BATCH;  // votes per lane (one inversion) in k_rec_final
+#ifndef HLC_FIN_LOADS
+#define HLC_FIN_LOADS 0  // A/B knob: k_rec_final's loads issued ahead of their use (see k_rec_final)
+#endif
 // ---- final: batched Z^-1 (one safegcd per FIN_BATCH votes) and affine Q, then (k_rec_addr, one
 // lane per vote at full occupancy) keccak of X || Y and the owner compare.  Split in two because
 // the eight keccak-f of a lane's batch made k_rec_final one long dependent chain per lane at ~1.2
@@ -288,6 +338,26 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t st,
   if (t >= L) return;
   fe acc;
   fe_set(acc, 1);
+#if HLC_FIN_LOADS
+  // every vote's state and Z issued before any is used (one memory round trip for the forward pass,
+  // was two per vote at ~1.2 waves/SIMD); the Zs stay in registers for the backward pass
+  uint32_t pend = 0;
+  fe zs[FIN_BATCH];
+#pragma unroll
+  for (int k = 0; k < FIN_BATCH; ++k) {
+    const uint64_t i = t + (uint64_t)k * L;
+    if (i >= n) break;
+    const bool p = (!pre || pre[i] == PRE_PENDING) && state[i] == REC_PENDING;
+    pend |= (uint32_t)p << k;
+    load_fe_ws(zs[k], q + (size_t)16 * st + i, st);
+  }
+#pragma unroll
+  for (int k = 0; k < FIN_BATCH; ++k) {
+    if (!((pend >> k) & 1u)) continue;
+    store_fe_ws(acc, pfx + (size_t)k * 8 * L + t, L);
+    fe_mul(acc, acc, zs[k]);
+  }
+#else
 #pragma unroll 1
   for (int k = 0; k < FIN_BATCH; ++k) {
     const uint64_t i = t + (uint64_t)k * L;
@@ -298,8 +368,19 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t st,
     store_fe_ws(acc, pfx + (size_t)k * 8 * L + t, L);
     fe_mul(acc, acc, z);
   }
+#endif
   fe cur;
   fe_inv(cur, acc);
+#if HLC_FIN_LOADS
+#pragma unroll
+  for (int k = FIN_BATCH - 1; k >= 0; --k) {
+    if (!((pend >> k) & 1u)) continue;
+    const uint64_t i = t + (uint64_t)k * L;
+    fe x, y, z = zs[k], prev, zi, zi2, zi3;
+    load_fe_ws(x, q + i, st);
+    load_fe_ws(y, q + (size_t)8 * st + i, st);
+    load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
+#else
 #pragma unroll 1
   for (int k = FIN_BATCH - 1; k >= 0; --k) {
     const uint64_t i = t + (uint64_t)k * L;
@@ -309,6 +390,7 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t st,
     load_fe_ws(y, q + (size_t)8 * st + i, st);
     load_fe_ws(z, q + (size_t)16 * st + i, st);
     load_fe_ws(prev, pfx + (size_t)k * 8 * L + t, L);
+#endif
     fe_mul(zi, prev, cur);  // Z_k^-1
     fe_mul(cur, cur, z);
     fe_sqr(zi2, zi);

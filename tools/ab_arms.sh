@@ -7,6 +7,7 @@
 # AB_MODE selects what each arm runs:
 #   headline (default)  bench.py headline leg, 150 timed steps after 50 warm-up
 #   legs                bench.py headline + config-5 legs, 20 steps
+#   c4                  bench.py headline (3 steps) + the config-4 shard leg (12.5M votes per call)
 #   host                tools/host_pipe.py (host-buffer entry, default schedule, 8 host threads), 20 calls
 #   wire                tools/wire_pipe.py (the wire entry from host buffers, default schedule), 20 calls
 #                       (AB_WIRE_ARGS="--device-walk lane" adds the device-resident wire entry)
@@ -29,6 +30,9 @@ for round in 1 2 3; do
     legs)
       HLC_BENCH_DETAIL=$PWD/$O.detail.json env $ENVS timeout -k 10 300 python bench.py --steps 20 --warmup 5 ${LEGS/--no-config5/} > $O.json 2> $O.err || { tail $O.err; exit 1; }
       python -c "import json;d=json.load(open('$O.json'));print('$round $v headline', round(d['value']), 'config5', round(d['legs']['config5']), 'votes/s')" ;;
+    c4)
+      HLC_BENCH_DETAIL=$PWD/$O.detail.json env $ENVS timeout -k 10 300 python bench.py --steps 3 --warmup 1 ${LEGS/--no-config4-shard/} > $O.json 2> $O.err || { tail $O.err; exit 1; }
+      python -c "import json;d=json.load(open('$O.json'));print('$round $v config4_shard', round(d['legs']['config4_shard']), 'votes/s headline', round(d['value']))" ;;
     host)
       env $ENVS timeout -k 10 200 python tools/host_pipe.py --threads 8 --steps 20 > $O.txt 2> $O.err || { tail $O.err; exit 1; }
       python -c "import json;d=json.loads(open('$O.txt').read().splitlines()[-1]);print('$round $v host', round(d['votes_per_s']), 'votes/s', round(d['ms_per_call'],3), 'ms')" ;;
