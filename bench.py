@@ -1128,7 +1128,10 @@ def main() -> int:
         assert (st == 0).all(), f"{int((st != 0).sum())} valid votes rejected"
         assert (res["status"] == 0).all() and (res["total"] == V).all()
 
-    eng.set_kernel_timing(True)
+    # the timed steps carry the recovery bracket only (two dispatch-bound events per call); the chain /
+    # tally and whole-call brackets bind three more kernels on the critical path, so they are timed in
+    # a pass of their own after the timed region (chain_pass below)
+    eng.set_kernel_timing(True, recovery_only=True)
     eng.take_kernel_time()
     eng.take_chain_time()
     if dist is not None:
@@ -1141,10 +1144,17 @@ def main() -> int:
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    rec_ms, rec_n, call_ms, calls = eng.take_kernel_time()
-    chain_ms, chain_n = eng.take_chain_time()
+    rec_ms, rec_n, _, _ = eng.take_kernel_time()
     eng.set_kernel_timing(False)
     live_clock = measure_live_clock(eng, step, torch)
+    # chain_pass: the same step, every bracket timed (chain check + duplicates + tally, the whole call)
+    eng.set_kernel_timing(True)
+    for _ in range(min(args.steps, 10)):
+        step()
+    torch.cuda.synchronize()
+    _, _, call_ms, calls = eng.take_kernel_time()
+    chain_ms, chain_n = eng.take_chain_time()
+    eng.set_kernel_timing(False)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1265,7 +1275,7 @@ def main() -> int:
             "kernel_launches": rec_n,
             "rocprof_kernel_ms": rk,
             "call_ms_avg": call_ms / max(calls, 1),
-            "kernel_share_of_step": rec_ms / max(call_ms, 1e-9),
+            "kernel_share_of_step": (rec_ms / max(rec_n, 1)) / max(call_ms / max(calls, 1), 1e-9),
         },
         "chain_tally": {
             "what": "chain check + duplicate detection + tally kernels (utils.rs:175-286, session.rs:253-298), "

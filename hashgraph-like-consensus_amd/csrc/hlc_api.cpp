@@ -355,7 +355,8 @@ struct hlc_ctx {
   DBuf out_res, out_status, out_reason, out_rec, out_misc;
   // internal workspace
   // measurement hooks
-  bool timing = false;
+  int timing = 0;  // 0, HLC_TIMING_ALL or HLC_TIMING_RECOVERY (hlc_ctx_set_kernel_timing)
+  bool timing_all() const { return timing == HLC_TIMING_ALL; }
   bool clock_probe = false;  // hlc_ctx_set_clock_probe: k_rec_main's per-wave clock stamps into clk_buf
   DBuf clk_buf;
   uint64_t clk_waves = 0;
@@ -386,7 +387,7 @@ struct hlc_ctx {
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (ev_prep) (void)hipEventDestroy(ev_prep);
-    for (auto& pr : call_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : call_ev) (void)hipEventDestroy(pr.first);  // (pr.second is chain_ev's)
     for (auto& pr : chain_ev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   }
   DBuf vote_prop, sha_sz, sha_off, kec_sz, kec_off, sha_buf, kec_buf, sha_dig, kec_dig, pre, pre_reason,
@@ -503,10 +504,16 @@ struct RecFront {
 // per range they cost 0.95 ms against 0.67 ms for one launch over 640k votes.)
 // verdicts != nullptr (the *_verdicts entries, any ConsensusSignatureScheme): the scheme step is the
 // caller's per-vote verdict; the prehash runs without the Ethereum checks and keccak, and no recovery runs.
+// aux_tables != nullptr: the large-proposal chain / duplicate tables' launcher (validate_device); with
+// the early comb it is enqueued on the aux stream behind k_rec_main, where it runs beside the comb
+// instead of on the launch stream's critical path, and *tables_done is set.
+// fork_recorded: validate_device bound c->ev_fork to its last kernel on `s` (no marker needed here).
+using TablesLaunch = std::function<void(hipStream_t, const hlc::KEv*)>;
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t np,
                uint64_t now, uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, uint8_t* chain_code,
                hipStream_t s, const RecFront* fronts = nullptr, int nfronts = 0, uint64_t rec_stride = 0,
-               const uint8_t* verdicts = nullptr) {
+               const uint8_t* verdicts = nullptr, const TablesLaunch* aux_tables = nullptr,
+               bool* tables_done = nullptr, bool fork_recorded = false) {
   const uint64_t n = dv->n;
   CHK(c->pre.ensure(n));
   CHK(c->pre_reason.ensure(n));
@@ -534,16 +541,20 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   // (HLC_SERIAL_STAGES=1: everything on `s`, prep + main after the prehash and the chain kernel --
   // the measurement of k_rec_main running alone)
   hipStream_t aux = c->opt.serial_stages ? s : c->aux;
-  hipEvent_t p0 = nullptr, p1 = nullptr, r0 = nullptr, r1 = nullptr;
+  // the recovery bracket: k_rec_prep's start .. k_rec_addr's end, both bound to the dispatches
+  hipEvent_t p0 = nullptr, r1 = nullptr;
   if (c->timing && !fronts) {
     p0 = c->take_event();
-    p1 = c->take_event();
-    r0 = c->take_event();
     r1 = c->take_event();
   }
-  bool early = false;  // HLC_OPT_EARLY_COMB (set below, after the prep launch)
+  // HLC_OPT_EARLY_COMB: u1 G (k_rec_ucomb) is enqueued on `s` behind the prehash and the prep stage;
+  // k_rec_main's persistent grid holds every register until its tail, so the comb's waves take the
+  // slots its waves leave, instead of starting after its last one (DESIGN.md §8.1)
+  const bool early = !fronts && (c->opt.early_comb & 1) && !c->opt.serial_stages;
+  // the prep stage's completion (early comb: what `s` waits on), bound to k_rec_prep's dispatch
+  const hipEvent_t prep_done = early ? c->ev_prep : nullptr;
   auto launch_ucomb = [&]() -> int {
-    HIPCHK(hipStreamWaitEvent(s, c->ev_prep, 0));
+    HIPCHK(hipStreamWaitEvent(s, prep_done, 0));
     hlc::launch_recover_ucomb(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), c->gtab.as<uint32_t>(),
                               c->rec_work.as<uint32_t>(), s, c->opt.rec_force_exact);
     return 0;
@@ -555,17 +566,12 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
                                c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(), s);
     if (drec) HIPCHK(hipMemsetAsync(drec, 0, n * 20, s));
     if (chain_code) {
-      hipEvent_t cs0 = nullptr, cs1 = nullptr;
-      if (c->timing) {
-        cs0 = c->take_event();
-        cs1 = c->take_event();
-        HIPCHK(hipEventRecord(cs0, s));
+      hlc::KEv cs;
+      if (c->timing_all()) {
+        cs = hlc::KEv{c->take_event(), c->take_event()};
+        c->chain_aux_ev.emplace_back(cs.start, cs.stop);
       }
-      hlc::launch_chain_small(dv, dprops, np, chain_code, red, s);
-      if (c->timing) {
-        HIPCHK(hipEventRecord(cs1, s));
-        c->chain_aux_ev.emplace_back(cs0, cs1);
-      }
+      hlc::launch_chain_small(dv, dprops, np, chain_code, red, s, &cs);
     }
     return 0;
   };
@@ -592,47 +598,49 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   if (c->opt.serial_stages) {
     CHK(prehash_and_chain());
   } else {
-    HIPCHK(hipEventRecord(c->ev_fork, s));
+    if (!fork_recorded) HIPCHK(hipEventRecord(c->ev_fork, s));
     HIPCHK(hipStreamWaitEvent(aux, c->ev_fork, 0));
   }
-  if (c->timing) HIPCHK(hipEventRecord(p0, aux));
   // votes the checks before the signature reject (proposal_id mismatch, empty owner / vote_hash,
   // no covering proposal) are not recovered: vote_prop exists before the fork
   const hlc::RecSkip skip{vote_prop, dprops, dv->proposal_id, dv->field_len};
+  const hlc::KEv pk{p0, prep_done};
   hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
-                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux, &skip);
-  if (c->timing) {
-    HIPCHK(hipEventRecord(p1, aux));
-    c->rec_prep_ev.emplace_back(p0, p1);
-  }
-  // HLC_OPT_EARLY_COMB: u1 G (k_rec_ucomb) is enqueued on `s` behind the prehash and this prep stage;
-  // k_rec_main's persistent grid holds every register until its tail, so the comb's waves take the
-  // slots its waves leave, instead of starting after its last one (DESIGN.md §8.1)
-  early = (c->opt.early_comb & 1) && !c->opt.serial_stages;
-  if (early) HIPCHK(hipEventRecord(c->ev_prep, aux));
-  if (c->timing) HIPCHK(hipEventRecord(r0, aux));
+                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux, &skip, nullptr, &pk);
   unsigned long long* clk = nullptr;
   if (c->clock_probe) {
     CHK(c->clk_buf.ensure((c->rec_lanes / 64) * 32 + 32));
     HIPCHK(hipMemsetAsync(c->clk_buf.p, 0, (c->rec_lanes / 64) * 32, aux));
     clk = c->clk_buf.as<unsigned long long>();
   }
+  // the join `s` waits on before the finish: k_rec_main's completion, or (early comb) that of the
+  // large-proposal tables enqueued behind it on aux -- a timing event when their bracket is timed
+  const bool tables_aux = early && aux_tables;
+  hipEvent_t t0 = nullptr, join = c->opt.serial_stages ? nullptr : c->ev_join;
+  if (tables_aux && c->timing_all()) {
+    t0 = c->take_event();
+    join = c->take_event();
+    c->chain_aux_ev.emplace_back(t0, join);
+  }
+  const hlc::KEv mk{nullptr, tables_aux ? nullptr : join};
   hlc::launch_recover_main(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, c->rec_scratch.as<uint32_t>(),
                            c->rec_lanes, c->rec_work.as<uint32_t>(), aux, c->opt.rec_force_exact, nullptr, clk,
-                           clk ? &c->clk_waves : nullptr);
+                           clk ? &c->clk_waves : nullptr, &mk);
+  if (tables_aux) {
+    const hlc::KEv tk{t0, join};
+    (*aux_tables)(aux, &tk);
+    if (tables_done) *tables_done = true;
+  }
   if (!c->opt.serial_stages) {
-    HIPCHK(hipEventRecord(c->ev_join, aux));
     CHK(prehash_and_chain());
     if (early) CHK(launch_ucomb());  // after the small-proposal chain kernel (before it: -0.4 to -1.1%)
-    HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+    HIPCHK(hipStreamWaitEvent(s, join, 0));
   }
+  const hlc::KEv fk{nullptr, r1};
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_OWNER,
                              HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
-                             drec, s, c->opt.rec_force_exact, 0, early);
-  if (c->timing) {
-    HIPCHK(hipEventRecord(r1, s));
-    c->rec_ev.emplace_back(r0, r1);
-  }
+                             drec, s, c->opt.rec_force_exact, 0, early, &fk);
+  if (c->timing) c->rec_ev.emplace_back(p0, r1);
   hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
                           c->verify.as<uint8_t>(), status, reason, red, s);
   HIPCHK(hipGetLastError());
@@ -664,16 +672,25 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
                     const uint8_t* verdicts = nullptr) {
   const uint64_t n = dv->n;
   if (n > 0xFFFFFFF0ull) return set_err(HLC_EINVAL, "too many votes in one call (max 2^32-16)");
-  hipEvent_t call0 = nullptr, call1 = nullptr;
-  if (c->timing) {
+  // timing: call0 .. ch1 (the call), ch0 .. ch1 (chain check + duplicates + tally), all bound to
+  // kernel dispatches (hlc::KEv); ch1 is shared by the two brackets and owned by chain_ev
+  hipEvent_t call0 = nullptr, ch0 = nullptr, ch1 = nullptr;
+  if (c->timing_all()) {
     call0 = c->take_event();
-    call1 = c->take_event();
-    HIPCHK(hipEventRecord(call0, s));
+    ch0 = c->take_event();
+    ch1 = c->take_event();
   }
   CHK(c->vote_prop.ensure(n * 4 + 4));
   CHK(c->flag.ensure(16));
-  HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(uint32_t), s));
-  HIPCHK(hlc::launch_assign_props(dprops, np, dv->field_len, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s));
+  CHK(c->red.ensure(np * 16 + 16));
+  // per-proposal reduction records and the call's flag word in one launch, then the vote -> proposal map
+  const hlc::KEv rk{call0, nullptr};
+  hlc::launch_red_init(c->red.as<uint32_t>(), np, s, c->flag.as<uint32_t>(), &rk, c->vote_prop.as<uint32_t>(), n);
+  // the aux stream's fork point: bound to k_assign_props's dispatch on the default recovery path
+  const bool bind_fork = n && !fronts && !verdicts && !c->opt.serial_stages;
+  const hlc::KEv ak{nullptr, bind_fork ? c->ev_fork : nullptr};
+  HIPCHK(hlc::launch_assign_props(dprops, np, dv->field_len, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s,
+                                  &ak, true));
   uint8_t* status = dstatus;
   uint8_t* reason = dreason;
   if (!status) {
@@ -685,37 +702,36 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
     reason = c->reason.as<uint8_t>();
   }
   CHK(c->chain_code.ensure(n + 1));
-  CHK(c->red.ensure(np * 16 + 16));
   // proposals > 512 votes use global chain / duplicate tables; the kernels are always enqueued and
   // do nothing unless k_assign_props raised FLAG_LARGE_PROPOSAL (no host read-back)
   uint64_t cap = 64;
   while (cap < 2 * n) cap <<= 1;
   CHK(c->chain_tab.ensure(cap * 4));
   CHK(c->dup_tab.ensure(cap * 4));
-  hlc::launch_red_init(c->red.as<uint32_t>(), np, s);
+  const TablesLaunch tables = [&](hipStream_t st, const hlc::KEv* ev) {
+    hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
+                       c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(),
+                       st, ev);
+  };
+  bool tables_done = false;
   // (the small proposals' chain / duplicate / YES kernel runs inside vote_stage, beside the
   // recovery's main stage: k_vote_status reports each proposal's first failing vote)
   if (n)
     CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, np, now, status, reason, drec, c->red.as<uint32_t>(),
-                   c->chain_code.as<uint8_t>(), s, fronts, nfronts, rec_stride, verdicts));
-  hipEvent_t ch0 = nullptr, ch1 = nullptr;
-  if (c->timing) {  // chain check + duplicate detection + tally (+ k_chain_small's bracket in vote_stage)
-    ch0 = c->take_event();
-    ch1 = c->take_event();
-    HIPCHK(hipEventRecord(ch0, s));
-  }
-  hlc::launch_tables(dv, n, c->vote_prop.as<uint32_t>(), dprops, c->chain_tab.as<uint32_t>(),
-                     c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
+                   c->chain_code.as<uint8_t>(), s, fronts, nfronts, rec_stride, verdicts, &tables, &tables_done,
+                   bind_fork));
+  // chain check + duplicate detection + tally (+ k_chain_small's and the aux tables' brackets in vote_stage)
+  const hlc::KEv c0{ch0, nullptr}, c1{nullptr, ch1};
+  if (!tables_done) tables(s, &c0);
   hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
                           c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
-                          c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s);
-  hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s);
+                          c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s, tables_done ? &c0 : nullptr);
+  hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s,
+                       &c1);
   HIPCHK(hipGetLastError());
-  if (c->timing) {
-    HIPCHK(hipEventRecord(ch1, s));
+  if (c->timing_all()) {
     c->chain_ev.emplace_back(ch0, ch1);
-    HIPCHK(hipEventRecord(call1, s));
-    c->call_ev.emplace_back(call0, call1);
+    c->call_ev.emplace_back(call0, ch1);
   }
   return 0;
 }
@@ -2156,7 +2172,7 @@ int hlc_ctx_reserve(hlc_ctx* ctx, uint64_t max_votes, uint64_t max_proposals, ui
 int hlc_ctx_set_kernel_timing(hlc_ctx* ctx, int enable) {
   if (!ctx) return set_err(HLC_EINVAL, "ctx is NULL");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  ctx->timing = enable != 0;
+  ctx->timing = enable == HLC_TIMING_RECOVERY ? HLC_TIMING_RECOVERY : (enable ? HLC_TIMING_ALL : 0);
   return 0;
 }
 
@@ -2212,7 +2228,7 @@ int hlc_ctx_take_kernel_time(hlc_ctx* ctx, double* recover_ms, uint64_t* recover
   for (auto* vec : {&ctx->rec_ev, &ctx->rec_prep_ev, &ctx->call_ev}) {
     for (auto& pr : *vec) {
       ctx->ev_pool.push_back(pr.first);
-      ctx->ev_pool.push_back(pr.second);
+      if (vec != &ctx->call_ev) ctx->ev_pool.push_back(pr.second);  // (a call's end is chain_ev's)
     }
     vec->clear();
   }

@@ -1,5 +1,6 @@
 // hlc_kernels.h -- host-side launchers of the HIP kernels (internal to libhlc.so).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -20,14 +21,39 @@ enum MsgMode { MSG_VOTE = 0, MSG_PAYLOAD = 1 };
 
 struct Workspace;  // defined in hlc_api.cpp
 
+// Events bound to a kernel's own dispatch (hipExtLaunchKernelGGL): `start` takes the kernel's start,
+// `stop` its completion, with no marker packet in the queue (a hipEventRecord between two kernels of
+// one stream leaves the queue idle for ~6 us; tools/ext_event_probe.hip).  A `stop`
+// event may also be what another stream waits on.  A launcher that launches nothing records the
+// events on its stream instead, so every bracket stays valid.
+struct KEv {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+template <typename F, typename... A>
+inline void launch_k(const KEv* ev, F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, A... args) {
+  if (ev && (ev->start || ev->stop))
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, ev->start, ev->stop, 0u, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+}
+inline void record_kev(const KEv* ev, hipStream_t s) {
+  if (!ev) return;
+  if (ev->start) (void)hipEventRecord(ev->start, s);
+  if (ev->stop) (void)hipEventRecord(ev->stop, s);
+}
+// the start half / the stop half of a pair (for launchers that run several kernels)
+inline KEv kev_start(const KEv* ev) { return KEv{ev ? ev->start : nullptr, nullptr}; }
+inline KEv kev_stop(const KEv* ev) { return KEv{nullptr, ev ? ev->stop : nullptr}; }
+
 // ---- prehash stage ----
 // call flags (one device word, cleared by the caller): set by the kernels, read once per call
 constexpr uint32_t FLAG_GENERAL_PATH = 1u;     // some vote exceeds the fused prehash LDS window
 constexpr uint32_t FLAG_LARGE_PROPOSAL = 2u;   // some proposal has > 512 votes (global chain tables)
 constexpr uint32_t FLAG_LARGE_PARENTS = 4u;    // some vote of such a proposal has a parent_hash (the chain table is needed)
 hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, const uint32_t* field_len, uint32_t* vote_prop,
-                               uint64_t nv, uint32_t* flags,
-                         hipStream_t s);
+                               uint64_t nv, uint32_t* flags, hipStream_t s,
+                               const KEv* ev = nullptr,  // ev: bound to k_assign_props
+                               bool map_cleared = false);  // vote_prop already NO_PROP (launch_red_init)
 void launch_msg_sizes(const hlc_votes* v, uint64_t n, const uint64_t* pay_off, const uint32_t* pay_len,
                       int mode, uint64_t* sha_sz, uint64_t* kec_sz, hipStream_t s);
 void launch_build_msgs(const hlc_votes* v, uint64_t n, const uint8_t* bytes, const uint64_t* pay_off,
@@ -95,16 +121,18 @@ struct RecRange {
 };
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s,
-                         const RecSkip* skip = nullptr, const RecRange* range = nullptr);
+                         const RecSkip* skip = nullptr, const RecRange* range = nullptr,
+                         const KEv* ev = nullptr);  // ev: bound to k_rec_prep
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact = 0,
                          const RecRange* range = nullptr, unsigned long long* clk = nullptr,
-                         uint64_t* clk_waves = nullptr);
+                         uint64_t* clk_waves = nullptr, const KEv* ev = nullptr);  // ev: bound to k_rec_main
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gtab, uint32_t* work,
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0,
                            uint64_t stride = 0,  // stride: the records' row stride (0 = n; the fronts' n)
-                           bool early_comb = false);  // u1 G from launch_recover_ucomb: k_rec_add, not k_rec_comb
+                           bool early_comb = false,  // u1 G from launch_recover_ucomb: k_rec_add, not k_rec_comb
+                           const KEv* ev = nullptr);  // ev: start at the first kernel, stop at k_rec_addr
 // u1 G alone (k_rec_ucomb) over a whole call's records (row stride n), once the prehash (pre, z_digest)
 // and the prep stage are done; launch_recover_finish(..., early_comb = true) adds u2 R after k_rec_main.
 void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint32_t* gtab,
@@ -121,17 +149,21 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
                         uint64_t now, const uint8_t* pre, const uint8_t* pre_reason, const uint8_t* verify,
                         uint8_t* status, uint8_t* reason, uint32_t* red, hipStream_t s);
 // per-proposal reduction records: first failing vote / chain error / duplicate = none, YES = 0
-void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s);
+// flag != nullptr: also clears the call's flag word; vote_prop != nullptr: also sets its nv entries to
+// NO_PROP for launch_assign_props(..., map_cleared = true) -- one launch instead of two memsets and a kernel
+void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s, uint32_t* flag = nullptr, const KEv* ev = nullptr,
+                     uint32_t* vote_prop = nullptr, uint64_t nv = 0);
 // large-proposal chain / duplicate tables: always enqueued, skipped on the device unless the call's
 // flag word has FLAG_LARGE_PROPOSAL (flags == nullptr: always run)
 // (the duplicate test reports into `red` from k_tables)
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                    uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, uint64_t np,
-                   const uint32_t* flags, hipStream_t s);
+                   const uint32_t* flags, hipStream_t s,
+                   const KEv* ev = nullptr);  // ev: start at the first kernel, stop at k_tables
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab,
                         uint32_t mask, uint8_t* chain_code, uint32_t* red, uint64_t np, const uint32_t* flags,
-                        hipStream_t s);
+                        hipStream_t s, const KEv* ev = nullptr);
 // batched handle_consensus_timeout: new state + status per session
 void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state, uint8_t* out_status, hipStream_t s);
 // proposals with <= 512 votes: chain / duplicate / YES count in LDS, one wave per proposal
@@ -139,13 +171,13 @@ void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state,
 // statuses: vote_stage enqueues it on the launch stream after the prehash kernels, beside k_rec_main
 // (which runs on the context's second stream), after launch_red_init.
 void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint8_t* chain_code,
-                        uint32_t* red, hipStream_t s);
+                        uint32_t* red, hipStream_t s, const KEv* ev = nullptr);
 // outcome counters: bins[0..31] += votes by status, bins[32..63] += proposals by status
 void launch_outcome_hist(const uint8_t* vote_status, uint64_t n, const hlc_result* res, uint64_t np,
                          unsigned long long* bins, hipStream_t s);
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
                      const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red,
-                     hlc_result* out, hipStream_t s);
+                     hlc_result* out, hipStream_t s, const KEv* ev = nullptr);
 
 // ---- wire decode (hlc_wire.hip) ----
 // mode 0: vote_count[m], wout[m], pout[m], first wire_slab() records per message in slab_*, *big |= 1 when

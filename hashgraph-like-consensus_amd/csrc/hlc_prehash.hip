@@ -1027,8 +1027,12 @@ __global__ void k_prehash_stream(hlc_votes v, uint64_t n, const uint32_t* vote_p
 }
 
 // per-proposal reduction records: first bad / chain / duplicate = none, YES = 0
-__global__ void k_red_init(uint32_t* red, uint64_t np) {
+// (flag != nullptr: the call's flag word is cleared too, before k_assign_props raises its bits;
+// vote_prop != nullptr: its nv entries are set to NO_PROP, the map k_assign_props then fills)
+__global__ void k_red_init(uint32_t* red, uint64_t np, uint32_t* flag, uint32_t* vote_prop, uint64_t nv) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (flag && p == 0) *flag = 0;
+  if (vote_prop && p < nv) vote_prop[p] = NO_PROP;
   if (p < np) reinterpret_cast<uint4*>(red)[p] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
 }
 
@@ -1182,17 +1186,17 @@ void launch_encode_payloads(const hlc_votes* v, uint64_t n, const uint64_t* off,
 
 
 hipError_t launch_assign_props(const hlc_proposal* props, uint64_t np, const uint32_t* field_len, uint32_t* vote_prop,
-                               uint64_t nv,
-                               uint32_t* flags, hipStream_t s) {
-  if (nv) {
+                               uint64_t nv, uint32_t* flags, hipStream_t s, const KEv* ev, bool map_cleared) {
+  if (nv && !map_cleared) {
     const hipError_t e = hipMemsetAsync(vote_prop, 0xFF, nv * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
   }
   // a second grid dimension when proposals are large on average (each block then covers ~4k votes)
   const uint64_t g = np ? std::min<uint64_t>(std::max<uint64_t>((nv / np + 4095) / 4096, 1), 1024) : 1;
   if (np)
-    hipLaunchKernelGGL(k_assign_props, dim3((unsigned)np, (unsigned)g), dim3(TPB), 0, s, props, field_len, vote_prop,
-                       flags);
+    launch_k(ev, k_assign_props, dim3((unsigned)np, (unsigned)g), dim3(TPB), 0, s, props, field_len, vote_prop, flags);
+  else
+    record_kev(ev, s);
   return hipSuccess;
 }
 
@@ -1239,22 +1243,30 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
                        pre_reason, verify, status, reason, red);
 }
 
-void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s) {
-  if (np) hipLaunchKernelGGL(k_red_init, dim3((unsigned)((np + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np);
+void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s, uint32_t* flag, const KEv* ev, uint32_t* vote_prop,
+                     uint64_t nv) {
+  if (!vote_prop) nv = 0;
+  const uint64_t m = std::max(np, nv);
+  if (m) {
+    launch_k(ev, k_red_init, dim3((unsigned)((m + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np, flag, vote_prop, nv);
+  } else {
+    record_kev(ev, s);
+    if (flag) (void)hipMemsetAsync(flag, 0, sizeof(uint32_t), s);
+  }
 }
 
 void launch_tables(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                    uint32_t* chain_tab, uint32_t* dup_tab, uint32_t mask, uint32_t* red, uint64_t np,
-                   const uint32_t* flags, hipStream_t s) {
-  (void)red;
+                   const uint32_t* flags, hipStream_t s, const KEv* ev) {
   (void)np;  // (red is initialised by launch_red_init before the vote stage)
-  if (!n) return;
+  if (!n) return record_kev(ev, s);
   const uint64_t words = (uint64_t)mask + 1;
   const unsigned cb = (unsigned)std::min<uint64_t>((words + TPB - 1) / TPB, 4096);
-  hipLaunchKernelGGL(k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PARENTS, chain_tab, words);
+  const KEv first = kev_start(ev), last = kev_stop(ev);
+  launch_k(&first, k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PARENTS, chain_tab, words);
   hipLaunchKernelGGL(k_clear_if, dim3(cb), dim3(TPB), 0, s, flags, FLAG_LARGE_PROPOSAL, dup_tab, words);
-  hipLaunchKernelGGL(k_tables, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, chain_tab, dup_tab,
-                     mask, red, flags);
+  launch_k(&last, k_tables, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, chain_tab, dup_tab, mask,
+           red, flags);
 }
 
 void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
@@ -1270,10 +1282,10 @@ void launch_prehash_stream(const hlc_votes* v, uint64_t n, const uint32_t* vote_
 
 void launch_chain_check(const hlc_votes* v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
                         const uint8_t* status, const uint32_t* chain_tab, const uint32_t* dup_tab, uint32_t mask,
-                        uint8_t* chain_code, uint32_t* red, uint64_t np, const uint32_t* flags, hipStream_t s) {
-  if (!np) return;  // (red initialised by launch_tables)
-  if (n)
-    hipLaunchKernelGGL(k_chain_check, dim3((unsigned)((n + CHAIN_TPB - 1) / CHAIN_TPB)), dim3(CHAIN_TPB), 0, s, *v, n,
+                        uint8_t* chain_code, uint32_t* red, uint64_t np, const uint32_t* flags, hipStream_t s,
+                        const KEv* ev) {
+  if (!np || !n) return record_kev(ev, s);  // (red initialised by launch_red_init)
+  launch_k(ev, k_chain_check, dim3((unsigned)((n + CHAIN_TPB - 1) / CHAIN_TPB)), dim3(CHAIN_TPB), 0, s, *v, n,
                        vote_prop, props, status,
                        chain_tab, dup_tab, mask, chain_code, red, flags);
 }
@@ -1284,8 +1296,11 @@ void launch_timeout(uint64_t n, const hlc_session_tally* ss, uint8_t* out_state,
 }
 
 void launch_chain_small(const hlc_votes* v, const hlc_proposal* props, uint64_t np, uint8_t* chain_code,
-                        uint32_t* red, hipStream_t s) {
-  if (np) hipLaunchKernelGGL(k_chain_small, dim3((unsigned)np), dim3(SMALL_TPB), 0, s, *v, props, chain_code, red);
+                        uint32_t* red, hipStream_t s, const KEv* ev) {
+  if (np)
+    launch_k(ev, k_chain_small, dim3((unsigned)np), dim3(SMALL_TPB), 0, s, *v, props, chain_code, red);
+  else
+    record_kev(ev, s);
 }
 
 namespace {
@@ -1318,10 +1333,12 @@ void launch_outcome_hist(const uint8_t* vote_status, uint64_t n, const hlc_resul
 
 void launch_finalize(const hlc_proposal* props, uint64_t np, uint64_t now, const uint8_t* status,
                      const uint8_t* reason, const uint8_t* chain_code, const uint32_t* red, hlc_result* out,
-                     hipStream_t s) {
+                     hipStream_t s, const KEv* ev) {
   if (np)
-    hipLaunchKernelGGL(k_finalize, dim3(blocks_for(np)), dim3(TPB), 0, s, props, np, now, status, reason,
-                       chain_code, red, out);
+    launch_k(ev, k_finalize, dim3(blocks_for(np)), dim3(TPB), 0, s, props, np, now, status, reason, chain_code, red,
+             out);
+  else
+    record_kev(ev, s);
 }
 
 }  // namespace hlc

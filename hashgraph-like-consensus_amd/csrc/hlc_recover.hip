@@ -599,31 +599,30 @@ FrontBufs front_bufs(uint64_t n, uint64_t v0, uint64_t m, uint32_t* work, uint32
 
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s, const RecSkip* skip,
-                         const RecRange* range) {
+                         const RecRange* range, const KEv* ev) {
   const uint64_t m = range ? range->m : n;
-  if (!m) return;
+  if (!m) return record_kev(ev, s);
   const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr, range);
   const unsigned pb = (unsigned)((f.b.L + PREP_TPB - 1) / PREP_TPB);
   (void)hipMemsetAsync(f.b.ctr, 0, 2 * sizeof(unsigned long long), s);  // grab counter, list length
   const RecSkip none{nullptr, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL(k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, m, f.st, f.b.L, bytes, sig_off, off_stride, sig_len,
-                     len_stride, f.b.rec, f.b.pfx, f.b.mst, f.b.list, f.b.ctr + 1, skip ? *skip : none);
+  launch_k(ev, k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, m, f.st, f.b.L, bytes, sig_off, off_stride, sig_len,
+           len_stride, f.b.rec, f.b.pfx, f.b.mst, f.b.list, f.b.ctr + 1, skip ? *skip : none);
 }
 
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact,
-                         const RecRange* range, unsigned long long* clk, uint64_t* clk_waves) {
+                         const RecRange* range, unsigned long long* clk, uint64_t* clk_waves, const KEv* ev) {
   const uint64_t m = range ? range->m : n;
-  if (!m) return;
+  if (!m) return record_kev(ev, s);
   const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr, range);
   uint64_t blocks = scratch_lanes / REC_TPB;
   uint64_t need = (m + REC_TPB - 1) / REC_TPB;
   if (blocks > need) blocks = need;
   if (blocks == 0) blocks = 1;  // a capped grid (HLC_OPT_WIRE_FRONT_CAP below one block) still runs
   if (clk_waves) *clk_waves = blocks * (REC_TPB / 64);
-  hipLaunchKernelGGL(k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, f.st, bytes, sig_off, off_stride,
-                     scratch, (uint64_t)blocks * REC_TPB, f.b.rec, f.b.q, f.b.mst, force_exact, f.b.ctr, f.b.list,
-                     f.b.ctr + 1, clk);
+  launch_k(ev, k_rec_main, dim3((unsigned)blocks), dim3(REC_TPB), 0, s, f.st, bytes, sig_off, off_stride, scratch,
+           (uint64_t)blocks * REC_TPB, f.b.rec, f.b.q, f.b.mst, force_exact, f.b.ctr, f.b.list, f.b.ctr + 1, clk);
 }
 
 void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint32_t* gcomb,
@@ -638,21 +637,22 @@ void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_dige
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb, uint32_t* work,
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact, uint64_t stride,
-                           bool early_comb) {
-  if (!n) return;
+                           bool early_comb, const KEv* ev) {
+  if (!n) return record_kev(ev, s);
   const uint64_t st = stride ? stride : n;  // the records' row stride (>= n)
   const RecBufs b = rec_bufs(st, work);
   const uint64_t Lf = (n + FIN_BATCH - 1) / FIN_BATCH;
   const unsigned fb = (unsigned)((Lf + PREP_TPB - 1) / PREP_TPB);
   const unsigned vb = (unsigned)((n + 255) / 256);
+  const KEv first = kev_start(ev), last = kev_stop(ev);
   if (early_comb)  // u1 G is in b.g already (launch_recover_ucomb, same stride)
-    hipLaunchKernelGGL(k_rec_add, dim3(vb), dim3(256), 0, s, n, st, pre, verify_out, b.q, b.g, b.mst);
+    launch_k(&first, k_rec_add, dim3(vb), dim3(256), 0, s, n, st, pre, verify_out, b.q, b.g, b.mst);
   else
-    hipLaunchKernelGGL(k_rec_comb, dim3(vb), dim3(256), 0, s, n, st, pre, z_digest, gcomb, verify_out, b.rec, b.q,
-                       b.mst, force_exact);
+    launch_k(&first, k_rec_comb, dim3(vb), dim3(256), 0, s, n, st, pre, z_digest, gcomb, verify_out, b.rec, b.q, b.mst,
+             force_exact);
   hipLaunchKernelGGL(k_rec_final, dim3(fb), dim3(PREP_TPB), 0, s, n, st, Lf, pre, verify_out, b.q, b.pfx);
-  hipLaunchKernelGGL(k_rec_addr, dim3(vb), dim3(256), 0, s, n, st, pre, bytes, id_off, off_stride, verify_out, b.q,
-                     addr_out);
+  launch_k(&last, k_rec_addr, dim3(vb), dim3(256), 0, s, n, st, pre, bytes, id_off, off_stride, verify_out, b.q,
+           addr_out);
 }
 
 

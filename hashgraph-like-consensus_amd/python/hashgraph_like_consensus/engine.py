@@ -402,8 +402,11 @@ class Engine:
         raw = self.lib.hlc_ctx_last_host_trace(self.ctx)
         return json.loads(raw.decode()) if raw else None
 
-    def set_kernel_timing(self, enable: bool) -> None:
-        _ffi.check(self.lib.hlc_ctx_set_kernel_timing(self.ctx, 1 if enable else 0))
+    def set_kernel_timing(self, enable: bool, recovery_only: bool = False) -> None:
+        """Time later validate-many calls with dispatch-bound HIP events: the recovery bracket, and unless
+        recovery_only also the chain/tally kernels and the whole call (HLC_TIMING_ALL / HLC_TIMING_RECOVERY)."""
+        mode = (2 if recovery_only else 1) if enable else 0
+        _ffi.check(self.lib.hlc_ctx_set_kernel_timing(self.ctx, mode))
 
     def take_kernel_time(self):
         """-> (recover_ms, recover_launches, call_ms, calls) since the previous take."""

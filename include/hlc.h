@@ -281,10 +281,14 @@ int hlc_host_threads(void);
 const char* hlc_ctx_last_host_trace(hlc_ctx* ctx);
 
 /* ---- Measurement hooks (bench.py roofline): HIP events on the launch stream ------ */
-/* enable != 0: every validate-many call records hipEvents around the signature-recovery
- * kernels (k_rec_prep and k_rec_main on the context's second stream; k_rec_comb, k_rec_final and
- * k_rec_addr on the launch stream), around the chain/tally kernels and around the whole call, on
- * the streams the kernels run on. */
+/* enable = HLC_TIMING_ALL (1, or any value but 0 and 2): every validate-many call times the signature
+ * recovery (k_rec_prep's start on the context's second stream .. k_rec_addr's end on the launch stream),
+ * the chain/tally kernels and the whole call; HLC_TIMING_RECOVERY (2): the recovery bracket alone.  The
+ * events are bound to the kernels' own dispatches (hipExtLaunchKernelGGL), not recorded between them:
+ * each bound kernel still costs the queue a few microseconds, so the recovery-only mode is the one a
+ * throughput measurement runs under (bench.py). */
+#define HLC_TIMING_ALL 1
+#define HLC_TIMING_RECOVERY 2
 int hlc_ctx_set_kernel_timing(hlc_ctx* ctx, int enable);
 /* Waits for the recorded events, returns the summed device time (ms) and launch count of
  * the recovery and of whole validate-many calls since the previous take, then resets them. */
