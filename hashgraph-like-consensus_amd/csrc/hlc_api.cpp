@@ -507,7 +507,8 @@ struct RecFront {
 // aux_tables != nullptr: the large-proposal chain / duplicate tables' launcher (validate_device); with
 // the early comb it is enqueued on the aux stream behind k_rec_main, where it runs beside the comb
 // instead of on the launch stream's critical path, and *tables_done is set.
-// fork_recorded: validate_device bound c->ev_fork to its last kernel on `s` (no marker needed here).
+// fork_recorded: validate_device bound c->ev_fork to its last kernel on `s` (no marker needed here) and
+// cleared the prep stage's work counters (hlc::recover_counters) in k_red_init.
 using TablesLaunch = std::function<void(hipStream_t, const hlc::KEv*)>;
 int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const hlc_proposal* dprops, uint64_t np,
                uint64_t now, uint8_t* status, uint8_t* reason, uint8_t* drec, uint32_t* red, uint8_t* chain_code,
@@ -606,7 +607,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   const hlc::RecSkip skip{vote_prop, dprops, dv->proposal_id, dv->field_len};
   const hlc::KEv pk{p0, prep_done};
   hlc::launch_recover_prep(n, dv->bytes, dv->field_off + HLC_F_SIGNATURE, HLC_NFIELDS, dv->field_len + HLC_F_SIGNATURE,
-                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux, &skip, nullptr, &pk);
+                           HLC_NFIELDS, c->rec_work.as<uint32_t>(), aux, &skip, nullptr, &pk, fork_recorded);
   unsigned long long* clk = nullptr;
   if (c->clock_probe) {
     CHK(c->clk_buf.ensure((c->rec_lanes / 64) * 32 + 32));
@@ -684,10 +685,17 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
   CHK(c->flag.ensure(16));
   CHK(c->red.ensure(np * 16 + 16));
   // per-proposal reduction records and the call's flag word in one launch, then the vote -> proposal map
-  const hlc::KEv rk{call0, nullptr};
-  hlc::launch_red_init(c->red.as<uint32_t>(), np, s, c->flag.as<uint32_t>(), &rk, c->vote_prop.as<uint32_t>(), n);
-  // the aux stream's fork point: bound to k_assign_props's dispatch on the default recovery path
+  // the default recovery path (prepped): the aux stream's fork point bound to k_assign_props's dispatch,
+  // and the prep stage's two work counters cleared here with the rest
   const bool bind_fork = n && !fronts && !verdicts && !c->opt.serial_stages;
+  unsigned long long* rec_ctr = nullptr;
+  if (bind_fork) {
+    CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
+    rec_ctr = hlc::recover_counters(n, c->rec_work.as<uint32_t>());
+  }
+  const hlc::KEv rk{call0, nullptr};
+  hlc::launch_red_init(c->red.as<uint32_t>(), np, s, c->flag.as<uint32_t>(), &rk, c->vote_prop.as<uint32_t>(), n,
+                       rec_ctr);
   const hlc::KEv ak{nullptr, bind_fork ? c->ev_fork : nullptr};
   HIPCHK(hlc::launch_assign_props(dprops, np, dv->field_len, c->vote_prop.as<uint32_t>(), n, c->flag.as<uint32_t>(), s,
                                   &ak, true));

@@ -122,7 +122,11 @@ struct RecRange {
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s,
                          const RecSkip* skip = nullptr, const RecRange* range = nullptr,
-                         const KEv* ev = nullptr);  // ev: bound to k_rec_prep
+                         const KEv* ev = nullptr,  // ev: bound to k_rec_prep
+                         bool ctr_cleared = false);  // (whole call) recover_counters already zero
+// the whole call's two work counters (grab counter, list length) inside `work`, which a launcher before
+// the prep stage may clear (launch_red_init) so that the prep stage needs no memset of its own
+unsigned long long* recover_counters(uint64_t n, uint32_t* work);
 void launch_recover_main(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          uint32_t* scratch, uint64_t scratch_lanes, uint32_t* work, hipStream_t s, int force_exact = 0,
                          const RecRange* range = nullptr, unsigned long long* clk = nullptr,
@@ -152,7 +156,8 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
 // flag != nullptr: also clears the call's flag word; vote_prop != nullptr: also sets its nv entries to
 // NO_PROP for launch_assign_props(..., map_cleared = true) -- one launch instead of two memsets and a kernel
 void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s, uint32_t* flag = nullptr, const KEv* ev = nullptr,
-                     uint32_t* vote_prop = nullptr, uint64_t nv = 0);
+                     uint32_t* vote_prop = nullptr, uint64_t nv = 0,
+                     unsigned long long* zero2 = nullptr);  // zero2: two words cleared too
 // large-proposal chain / duplicate tables: always enqueued, skipped on the device unless the call's
 // flag word has FLAG_LARGE_PROPOSAL (flags == nullptr: always run)
 // (the duplicate test reports into `red` from k_tables)

@@ -1029,9 +1029,11 @@ __global__ void k_prehash_stream(hlc_votes v, uint64_t n, const uint32_t* vote_p
 // per-proposal reduction records: first bad / chain / duplicate = none, YES = 0
 // (flag != nullptr: the call's flag word is cleared too, before k_assign_props raises its bits;
 // vote_prop != nullptr: its nv entries are set to NO_PROP, the map k_assign_props then fills)
-__global__ void k_red_init(uint32_t* red, uint64_t np, uint32_t* flag, uint32_t* vote_prop, uint64_t nv) {
+__global__ void k_red_init(uint32_t* red, uint64_t np, uint32_t* flag, uint32_t* vote_prop, uint64_t nv,
+                           unsigned long long* zero2) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (flag && p == 0) *flag = 0;
+  if (zero2 && p < 2) zero2[p] = 0;
   if (vote_prop && p < nv) vote_prop[p] = NO_PROP;
   if (p < np) reinterpret_cast<uint4*>(red)[p] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
 }
@@ -1244,11 +1246,12 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
 }
 
 void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s, uint32_t* flag, const KEv* ev, uint32_t* vote_prop,
-                     uint64_t nv) {
+                     uint64_t nv, unsigned long long* zero2) {
   if (!vote_prop) nv = 0;
-  const uint64_t m = std::max(np, nv);
+  const uint64_t m = std::max(std::max(np, nv), zero2 ? (uint64_t)2 : 0);
   if (m) {
-    launch_k(ev, k_red_init, dim3((unsigned)((m + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np, flag, vote_prop, nv);
+    launch_k(ev, k_red_init, dim3((unsigned)((m + TPB - 1) / TPB)), dim3(TPB), 0, s, red, np, flag, vote_prop, nv,
+             zero2);
   } else {
     record_kev(ev, s);
     if (flag) (void)hipMemsetAsync(flag, 0, sizeof(uint32_t), s);

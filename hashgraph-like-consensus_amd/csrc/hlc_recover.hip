@@ -597,14 +597,17 @@ FrontBufs front_bufs(uint64_t n, uint64_t v0, uint64_t m, uint32_t* work, uint32
 }
 }  // namespace
 
+unsigned long long* recover_counters(uint64_t n, uint32_t* work) { return rec_bufs(n, work).ctr; }
+
 void launch_recover_prep(uint64_t n, const uint8_t* bytes, const uint64_t* sig_off, size_t off_stride,
                          const uint32_t* sig_len, size_t len_stride, uint32_t* work, hipStream_t s, const RecSkip* skip,
-                         const RecRange* range, const KEv* ev) {
+                         const RecRange* range, const KEv* ev, bool ctr_cleared) {
   const uint64_t m = range ? range->m : n;
   if (!m) return record_kev(ev, s);
   const FrontBufs f = front_bufs(n, range ? range->v0 : 0, m, work, range ? range->work : nullptr, range);
   const unsigned pb = (unsigned)((f.b.L + PREP_TPB - 1) / PREP_TPB);
-  (void)hipMemsetAsync(f.b.ctr, 0, 2 * sizeof(unsigned long long), s);  // grab counter, list length
+  if (!ctr_cleared || range)
+    (void)hipMemsetAsync(f.b.ctr, 0, 2 * sizeof(unsigned long long), s);  // grab counter, list length
   const RecSkip none{nullptr, nullptr, nullptr, nullptr};
   launch_k(ev, k_rec_prep, dim3(pb), dim3(PREP_TPB), 0, s, m, f.st, f.b.L, bytes, sig_off, off_stride, sig_len,
            len_stride, f.b.rec, f.b.pfx, f.b.mst, f.b.list, f.b.ctr + 1, skip ? *skip : none);
