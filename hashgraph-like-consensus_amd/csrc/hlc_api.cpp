@@ -532,6 +532,8 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   CHK(c->verify.ensure(n));
   CHK(c->kec_dig.ensure(n * 32));
   CHK(ensure_recover_scratch(c));
+  // the vote statuses are written by the finish's last kernel (k_rec_addr), not by a k_vote_status after it
+  const hlc::VoteStatusArgs sa{*dv, vote_prop, dprops, now, c->pre_reason.as<uint8_t>(), status, reason, red};
   // (fronts: the ranges' records are in flight in rec_work, sized by the caller)
   if (!fronts) CHK(c->rec_work.ensure(hlc::recover_work_words(n) * sizeof(uint32_t)));
   // The recovery's prep stage (signature parse, batched r^-1, GLV digits) and main stage (R, its
@@ -590,9 +592,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
                                dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(),
                                c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->opt.rec_force_exact,
-                               rec_stride, early_host);
-    hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
-                            c->verify.as<uint8_t>(), status, reason, red, s);
+                               rec_stride, early_host, nullptr, &sa);
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -640,10 +640,8 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   const hlc::KEv fk{nullptr, r1};
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_OWNER,
                              HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
-                             drec, s, c->opt.rec_force_exact, 0, early, &fk);
+                             drec, s, c->opt.rec_force_exact, 0, early, &fk, &sa);
   if (c->timing) c->rec_ev.emplace_back(p0, r1);
-  hlc::launch_vote_status(dv, n, vote_prop, dprops, now, c->pre.as<uint8_t>(), c->pre_reason.as<uint8_t>(),
-                          c->verify.as<uint8_t>(), status, reason, red, s);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -721,21 +719,34 @@ int validate_device(hlc_ctx* c, const hlc_votes* dv, const hlc_proposal* dprops,
                        c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(),
                        st, ev);
   };
+  // the large proposals' chain check reads no vote status, only the tables: it follows them
+  auto chain_check = [&](hipStream_t st, const hlc::KEv* ev) {
+    hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
+                            c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
+                            c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), st, ev);
+  };
+  // early comb: the tables and the chain check behind k_rec_main on the aux stream (vote_stage), beside
+  // the comb, so that only k_finalize follows the recovery's finish on `s`
+  const TablesLaunch tables_check = [&](hipStream_t st, const hlc::KEv* ev) {
+    const hlc::KEv first = hlc::kev_start(ev), last = hlc::kev_stop(ev);
+    tables(st, &first);
+    chain_check(st, &last);
+  };
   bool tables_done = false;
   // (the small proposals' chain / duplicate / YES kernel runs inside vote_stage, beside the
-  // recovery's main stage: k_vote_status reports each proposal's first failing vote)
+  // recovery's main stage: the finish reports each proposal's first failing vote)
   if (n)
     CHK(vote_stage(c, dv, c->vote_prop.as<uint32_t>(), dprops, np, now, status, reason, drec, c->red.as<uint32_t>(),
-                   c->chain_code.as<uint8_t>(), s, fronts, nfronts, rec_stride, verdicts, &tables, &tables_done,
-                   bind_fork));
+                   c->chain_code.as<uint8_t>(), s, fronts, nfronts, rec_stride, verdicts, &tables_check,
+                   &tables_done, bind_fork));
   // chain check + duplicate detection + tally (+ k_chain_small's and the aux tables' brackets in vote_stage)
-  const hlc::KEv c0{ch0, nullptr}, c1{nullptr, ch1};
-  if (!tables_done) tables(s, &c0);
-  hlc::launch_chain_check(dv, n, c->vote_prop.as<uint32_t>(), dprops, status, c->chain_tab.as<uint32_t>(),
-                          c->dup_tab.as<uint32_t>(), (uint32_t)(cap - 1), c->chain_code.as<uint8_t>(),
-                          c->red.as<uint32_t>(), np, c->flag.as<uint32_t>(), s, tables_done ? &c0 : nullptr);
+  const hlc::KEv c0{ch0, nullptr}, c1{nullptr, ch1}, cf{ch0, ch1};
+  if (!tables_done) {
+    tables(s, &c0);
+    chain_check(s, nullptr);
+  }
   hlc::launch_finalize(dprops, np, now, status, reason, c->chain_code.as<uint8_t>(), c->red.as<uint32_t>(), dres, s,
-                       &c1);
+                       tables_done ? &cf : &c1);
   HIPCHK(hipGetLastError());
   if (c->timing_all()) {
     c->chain_ev.emplace_back(ch0, ch1);

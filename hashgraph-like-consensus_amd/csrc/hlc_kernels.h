@@ -16,6 +16,48 @@ constexpr uint8_t PRE_PENDING = 0xFE;  // needs signature recovery
 constexpr uint8_t PRE_SKIP = 0xFF;     // vote not covered by any proposal
 constexpr uint8_t PRE_GENERAL = 0xFD;  // too long for the fused LDS path: general pipeline decides
 
+// The validate_vote tail of one vote (utils.rs:154-168): its pre-status st, the scheme result vr (the
+// verify byte: HLC_VERIFY_TRUE / FALSE or 1 + SCHEME) when st is PRE_PENDING, then the timestamps; with
+// red != nullptr also the proposal's first failing vote (red[4p + 0], the local index), so that the chain /
+// duplicate / tally kernels need no vote statuses.  k_vote_status runs it over a call's votes; k_rec_addr
+// runs it right after a vote's address compare when the finish is given these arguments (one kernel
+// boundary less on the call's critical path).
+struct VoteStatusArgs {
+  hlc_votes v;
+  const uint32_t* vote_prop;
+  const hlc_proposal* props;
+  uint64_t now;
+  const uint8_t* pre_reason;
+  uint8_t* status;
+  uint8_t* reason;
+  uint32_t* red;
+};
+__device__ inline void vote_status_one(const VoteStatusArgs& a, uint64_t i, uint8_t st, uint8_t vr) {
+  uint8_t rs = a.pre_reason[i];
+  if (st == PRE_PENDING) {
+    const hlc_proposal& p = a.props[a.vote_prop[i]];
+    const uint64_t ts = a.v.timestamp[i];
+    if (vr >= 2) {
+      st = HLC_SIGNATURE_SCHEME;
+      rs = min(vr - 1, HLC_SCHEME_PLUGIN);  // (a caller's verdict above HLC_VERIFY_ERR reads as it)
+    } else if (vr == HLC_VERIFY_FALSE) {
+      st = HLC_INVALID_VOTE_SIGNATURE;
+    } else if (ts < p.timestamp) {
+      st = HLC_TIMESTAMP_OLDER_THAN_CREATION;
+    } else if (ts > p.expiration_timestamp || a.now > p.expiration_timestamp) {
+      st = HLC_VOTE_EXPIRED;
+    } else {
+      st = HLC_OK;
+    }
+  }
+  a.status[i] = st;
+  a.reason[i] = rs;
+  if (a.red && st != HLC_OK) {
+    const uint32_t p = a.vote_prop[i];
+    if (p != NO_PROP) atomicMin(&a.red[4 * p + 0], (uint32_t)(i - a.props[p].vote_begin));
+  }
+}
+
 // message-building modes
 enum MsgMode { MSG_VOTE = 0, MSG_PAYLOAD = 1 };
 
@@ -136,7 +178,8 @@ void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_dig
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact = 0,
                            uint64_t stride = 0,  // stride: the records' row stride (0 = n; the fronts' n)
                            bool early_comb = false,  // u1 G from launch_recover_ucomb: k_rec_add, not k_rec_comb
-                           const KEv* ev = nullptr);  // ev: start at the first kernel, stop at k_rec_addr
+                           const KEv* ev = nullptr,  // ev: start at the first kernel, stop at k_rec_addr
+                           const VoteStatusArgs* sa = nullptr);  // sa: k_rec_addr also writes the vote statuses
 // u1 G alone (k_rec_ucomb) over a whole call's records (row stride n), once the prehash (pre, z_digest)
 // and the prep stage are done; launch_recover_finish(..., early_comb = true) adds u2 R after k_rec_main.
 void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint32_t* gtab,

@@ -268,35 +268,11 @@ __global__ void k_pre_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop,
 // validate_vote tail (utils.rs:154-168): scheme result, then timestamps
 // With red != nullptr also the first failing vote per proposal (red[4p + 0], the local index): the
 // chain / duplicate / tally kernels then need no vote statuses and run beside the recovery.
-__global__ void k_vote_status(hlc_votes v, uint64_t n, const uint32_t* vote_prop, const hlc_proposal* props,
-                              uint64_t now, const uint8_t* pre, const uint8_t* pre_reason,
-                              const uint8_t* verify, uint8_t* status, uint8_t* reason, uint32_t* red) {
+__global__ void k_vote_status(VoteStatusArgs a, uint64_t n, const uint8_t* pre, const uint8_t* verify) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint8_t st = pre[i], rs = pre_reason[i];
-  if (st == PRE_PENDING) {
-    uint8_t vr = verify[i];
-    const hlc_proposal& p = props[vote_prop[i]];
-    uint64_t ts = v.timestamp[i];
-    if (vr >= 2) {
-      st = HLC_SIGNATURE_SCHEME;
-      rs = min(vr - 1, HLC_SCHEME_PLUGIN);  // (a caller's verdict above HLC_VERIFY_ERR reads as it)
-    } else if (vr == HLC_VERIFY_FALSE) {
-      st = HLC_INVALID_VOTE_SIGNATURE;
-    } else if (ts < p.timestamp) {
-      st = HLC_TIMESTAMP_OLDER_THAN_CREATION;
-    } else if (ts > p.expiration_timestamp || now > p.expiration_timestamp) {
-      st = HLC_VOTE_EXPIRED;
-    } else {
-      st = HLC_OK;
-    }
-  }
-  status[i] = st;
-  reason[i] = rs;
-  if (red && st != HLC_OK) {
-    const uint32_t p = vote_prop[i];
-    if (p != NO_PROP) atomicMin(&red[4 * p + 0], (uint32_t)(i - props[p].vote_begin));
-  }
+  const uint8_t st = pre[i];
+  vote_status_one(a, i, st, st == PRE_PENDING ? verify[i] : 0);
 }
 
 // ---------------- chain / duplicate tables ----------------
@@ -1241,8 +1217,8 @@ void launch_vote_status(const hlc_votes* v, uint64_t n, const uint32_t* vote_pro
                         uint64_t now, const uint8_t* pre, const uint8_t* pre_reason, const uint8_t* verify,
                         uint8_t* status, uint8_t* reason, uint32_t* red, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_vote_status, dim3(blocks_for(n)), dim3(TPB), 0, s, *v, n, vote_prop, props, now, pre,
-                       pre_reason, verify, status, reason, red);
+    hipLaunchKernelGGL(k_vote_status, dim3(blocks_for(n)), dim3(TPB), 0, s,
+                       VoteStatusArgs{*v, vote_prop, props, now, pre_reason, status, reason, red}, n, pre, verify);
 }
 
 void launch_red_init(uint32_t* red, uint64_t np, hipStream_t s, uint32_t* flag, const KEv* ev, uint32_t* vote_prop,

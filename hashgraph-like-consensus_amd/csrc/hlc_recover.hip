@@ -302,6 +302,10 @@ __global__ void __launch_bounds__(256, HLC_COMB_MIN_WAVES) k_rec_ucomb(uint64_t 
 }
 
 // ---- after k_rec_main and k_rec_ucomb: Q = u2 R + u1 G, the same states as k_rec_comb ----
+// (Measured and not kept, round 6: k_rec_ucomb forming Q itself for the votes whose u2 R k_rec_main had
+// published -- a release of the vote's mst byte after its stores, an acquire in the comb -- left k_rec_add
+// 7 us of work but ran the step 1.4% slower, 103.6 vs 105.1 M votes/s; the comb starts after k_rec_main's
+// last wave anyway, behind k_chain_small on the launch stream (profiles/r06g/ab_uadd.txt, uadd_timeline.txt).)
 __global__ void __launch_bounds__(256) k_rec_add(uint64_t n, uint64_t st, const uint8_t* pre, uint8_t* state,
                                                  uint32_t* q, const uint32_t* g, const uint8_t* mst) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -404,11 +408,24 @@ __global__ void __launch_bounds__(PREP_TPB) k_rec_final(uint64_t n, uint64_t st,
   }
 }
 
+// STATUS: also the vote's validate_vote tail (vote_status_one) for every vote of the call, recovered or not
+// (k_vote_status's work, without its launch after this one)
+template <bool STATUS>
 __global__ void __launch_bounds__(256) k_rec_addr(uint64_t n, uint64_t st, const uint8_t* pre, const uint8_t* bytes,
                                                   const uint64_t* id_off, size_t off_stride, uint8_t* state,
-                                                  const uint32_t* q, uint8_t* addr_out) {
+                                                  const uint32_t* q, uint8_t* addr_out, VoteStatusArgs sa) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || (pre && pre[i] != PRE_PENDING) || state[i] != REC_PENDING) return;
+  if (i >= n) return;
+  const uint8_t ps = pre ? pre[i] : PRE_PENDING;
+  if (ps != PRE_PENDING) {
+    if (STATUS) vote_status_one(sa, i, ps, 0);
+    return;
+  }
+  const uint8_t s0 = state[i];
+  if (s0 != REC_PENDING) {
+    if (STATUS) vote_status_one(sa, i, ps, s0);
+    return;
+  }
   fe x, y;
   load_fe_ws(x, q + i, st);
   load_fe_ws(y, q + (size_t)8 * st + i, st);
@@ -418,7 +435,9 @@ __global__ void __launch_bounds__(256) k_rec_addr(uint64_t n, uint64_t st, const
   uint32_t diff = 0;
 #pragma unroll
   for (int w = 0; w < 5; ++w) diff |= addr[w] ^ load_le32(id + 4 * w);
-  state[i] = diff == 0 ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
+  const uint8_t vr = diff == 0 ? HLC_VERIFY_TRUE : HLC_VERIFY_FALSE;
+  state[i] = vr;
+  if (STATUS) vote_status_one(sa, i, ps, vr);
   if (addr_out) {
 #pragma unroll
     for (int w = 0; w < 5; ++w) {
@@ -640,7 +659,7 @@ void launch_recover_ucomb(uint64_t n, const uint8_t* pre, const uint32_t* z_dige
 void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_digest, const uint8_t* bytes,
                            const uint64_t* id_off, size_t off_stride, const uint32_t* gcomb, uint32_t* work,
                            uint8_t* verify_out, uint8_t* addr_out, hipStream_t s, int force_exact, uint64_t stride,
-                           bool early_comb, const KEv* ev) {
+                           bool early_comb, const KEv* ev, const VoteStatusArgs* sa) {
   if (!n) return record_kev(ev, s);
   const uint64_t st = stride ? stride : n;  // the records' row stride (>= n)
   const RecBufs b = rec_bufs(st, work);
@@ -654,8 +673,12 @@ void launch_recover_finish(uint64_t n, const uint8_t* pre, const uint32_t* z_dig
     launch_k(&first, k_rec_comb, dim3(vb), dim3(256), 0, s, n, st, pre, z_digest, gcomb, verify_out, b.rec, b.q, b.mst,
              force_exact);
   hipLaunchKernelGGL(k_rec_final, dim3(fb), dim3(PREP_TPB), 0, s, n, st, Lf, pre, verify_out, b.q, b.pfx);
-  launch_k(&last, k_rec_addr, dim3(vb), dim3(256), 0, s, n, st, pre, bytes, id_off, off_stride, verify_out, b.q,
-           addr_out);
+  if (sa)
+    launch_k(&last, k_rec_addr<true>, dim3(vb), dim3(256), 0, s, n, st, pre, bytes, id_off, off_stride, verify_out, b.q,
+             addr_out, *sa);
+  else
+    launch_k(&last, k_rec_addr<false>, dim3(vb), dim3(256), 0, s, n, st, pre, bytes, id_off, off_stride, verify_out,
+             b.q, addr_out, VoteStatusArgs{});
 }
 
 
