@@ -1021,8 +1021,8 @@ def write_detail(out: dict, path: str):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, choices=[2, 4], default=None,
                     help="2: 10,000 x 64 votes per GPU (default at N=1); 4: this rank's 1/8 shard of the "
                          "100M-vote config 4, 195,313 x 64 votes (default at N>1)")

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -317,6 +318,48 @@ Options read_env() {
   return o;
 }
 
+// The fixed-base tables: the signing comb (32 x 256 affine points, 512 KiB) and the recovery's u1 G comb
+// it is built from (hlc_recover.hpp: 11 windows x 2^23 affine points of 64 B = 5.9 GB at W = 24).  Both are
+// read-only once built, so there is one pair per device per process, shared by every context on that
+// device and freed with the last of them: a second context costs no table memory and no build.
+struct GenTables {
+  int device = -1;
+  void* fb = nullptr;
+  void* g = nullptr;
+  ~GenTables() {
+    if (!fb && !g) return;
+    (void)hipSetDevice(device);
+    if (fb) (void)hipFree(fb);
+    if (g) (void)hipFree(g);
+  }
+};
+std::mutex g_gen_mu;
+std::map<int, std::weak_ptr<GenTables>>* g_gen = new std::map<int, std::weak_ptr<GenTables>>();  // (never freed:
+                                                   // contexts destroyed by static destructors still find it)
+
+// The device's tables (built on `s` and synchronised on first use; the caller has set `device`).
+int gen_tables(int device, hipStream_t s, std::shared_ptr<GenTables>& out) {
+  std::lock_guard<std::mutex> lk(g_gen_mu);
+  if ((out = (*g_gen)[device].lock())) return 0;
+  auto t = std::make_shared<GenTables>();
+  t->device = device;
+  const size_t gbytes = hlc::gcomb_words() * sizeof(uint32_t);
+  hipError_t e = hipMalloc(&t->fb, hlc::FBTAB_WORDS * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&t->g, gbytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(HLC_ENOMEM, "fixed-base table allocation (" + std::to_string(gbytes >> 20) +
+                                   " MiB u1 G comb) failed: " + hipGetErrorString(e));
+  }
+  hlc::launch_build_fbtab(reinterpret_cast<uint32_t*>(t->fb), s);
+  hlc::launch_build_gcomb(reinterpret_cast<uint32_t*>(t->g), reinterpret_cast<const uint32_t*>(t->fb), s);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return set_err(HLC_EDEVICE, "generator table construction failed");
+  (*g_gen)[device] = t;
+  out = std::move(t);
+  return 0;
+}
+
 }  // namespace
 
 struct hlc_ctx {
@@ -326,7 +369,10 @@ struct hlc_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // caller stream -> aux -> caller stream
   hipEvent_t ev_prep = nullptr;  // aux: the recovery's prep stage done (HLC_OPT_EARLY_COMB)
   std::mutex mu;
-  DBuf gtab, fbtab, rec_scratch, rec_work;
+  std::shared_ptr<GenTables> gen;  // the device's fixed-base tables (gen_tables), shared with its other contexts
+  const uint32_t* gtab = nullptr;  // the u1 G comb (gen->g)
+  const uint32_t* fbtab = nullptr; // the signing comb (gen->fb)
+  DBuf rec_scratch, rec_work;
   uint64_t rec_lanes = 0;
   Options opt;  // hlc_ctx_set_option; defaults from the environment at creation (read_env)
   // hlc_validate_proposals (host buffers): a second recovery slot (stream, per-lane scratch, per-vote
@@ -473,12 +519,7 @@ int ensure_recover_scratch(hlc_ctx* c) {
 }
 
 int ensure_fbtab(hlc_ctx* c) {
-  if (c->fbtab.p) return 0;
-  CHK(c->fbtab.ensure(hlc::FBTAB_WORDS * sizeof(uint32_t)));
-  hlc::launch_build_fbtab(c->fbtab.as<uint32_t>(), c->stream);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  return c->fbtab ? 0 : set_err(HLC_EINVAL, "context without its fixed-base tables");  // (built at creation)
 }
 
 // A recovery range whose front half (k_rec_prep + k_rec_main over votes [v0, v1), records in the
@@ -558,7 +599,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   const hipEvent_t prep_done = early ? c->ev_prep : nullptr;
   auto launch_ucomb = [&]() -> int {
     HIPCHK(hipStreamWaitEvent(s, prep_done, 0));
-    hlc::launch_recover_ucomb(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), c->gtab.as<uint32_t>(),
+    hlc::launch_recover_ucomb(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), c->gtab,
                               c->rec_work.as<uint32_t>(), s, c->opt.rec_force_exact);
     return 0;
   };
@@ -585,12 +626,12 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
     const bool early_host = (c->opt.early_comb & 2) != 0;
     if (early_host) {
       for (int k = 0; k < nfronts; ++k) HIPCHK(hipStreamWaitEvent(s, fronts[k].prep, 0));
-      hlc::launch_recover_ucomb(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), c->gtab.as<uint32_t>(),
+      hlc::launch_recover_ucomb(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), c->gtab,
                                 c->rec_work.as<uint32_t>(), s, c->opt.rec_force_exact, rec_stride);
     }
     for (int k = 0; k < nfronts; ++k) HIPCHK(hipStreamWaitEvent(s, fronts[k].done, 0));
     hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes,
-                               dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab.as<uint32_t>(),
+                               dv->field_off + HLC_F_OWNER, HLC_NFIELDS, c->gtab,
                                c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(), drec, s, c->opt.rec_force_exact,
                                rec_stride, early_host, nullptr, &sa);
     HIPCHK(hipGetLastError());
@@ -639,7 +680,7 @@ int vote_stage(hlc_ctx* c, const hlc_votes* dv, const uint32_t* vote_prop, const
   }
   const hlc::KEv fk{nullptr, r1};
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dv->bytes, dv->field_off + HLC_F_OWNER,
-                             HLC_NFIELDS, c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
+                             HLC_NFIELDS, c->gtab, c->rec_work.as<uint32_t>(), c->verify.as<uint8_t>(),
                              drec, s, c->opt.rec_force_exact, 0, early, &fk, &sa);
   if (c->timing) c->rec_ev.emplace_back(p0, r1);
   HIPCHK(hipGetLastError());
@@ -1593,7 +1634,7 @@ int verify_host(hlc_ctx* c, uint64_t n, const uint8_t* bytes, uint64_t bytes_len
   if (daddr) HIPCHK(hipMemsetAsync(daddr, 0, n * 20, s));
   for (const RecFront& f : fronts) HIPCHK(hipStreamWaitEvent(s, f.done, 0));
   hlc::launch_recover_finish(n, c->pre.as<uint8_t>(), c->kec_dig.as<uint32_t>(), dbytes, did_off, 1,
-                             c->gtab.as<uint32_t>(), c->rec_work.as<uint32_t>(), dstat, daddr, s, c->opt.rec_force_exact);
+                             c->gtab, c->rec_work.as<uint32_t>(), dstat, daddr, s, c->opt.rec_force_exact);
   HIPCHK(hipGetLastError());
   tr.ev("kernels_end", s);
   HIPCHK(hipMemcpyAsync(c->pin_out.p, ob, r2, hipMemcpyDeviceToHost, s));
@@ -2145,26 +2186,16 @@ int hlc_ctx_create(int device, hlc_ctx** out) {
     delete c;
     return set_err(HLC_EDEVICE, "stream creation failed");
   }
-  // fixed-base tables, built once per context: the signing comb (32 x 256 points, 512 KiB) and the
-  // recovery's u1 G comb (12 windows x 2^21 affine points of 64 B = 1.5 GiB of HBM, hlc.h)
-  if (c->fbtab.ensure(hlc::FBTAB_WORDS * sizeof(uint32_t)) != 0 ||
-      c->gtab.ensure(hlc::gcomb_words() * sizeof(uint32_t)) != 0) {
-    const std::string why = g_err;
-    hipStream_t st = c->stream, ax = c->aux;
-    delete c;  // frees whichever table was allocated and the events
-    (void)hipStreamDestroy(st);
-    (void)hipStreamDestroy(ax);
-    return set_err(HLC_ENOMEM, "fixed-base table allocation (1.5 GiB u1 G comb) failed: " + why);
-  }
-  hlc::launch_build_fbtab(c->fbtab.as<uint32_t>(), c->stream);
-  hlc::launch_build_gcomb(c->gtab.as<uint32_t>(), c->fbtab.as<uint32_t>(), c->stream);
-  if (hipStreamSynchronize(c->stream) != hipSuccess) {
+  // the fixed-base tables: built by the first context on this device, shared by the others (gen_tables)
+  if (const int rc = gen_tables(device, c->stream, c->gen)) {
     hipStream_t st = c->stream, ax = c->aux;
     delete c;
     (void)hipStreamDestroy(st);
     (void)hipStreamDestroy(ax);
-    return set_err(HLC_EDEVICE, "generator table construction failed");
+    return rc;
   }
+  c->gtab = reinterpret_cast<const uint32_t*>(c->gen->g);
+  c->fbtab = reinterpret_cast<const uint32_t*>(c->gen->fb);
   *out = c;
   return 0;
 }
@@ -2751,7 +2782,7 @@ int hlc_synth_votes_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_proposal,
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
   CHK(ensure_fbtab(ctx));
   hlc::launch_synth(seed, start_proposal, n_proposals, votes_per_proposal, expected_voters, gossipsub, out_votes,
-                    out_proposals, out_priv, ctx->fbtab.as<uint32_t>(), s);
+                    out_proposals, out_priv, ctx->fbtab, s);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -2772,7 +2803,7 @@ int hlc_synth_byzantine_device(hlc_ctx* ctx, uint64_t seed, uint64_t start_propo
   CHK(ensure_fbtab(ctx));
   CHK(ctx->byz_key.ensure(n * 8 + 8));
   hlc::launch_synth_byzantine(seed, start_proposal, n_proposals, votes_per_proposal, votes, out_kind,
-                              ctx->byz_key.as<uint64_t>(), ctx->fbtab.as<uint32_t>(), s);
+                              ctx->byz_key.as<uint64_t>(), ctx->fbtab, s);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -2786,7 +2817,7 @@ int hlc_eth_address_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, uint8
   CHK(ensure_fbtab(ctx));
   CHK(upload(ctx->in_priv, priv32, n * 32, s));
   CHK(ctx->out_rec.ensure(n * 20 + 20));
-  hlc::launch_address(n, ctx->in_priv.as<uint8_t>(), ctx->fbtab.as<uint32_t>(), ctx->out_rec.as<uint8_t>(), s);
+  hlc::launch_address(n, ctx->in_priv.as<uint8_t>(), ctx->fbtab, ctx->out_rec.as<uint8_t>(), s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_addr20, ctx->out_rec.p, n * 20, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -2811,7 +2842,7 @@ int hlc_eth_sign_batch(hlc_ctx* ctx, uint64_t n, const uint8_t* priv32, const ui
   CHK(run_prehash(ctx, nullptr, n, hlc::MSG_PAYLOAD, ctx->in_bytes.as<uint8_t>(), ctx->in_off2.as<uint64_t>(),
                   ctx->in_len2.as<uint32_t>(), s));
   CHK(ctx->out_misc.ensure(n * 65 + 65));
-  hlc::launch_sign(n, ctx->in_priv.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), ctx->fbtab.as<uint32_t>(),
+  hlc::launch_sign(n, ctx->in_priv.as<uint8_t>(), ctx->kec_dig.as<uint32_t>(), ctx->fbtab,
                    ctx->out_misc.as<uint8_t>(), s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_sig65, ctx->out_misc.p, n * 65, hipMemcpyDeviceToHost, s));

@@ -33,7 +33,7 @@
 //       and brought to one common Z ("effective affine", as libsecp256k1's
 //       ge_table_set_globalz), so every chain addition is one mixed Jacobian+affine add.
 //   u1 G: a fixed-base comb with NO doublings over a table resident in HBM: GC_WINDOWS windows of
-//       GC_W bits (12 x 22), T[w][j] = (2j+1) 2^(W w) G (affine), regular signed digits of the odd
+//       GC_W bits (11 x 24), T[w][j] = (2j+1) 2^(W w) G (affine), regular signed digits of the odd
 //       representative of u1 (u1 or n - u1, the sign folded into the digits); the recoding's
 //       top digit is provably 1, so the last window is the constant start point 2^(W windows) G.
 //       GC_WINDOWS mixed additions, each table entry prefetched one window ahead.
@@ -90,12 +90,16 @@ constexpr int Q_WORDS = 24;                     // main -> final: Jacobian X, Y,
 constexpr int REC_BATCH = HLC_REC_BATCH;        // votes per lane (one inversion) in prep / final
 constexpr uint8_t REC_PENDING = 0xFF;           // verify_out state between the stages
 
-// fixed-base comb for u1 G (global memory, built once per context by k_build_gcomb).  Wider
-// windows mean fewer additions per vote and a larger table: W = 22 -> 12 additions over
-// 12 x 2^21 affine points (1.5 GiB in HBM, out of the Infinity Cache; every entry is prefetched
-// one window ahead, so the gather latency hides behind an addition).
+// fixed-base comb for u1 G (global memory, built by k_build_gcomb once per device and process and
+// shared by its contexts, hlc_api.cpp gen_tables).  Wider windows mean fewer additions per vote and a
+// larger table: W = 24 -> 11 additions over 11 x 2^23 affine points (5.9 GB of the 288 GB HBM, out of
+// the Infinity Cache; every entry is prefetched one window ahead, so the gather latency hides behind
+// an addition).  W = 22 (12 additions, 1.5 GiB) shipped through round 6; with the comb in its own
+// kernel after the u2 R stage, 24 measured +0.6% and 26 (10 additions, 21.5 GB) +0.6% on one box,
+// three rounds each (profiles/r06g/ab_gc.txt).  W = 24 keeps 2^(W windows) = 2^264, so the comb's
+// exceptional additions stay unreachable (tests/crypto_items.py comb_collisions_possible).
 #ifndef HLC_GC_W
-#define HLC_GC_W 22
+#define HLC_GC_W 24
 #endif
 constexpr int GC_W = HLC_GC_W;                  // bits per window
 constexpr int GC_WINDOWS = (255 + GC_W - 1) / GC_W;  // W * windows >= 255: the recoding's top is 1

@@ -200,10 +200,11 @@ typedef struct hlc_ctx hlc_ctx;
 
 /* ---- Context -------------------------------------------------------------------- */
 /* Creates a context on HIP device `device` (process-global lazily-initialised device
- * state is what the static `Signer::verify` of signing.rs:69 needs).  Every context allocates
- * and builds its fixed-base tables (~40 ms): the u1 G comb of the recovery, 12 x 2^21 affine
- * points = 1.5 GiB of HBM, and the 512 KiB signing comb; HLC_ENOMEM (with hlc_last_error) when
- * they do not fit.  The recovery's per-lane workspace (~205 MB: one R table of 16 x 64 B plus the
+ * state is what the static `Signer::verify` of signing.rs:69 needs).  The fixed-base tables -- the
+ * u1 G comb of the recovery, 11 x 2^23 affine points = 5.9 GB of HBM, and the 512 KiB signing
+ * comb -- are read-only, so there is one pair per device per process: the first context on a device
+ * allocates and builds them (~0.1-0.25 s), later contexts on it share them (~1 ms), and the last one
+ * destroyed frees them; HLC_ENOMEM (with hlc_last_error) when they do not fit.  The recovery's per-lane workspace (~205 MB: one R table of 16 x 64 B plus the
  * z-ratios per lane of the persistent grid) and the per-vote workspace (~0.5 KB per vote of the
  * largest batch) are allocated on first use (or hlc_ctx_reserve).
  * The host-buffer entries (hlc_validate_proposals, hlc_eth_verify_batch) add on their first call:

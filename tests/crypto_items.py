@@ -53,7 +53,7 @@ def _kg(k: int):
     return po.point_mul(k, po.G)
 
 
-COMB_W = 22                                  # HLC_GC_W of the default build (hlc_recover.hpp)
+COMB_W = 24                                  # HLC_GC_W of the default build (hlc_recover.hpp)
 COMB_N = (255 + COMB_W - 1) // COMB_W        # windows; the top value is 1 at 2^(W N)
 
 
@@ -63,7 +63,7 @@ def comb_collisions_possible(w: int = COMB_W) -> bool:
     to equal +- d_j 2^(W j) (even, < 2^(W (j+1)) << n).  As integers that needs
     (2^(W N) mod n) + L_j = d_j 2^(W j): odd + odd = even only when 2^(W N) mod n is odd.  For
     W = 16 (2^256 mod n, odd) collisions are constructible (`_comb_collision_sig`); for the
-    shipped W = 22 (2^264 mod n, even) none exists, u1 = 0 aside (k = n: unreachable, it needs
+    shipped W = 24 (11 windows: 2^264 mod n, even; so was W = 22 through round 6) none exists, u1 = 0 aside (k = n: unreachable, it needs
     a prehash == 0 mod n)."""
     n_win = (255 + w - 1) // w
     return pow(2, w * n_win, po.N) & 1 == 1

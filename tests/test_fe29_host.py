@@ -443,12 +443,13 @@ def test_coz_addition_at_limb_bounds(checked):
 
 def test_comb_collision_parity_argument():
     """tests/crypto_items.comb_collisions_possible: with 16-bit windows (2^256 mod n odd) the
-    crafted construction exists and its windows really collide; with the shipped 22-bit windows
-    (2^264 mod n even) it cannot (the parity argument in its docstring)."""
+    crafted construction exists and its windows really collide; with the shipped 24-bit windows
+    (11 of them: 2^264 mod n even, as the 22-bit windows of rounds 1-6) it cannot (the parity
+    argument in its docstring)."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import crypto_items as ci
-    assert ci.COMB_W == 22 and not ci.comb_collisions_possible(22)
+    assert ci.COMB_W == 24 and not ci.comb_collisions_possible(24) and not ci.comb_collisions_possible(22)
     assert ci.comb_collisions_possible(16)
 
 
