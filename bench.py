@@ -75,10 +75,15 @@ def _pmc_rows(name: str):
         return list(csv.DictReader(f))
 
 
+def _is_kernel(name: str, kernel: str) -> bool:
+    """Whether a trace row's Kernel_Name is `kernel` (a template instance such as k_rec_addr<true> too)."""
+    return f"::{kernel}(" in name or f"::{kernel}<" in name
+
+
 def pmc_per_launch(name: str, counter: str, kernel: str):
     """Average per launch of `counter` for `kernel` in the committed PMC pass `name`, or None."""
     vals = [float(r["Counter_Value"]) for r in _pmc_rows(name)
-            if f"::{kernel}(" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if _is_kernel(r["Kernel_Name"], kernel) and r["Counter_Name"] == counter]
     return sum(vals) / len(vals) if vals else None
 
 
@@ -86,7 +91,7 @@ def pmc_duration_ms(name: str, kernel: str):
     """Average duration of `kernel` during the PMC pass `name` (its own dispatch timestamps)."""
     seen, durs = set(), []
     for r in _pmc_rows(name):
-        if f"::{kernel}(" in r["Kernel_Name"] and r["Dispatch_Id"] not in seen:
+        if _is_kernel(r["Kernel_Name"], kernel) and r["Dispatch_Id"] not in seen:
             seen.add(r["Dispatch_Id"])
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     return sum(durs) / len(durs) if durs else None
@@ -232,7 +237,7 @@ def rocprof_kernel_ms():
     rows = []
     with open(path, newline="") as f:
         for r in csv.DictReader(f):
-            m = re.search(r"::(k_\w+)\(", r["Kernel_Name"])
+            m = re.search(r"::(k_\w+)[(<]", r["Kernel_Name"])
             if m:
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1)))
     rows.sort()
@@ -283,7 +288,7 @@ def chain_counters(trace_dir: str, fetch_dir: str, write_dir: str):
             return list(csv.DictReader(f))
 
     def kname(r):
-        m = re.search(r"::(k_\w+)\(", r["Kernel_Name"])
+        m = re.search(r"::(k_\w+)[(<]", r["Kernel_Name"])
         return m.group(1) if m else None
 
     tr = rows(trace_dir, "run_kernel_trace.csv")

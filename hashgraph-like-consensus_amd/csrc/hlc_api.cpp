@@ -328,9 +328,12 @@ struct GenTables {
   void* g = nullptr;
   ~GenTables() {
     if (!fb && !g) return;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
     (void)hipSetDevice(device);
     if (fb) (void)hipFree(fb);
     if (g) (void)hipFree(g);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);  // the caller's current device, unchanged
   }
 };
 std::mutex g_gen_mu;

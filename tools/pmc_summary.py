@@ -9,7 +9,7 @@ import sys
 
 
 def kernel_short(name: str) -> str:
-    m = re.search(r"::(k_\w+)\(", name)
+    m = re.search(r"::(k_\w+)[(<]", name)
     return m.group(1) if m else name.split("(")[0][-40:]
 
 

@@ -23,7 +23,7 @@ CHAIN_EARLY = ("k_rec_prep", "k_rec_main", "k_rec_ucomb", "k_rec_add", "k_rec_fi
 
 
 def short(name: str) -> str:
-    m = re.search(r"::(k_\w+)\(", name)
+    m = re.search(r"::(k_\w+)[(<]", name)
     return m.group(1) if m else name[:40]
 
 
