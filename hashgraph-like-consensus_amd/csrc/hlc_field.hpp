@@ -10,14 +10,15 @@
 //    product scanning, 64 MACs per 256x256 product, 36 per square;
 //  * mod p: pseudo-Mersenne fold 2^256 == 2^32 + 977 (two folds, one conditional subtract);
 //    all field values are kept fully reduced (< p) so equality tests are limb compares;
-//  * mod n: Montgomery multiplication (CIOS, R = 2^256), used for the few scalar ops
-//    per vote (r^-1, u1, u2, GLV split products).
+//  * mod n: Montgomery multiplication (R = 2^256) over 29-bit limbs (hlc_scmul.hpp; 8 x 32 CIOS
+//    through round 6), used for the few scalar ops per vote (r^-1, u1, u2, GLV split products).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "hlc_field_asm.hpp"
 #include "hlc_modinv.hpp"
+#include "hlc_scmul.hpp"
 
 #define HLC_DEV __device__ __forceinline__
 
@@ -301,6 +302,13 @@ HLC_DEV bool fe_sqrt(fe& r, const fe& a) {
 static constexpr uint32_t N0INV = 0x5588B13Fu;  // -n^-1 mod 2^32
 
 // r = a*b*R^-1 mod n   (CIOS; inputs < n, output < n)
+#ifndef HLC_SC_CIOS
+#define HLC_SC_CIOS 0  // 1: the A/B arm with the 8 x 32 CIOS form below (through round 6)
+#endif
+#if !HLC_SC_CIOS
+// a b 2^-256 mod n by 29-bit limbs (hlc_scmul.hpp): the same result as the CIOS form, ~2.3x fewer instructions
+HLC_DEV void sc_mont_mul(fe& r, const fe& a, const fe& b) { sc_mont_mul29(r.v, a.v, b.v); }
+#else
 HLC_DEV void sc_mont_mul(fe& r, const fe& a, const fe& b) {
   uint32_t t[10];
 #pragma unroll
@@ -338,6 +346,7 @@ HLC_DEV void sc_mont_mul(fe& r, const fe& a, const fe& b) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = use_d ? d[i] : t[i];
 }
+#endif
 
 // r = x mod n for any 256-bit x (n > 2^255 so one conditional subtract suffices)
 HLC_DEV void sc_reduce(fe& r, const fe& x) {

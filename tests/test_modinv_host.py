@@ -35,3 +35,40 @@ def test_safegcd_inverse_mod_p_and_n():
         got = _run(vals, which)
         bad = [v for v, r in zip(vals, got) if r != pow(v, -1, m)]
         assert not bad, f"modulus {which}: {len(bad)} wrong inverses, e.g. {hex(bad[0])}"
+
+
+def _mont_ref(a: int, b: int) -> int:
+    """What the 8 x 32 CIOS form returned (and hlc_scmul.hpp must): t = (a b + M n) / 2^256,
+    M = -a b n^-1 mod 2^256, then t - n when t >= n (one conditional subtract, any a, b < 2^256)."""
+    R = 1 << 256
+    m = (-a * b * pow(N, -1, R)) % R
+    t = (a * b + m * N) >> 256
+    return t - N if t >= N else t
+
+
+def test_sc_mont_mul29_matches_the_cios_form():
+    """csrc/hlc_scmul.hpp sc_mont_mul29 (the recovery's products mod n since round 6) against the
+    Montgomery product it replaced, bit for bit: random scalars, the edges of [0, n) and inputs
+    >= n up to 2^256 - 1 (the form is defined for any 256-bit operands)."""
+    lib = ctypes.CDLL(LIB)
+    lib.hlc_sc_mont_mul_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    rnd = random.Random(29)
+    edge = [0, 1, 2, N - 1, N - 2, N, N + 1, 2**256 - 1, 2**255, 2**232 - 1, 2**232, (N - 1) // 2,
+            2**29 - 1, 2**261 % N, 2**256 % N]
+    pairs = [(x, y) for x in edge for y in edge]
+    pairs += [(rnd.randrange(N), rnd.randrange(N)) for _ in range(20000)]
+    pairs += [(rnd.randrange(2**256), rnd.randrange(2**256)) for _ in range(5000)]
+    pairs += [(rnd.randrange(N), (1 << rnd.randrange(256)) - 1) for _ in range(2000)]
+
+    def words(vals):
+        arr = np.zeros((len(vals), 8), np.uint32)
+        for i, v in enumerate(vals):
+            for k in range(8):
+                arr[i, k] = (v >> (32 * k)) & 0xFFFFFFFF
+        return arr
+    a, b = words([p[0] for p in pairs]), words([p[1] for p in pairs])
+    out = np.zeros_like(a)
+    lib.hlc_sc_mont_mul_host(a.ctypes.data, b.ctypes.data, out.ctypes.data, len(pairs))
+    got = [sum(int(out[i, k]) << (32 * k) for k in range(8)) for i in range(len(pairs))]
+    bad = [(hex(x), hex(y)) for (x, y), g in zip(pairs, got) if g != _mont_ref(x, y)]
+    assert not bad, f"{len(bad)} wrong products, e.g. {bad[0]}"
