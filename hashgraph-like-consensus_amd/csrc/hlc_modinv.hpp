@@ -204,6 +204,9 @@ HLC_HD void normalize_30(s30& r, int32_t sign, const modinfo30& mi) {
   }
 }
 
+#ifndef HLC_MODINV_EARLY_EXIT
+#define HLC_MODINV_EARLY_EXIT 1  // 0: the A/B arm that always runs the 20 batches
+#endif
 // out = a^-1 mod modulus (a in [0, modulus), 8 x 32-bit limbs); a == 0 gives 0.
 HLC_HD void modinv_safegcd(uint32_t out[8], const uint32_t a[8], const modinfo30& mi) {
   s30 d = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
@@ -213,6 +216,16 @@ HLC_HD void modinv_safegcd(uint32_t out[8], const uint32_t a[8], const modinfo30
   to_s30(g, a);
   int32_t zeta = -1;
   for (int i = 0; i < 20; ++i) {
+    // Once g == 0 every further batch is [[2^30, 0], [0, 1]]: d and f stay as they are (only e changes),
+    // so the loop may stop.  Random 256-bit inputs reach g == 0 after 17 or 18 batches (every 64-lane
+    // group of 128k random inputs mod p and mod n needs 18, tools/modinv_batches.cpp), so the test
+    // starts at batch 17: a wave then runs 18 batches instead of 20, with the same result.
+    if (HLC_MODINV_EARLY_EXIT && i >= 17) {
+      int32_t gz = 0;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) gz |= g.v[k];
+      if (gz == 0) break;
+    }
     trans2x2 t;
     zeta = divsteps_30(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
     update_de_30(d, e, t, mi);
